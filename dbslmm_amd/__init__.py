@@ -1,0 +1,198 @@
+"""dbslmm_amd -- MI355X-native per-LD-block effect-size solver of DBSLMM.
+
+Python front-end over the C-ABI library ``libdbslmm_hip.so`` (include/dbslmm_hip.h).  The
+entry points mirror the reference operator interface (fboehm/DBSLMM, scr/dbslmmfit.hpp):
+
+* ``DBSLMMFIT.est(...)``  -- DBSLMMFIT::est, both overloads (dbslmmfit.hpp:38-66): large +
+  small effects, or LMM-only when no large SNPs are given.
+* ``Plan``                -- the same problem kept resident in HBM for repeated solves.
+* ``bed_maf``             -- the MAF pass of IO::readBim (dtpr.cpp:93-102).
+* ``read_snp_std``        -- IO::readSNPIm + SNPPROC::nomalizeVec for a list of rows.
+
+All compute runs on the GPU through the HIP library; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import (BLOCK_EMPTY, BLOCK_MONOMORPHIC, BLOCK_NOT_PD, BLOCK_OK, KERNEL_NAMES,
+                   DbslmmError)
+
+__all__ = ["Context", "Plan", "DBSLMMFIT", "BlockProblem", "bed_maf", "read_snp_std",
+           "DbslmmError", "BLOCK_OK", "BLOCK_EMPTY", "BLOCK_NOT_PD", "BLOCK_MONOMORPHIC",
+           "KERNEL_NAMES"]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One HIP device (dbslmm_ctx_create)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        rc = self.lib.dbslmm_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            raise DbslmmError(f"dbslmm_ctx_create(device={device}) failed rc={rc}")
+        self.h = h
+        self.device = device
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.dbslmm_last_error(self.h).decode(errors="replace")
+            raise DbslmmError(f"{what} failed rc={rc}: {msg}")
+
+    def close(self):
+        if self.h:
+            self.lib.dbslmm_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class BlockProblem:
+    """Flat form of DBSLMMFIT::est's arguments (see include/dbslmm_hip.h dbslmm_problem)."""
+    bed: np.ndarray            # uint8 .bed image incl. magic
+    n_ref: int
+    n_obs: int
+    sigma_s: float
+    s_ptr: np.ndarray          # int64 [num_block+1]
+    s_pos: np.ndarray          # int32 bed rows
+    z_s: np.ndarray            # float64
+    l_ptr: np.ndarray | None = None
+    l_pos: np.ndarray | None = None
+    z_l: np.ndarray | None = None
+    tau: float = 0.8
+
+    def __post_init__(self):
+        self.bed = np.ascontiguousarray(self.bed, dtype=np.uint8)
+        self.s_ptr = np.ascontiguousarray(self.s_ptr, dtype=np.int64)
+        self.s_pos = np.ascontiguousarray(self.s_pos, dtype=np.int32)
+        self.z_s = np.ascontiguousarray(self.z_s, dtype=np.float64)
+        if self.l_ptr is not None:
+            self.l_ptr = np.ascontiguousarray(self.l_ptr, dtype=np.int64)
+            self.l_pos = np.ascontiguousarray(self.l_pos, dtype=np.int32)
+            self.z_l = np.ascontiguousarray(self.z_l, dtype=np.float64)
+        nb = len(self.s_ptr) - 1
+        if self.l_ptr is not None and len(self.l_ptr) != nb + 1:
+            raise ValueError("s_ptr and l_ptr must have the same number of blocks")
+
+    @property
+    def num_block(self) -> int:
+        return len(self.s_ptr) - 1
+
+    @property
+    def n_s(self) -> int:
+        return int(self.s_ptr[-1])
+
+    @property
+    def n_l(self) -> int:
+        return 0 if self.l_ptr is None else int(self.l_ptr[-1])
+
+    def c_struct(self) -> _lib.Problem:
+        return _lib.Problem(
+            _ptr(self.bed), self.bed.size, self.n_ref, self.n_obs, self.sigma_s, self.tau,
+            self.num_block, _ptr(self.s_ptr), _ptr(self.s_pos), _ptr(self.z_s),
+            _ptr(self.l_ptr), _ptr(self.l_pos), _ptr(self.z_l))
+
+
+class Plan:
+    """A BlockProblem resident in HBM (dbslmm_plan_*)."""
+
+    def __init__(self, ctx: Context, prob: BlockProblem):
+        self.ctx, self.prob = ctx, prob
+        self._cs = prob.c_struct()          # keep the struct (and arrays) alive
+        h = C.c_void_p()
+        ctx.check(ctx.lib.dbslmm_plan_create(ctx.h, C.byref(self._cs), C.byref(h)), "plan_create")
+        self.h = h
+
+    def run(self):
+        self.ctx.check(self.ctx.lib.dbslmm_plan_run(self.h), "plan_run")
+
+    def sync(self):
+        self.ctx.check(self.ctx.lib.dbslmm_plan_sync(self.h), "plan_sync")
+
+    def set_sigma(self, sigma_s: float):
+        self.ctx.check(self.ctx.lib.dbslmm_plan_set_sigma(self.h, float(sigma_s)), "plan_set_sigma")
+
+    def enable_timing(self, on: bool = True):
+        self.ctx.check(self.ctx.lib.dbslmm_plan_enable_timing(self.h, int(on)), "plan_enable_timing")
+
+    def kernel_ms(self):
+        out = np.zeros(3)
+        n = np.zeros(1, dtype=np.int32)
+        self.ctx.check(self.ctx.lib.dbslmm_plan_kernel_ms(self.h, _ptr(out), _ptr(n)), "plan_kernel_ms")
+        return out, int(n[0])
+
+    def workload(self) -> dict:
+        w = np.zeros(8)
+        self.ctx.check(self.ctx.lib.dbslmm_plan_workload(self.h, _ptr(w)), "plan_workload")
+        keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
+                "gram_ops_exec", "chol_flops", "blocks", "gram_tiles")
+        return dict(zip(keys, w.tolist()))
+
+    def download(self):
+        p = self.prob
+        bs = np.zeros(p.n_s)
+        bl = np.zeros(p.n_l)
+        st = np.zeros(p.num_block, dtype=np.int32)
+        self.ctx.check(self.ctx.lib.dbslmm_plan_download(self.h, _ptr(bs), _ptr(bl), _ptr(st)),
+                       "plan_download")
+        return bs, bl, st
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.dbslmm_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DBSLMMFIT:
+    """Mirror of the reference's DBSLMMFIT::est (scr/dbslmmfit.hpp:35-66) on one GPU."""
+
+    def __init__(self, device: int = 0):
+        self.ctx = Context(device)
+
+    def est(self, prob: BlockProblem):
+        """Return (beta_s, beta_l, block_status).  LMM-only when prob.l_ptr is None."""
+        bs = np.zeros(prob.n_s)
+        bl = np.zeros(prob.n_l)
+        st = np.zeros(prob.num_block, dtype=np.int32)
+        cs = prob.c_struct()
+        self.ctx.check(self.ctx.lib.dbslmm_est(self.ctx.h, C.byref(cs), _ptr(bs), _ptr(bl), _ptr(st)),
+                       "dbslmm_est")
+        return bs, bl, st
+
+
+def bed_maf(ctx: Context, bed: np.ndarray, n_ref: int, n_snp: int) -> np.ndarray:
+    bed = np.ascontiguousarray(bed, dtype=np.uint8)
+    maf = np.zeros(n_snp)
+    ctx.check(ctx.lib.dbslmm_bed_maf(ctx.h, _ptr(bed), bed.size, n_ref, n_snp, _ptr(maf)), "bed_maf")
+    return maf
+
+
+def read_snp_std(ctx: Context, bed: np.ndarray, n_ref: int, rows) -> tuple[np.ndarray, np.ndarray]:
+    """Standardised genotype columns (n_ref x len(rows), Fortran order) and MAFs."""
+    bed = np.ascontiguousarray(bed, dtype=np.uint8)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    out = np.zeros(n_ref * len(rows))
+    maf = np.zeros(len(rows))
+    ctx.check(ctx.lib.dbslmm_read_snp_std(ctx.h, _ptr(bed), bed.size, n_ref, _ptr(rows), len(rows),
+                                          _ptr(out), _ptr(maf)), "read_snp_std")
+    return out.reshape(len(rows), n_ref).T, maf

@@ -1,0 +1,77 @@
+"""ctypes binding of libdbslmm_hip.so (the C-ABI declared in include/dbslmm_hip.h).
+
+The product path has no CPU fallback: if the in-tree HIP library is missing or no GPU is
+present, every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdbslmm_hip.so")
+
+# symbols include/dbslmm_hip.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "dbslmm_abi_version", "dbslmm_ctx_create", "dbslmm_ctx_destroy", "dbslmm_last_error",
+    "dbslmm_est", "dbslmm_plan_create", "dbslmm_plan_run", "dbslmm_plan_sync",
+    "dbslmm_plan_download", "dbslmm_plan_set_sigma", "dbslmm_plan_destroy",
+    "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
+    "dbslmm_bed_maf", "dbslmm_read_snp_std",
+)
+
+K_UNPACK, K_GRAM, K_CHOL = 0, 1, 2
+KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_solve")
+BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC = 0, 1, 2, 3
+
+
+class Problem(C.Structure):
+    _fields_ = [
+        ("bed", C.c_void_p), ("bed_len", C.c_int64), ("n_ref", C.c_int32), ("n_obs", C.c_int32),
+        ("sigma_s", C.c_double), ("tau", C.c_double), ("num_block", C.c_int32),
+        ("s_ptr", C.c_void_p), ("s_pos", C.c_void_p), ("z_s", C.c_void_p),
+        ("l_ptr", C.c_void_p), ("l_pos", C.c_void_p), ("z_l", C.c_void_p),
+    ]
+
+
+_lib = None
+
+
+class DbslmmError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load the in-tree HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise DbslmmError(f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (or `make -C dbslmm_amd/csrc`)")
+    L = C.CDLL(p)
+    V, P = C.c_void_p, C.POINTER
+    L.dbslmm_abi_version.restype = C.c_int
+    L.dbslmm_ctx_create.argtypes = [C.c_int, P(V)]
+    L.dbslmm_ctx_destroy.argtypes = [V]
+    L.dbslmm_ctx_destroy.restype = None
+    L.dbslmm_last_error.argtypes = [V]
+    L.dbslmm_last_error.restype = C.c_char_p
+    L.dbslmm_est.argtypes = [V, P(Problem), V, V, V]
+    L.dbslmm_plan_create.argtypes = [V, P(Problem), P(V)]
+    L.dbslmm_plan_run.argtypes = [V]
+    L.dbslmm_plan_sync.argtypes = [V]
+    L.dbslmm_plan_download.argtypes = [V, V, V, V]
+    L.dbslmm_plan_set_sigma.argtypes = [V, C.c_double]
+    L.dbslmm_plan_destroy.argtypes = [V]
+    L.dbslmm_plan_destroy.restype = None
+    L.dbslmm_plan_enable_timing.argtypes = [V, C.c_int]
+    L.dbslmm_plan_kernel_ms.argtypes = [V, V, V]
+    L.dbslmm_plan_workload.argtypes = [V, V]
+    L.dbslmm_bed_maf.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int64, V]
+    L.dbslmm_read_snp_std.argtypes = [V, V, C.c_int64, C.c_int32, V, C.c_int32, V, V]
+    if L.dbslmm_abi_version() != 1:
+        raise DbslmmError("ABI version mismatch")
+    _lib = L
+    return L

@@ -1,0 +1,508 @@
+// plan.hip -- host side of libdbslmm_hip.so: contexts, plans (HBM layout + work lists),
+// launches and the extern "C" entry points declared in include/dbslmm_hip.h.
+//
+// HBM layout of a plan (one context = one GPU):
+//   bed       the .bed image as-is (3 magic bytes kept, rows at 3 + r*ceil(n/4)), +16 B pad
+//   slots     non-empty blocks, in block order, each padded to a multiple of 32 slots:
+//             [small SNPs | large SNPs | padding]; per slot: bed row (-1 = pad), block,
+//             z-score, output index (>= 0 small, -1-i large)
+//   G         int8 [n_slots][kpad] dosages, kpad = roundup(n_ref, 64)
+//   M         fp64 per block ld x ld row-major (ld = padded block size), lower triangle
+//   stats     S, mu, 1/sd per slot; y (solve scratch) per slot; flags/status per block
+// The whole problem stays resident; plan_run re-executes unpack -> gram -> chol from the
+// packed genotypes (nothing cached between runs except the uploaded inputs).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/dbslmm_hip.h"
+
+// The kernels are compiled in this translation unit (no relocatable device code needed).
+#include "kernels.hip"
+
+namespace {
+constexpr size_t kCholLdsSmall = sizeof(double) * (2 + kTile * kLdsStride + 8 * kTile);
+constexpr size_t kCholLdsBig = kCholLdsSmall + sizeof(double) * (4 * 2 * kTile * kLdsStride);
+
+int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+}  // namespace
+
+struct dbslmm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+};
+
+struct dbslmm_plan {
+    dbslmm_ctx* ctx = nullptr;
+    int32_t n_ref = 0, n_obs = 0, num_block = 0;
+    double sigma_s = 0.0, tau = 0.8;
+    int64_t n_s = 0, n_l = 0, bytes_per_snp = 0, kpad = 0, bed_len = 0;
+    int32_t n_slots = 0, n_nonempty = 0, n_tiles = 0;
+    int64_t M_elems = 0;
+    // device
+    uint8_t* d_bed = nullptr;
+    int8_t* d_G = nullptr;
+    int32_t *d_slot_pos = nullptr, *d_slot_block = nullptr, *d_slot_out = nullptr;
+    double *d_z = nullptr, *d_S = nullptr, *d_mu = nullptr, *d_rsd = nullptr, *d_y = nullptr;
+    int32_t *d_flags = nullptr, *d_status = nullptr, *d_order = nullptr, *d_blk_id = nullptr;
+    int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
+    int64_t* d_matoff = nullptr;
+    GramTile* d_tiles = nullptr;
+    double* d_M = nullptr;
+    double *d_beta_s = nullptr, *d_beta_l = nullptr;
+    std::vector<int32_t> h_ld;  // per non-empty block
+    std::vector<int32_t> h_empty;  // original ids of empty blocks
+    // workload figures
+    double wl[8] = {0};
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;  // 4 per run
+    int runs_pending = 0;
+    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0};
+    int32_t ms_runs = 0;
+    bool ran = false;
+};
+
+#define HIP_TRY(ctx, expr)                                                               \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+            return DBSLMM_E_HIP;                                                         \
+        }                                                                                \
+    } while (0)
+
+#define ARG_CHECK(ctx, cond, msg)                   \
+    do {                                            \
+        if (!(cond)) {                              \
+            (ctx)->err = msg;                       \
+            return DBSLMM_E_ARG;                    \
+        }                                           \
+    } while (0)
+
+template <typename T>
+static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
+    size_t bytes = std::max<size_t>(sizeof(T), src.size() * sizeof(T));
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(dst), bytes);
+    if (e != hipSuccess) return e;
+    if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
+extern "C" {
+
+int dbslmm_abi_version(void) { return DBSLMM_ABI_VERSION; }
+
+int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
+    if (!out) return DBSLMM_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DBSLMM_E_HIP;
+    if (device < 0 || device >= n) return DBSLMM_E_ARG;
+    auto* c = new dbslmm_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return DBSLMM_E_HIP;
+    }
+    *out = c;
+    return DBSLMM_OK;
+}
+
+void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* dbslmm_last_error(const dbslmm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void dbslmm_plan_destroy(dbslmm_plan* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->ctx->device);
+    void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
+                    p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
+                    p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
+                    p->d_M, p->d_beta_s, p->d_beta_l};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+    delete p;
+}
+
+int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out) {
+    if (!ctx) return DBSLMM_E_ARG;
+    ARG_CHECK(ctx, pr && out, "null problem/out");
+    *out = nullptr;
+    ARG_CHECK(ctx, pr->bed && pr->n_ref > 1 && pr->n_obs > 0 && pr->num_block >= 0, "bad sizes");
+    ARG_CHECK(ctx, pr->s_ptr && (pr->s_ptr[pr->num_block] == 0 || (pr->s_pos && pr->z_s)), "bad small CSR");
+    ARG_CHECK(ctx, pr->sigma_s > 0.0 && std::isfinite(pr->sigma_s), "sigma_s must be > 0");
+    const int64_t bps = pr->n_ref / 4 + (pr->n_ref % 4 ? 1 : 0);
+    const int64_t n_snp_bed = (pr->bed_len - 3) / bps;
+    ARG_CHECK(ctx, pr->bed_len >= 3 + bps, "bed image shorter than one SNP row");
+    const bool has_l = pr->l_ptr != nullptr;
+    if (has_l) ARG_CHECK(ctx, pr->l_ptr[pr->num_block] == 0 || (pr->l_pos && pr->z_l), "bad large CSR");
+
+    auto* p = new dbslmm_plan();
+    p->ctx = ctx;
+    p->n_ref = pr->n_ref;
+    p->n_obs = pr->n_obs;
+    p->num_block = pr->num_block;
+    p->sigma_s = pr->sigma_s;
+    p->tau = pr->tau;
+    p->bytes_per_snp = bps;
+    p->kpad = round_up(pr->n_ref, 64);
+    p->bed_len = pr->bed_len;
+    p->n_s = pr->s_ptr[pr->num_block];
+    p->n_l = has_l ? pr->l_ptr[pr->num_block] : 0;
+
+    // ---- host-side layout
+    std::vector<int32_t> slot_pos, slot_block, slot_out, row0, mv, msv, ldv, blk_id;
+    std::vector<double> z;
+    std::vector<int64_t> matoff;
+    std::vector<GramTile> tiles;
+    int64_t moff = 0;
+    double ops_alg = 0, ops_exec = 0, chol_flops = 0;
+    for (int b = 0; b < pr->num_block; ++b) {
+        const int64_t s0 = pr->s_ptr[b], ms = pr->s_ptr[b + 1] - s0;
+        const int64_t l0 = has_l ? pr->l_ptr[b] : 0, ml = has_l ? pr->l_ptr[b + 1] - l0 : 0;
+        if (ms < 0 || ml < 0) { ctx->err = "CSR offsets not monotone"; dbslmm_plan_destroy(p); return DBSLMM_E_ARG; }
+        const int64_t m = ms + ml;
+        if (m == 0) { p->h_empty.push_back(b); continue; }
+        const int nb = static_cast<int>(row0.size());
+        const int64_t ld = round_up(m, kTile);
+        row0.push_back(static_cast<int32_t>(slot_pos.size()));
+        mv.push_back(static_cast<int32_t>(m));
+        msv.push_back(static_cast<int32_t>(ms));
+        ldv.push_back(static_cast<int32_t>(ld));
+        blk_id.push_back(b);
+        matoff.push_back(moff);
+        moff += ld * ld;
+        for (int64_t i = 0; i < ms; ++i) {
+            const int32_t r = pr->s_pos[s0 + i];
+            if (r < 0 || r >= n_snp_bed) { ctx->err = "small SNP bed row out of range"; dbslmm_plan_destroy(p); return DBSLMM_E_ARG; }
+            slot_pos.push_back(r);
+            slot_block.push_back(nb);
+            slot_out.push_back(static_cast<int32_t>(s0 + i));
+            z.push_back(pr->z_s[s0 + i]);
+        }
+        for (int64_t i = 0; i < ml; ++i) {
+            const int32_t r = pr->l_pos[l0 + i];
+            if (r < 0 || r >= n_snp_bed) { ctx->err = "large SNP bed row out of range"; dbslmm_plan_destroy(p); return DBSLMM_E_ARG; }
+            slot_pos.push_back(r);
+            slot_block.push_back(nb);
+            slot_out.push_back(static_cast<int32_t>(-1 - (l0 + i)));
+            z.push_back(pr->z_l[l0 + i]);
+        }
+        for (int64_t i = m; i < ld; ++i) {
+            slot_pos.push_back(-1);
+            slot_block.push_back(nb);
+            slot_out.push_back(INT32_MIN);
+            z.push_back(0.0);
+        }
+        const int T = static_cast<int>(ld / kTile);
+        for (int ti = 0; ti < T; ++ti)
+            for (int tj = 0; tj <= ti; ++tj) tiles.push_back({nb, ti, tj, 0});
+        ops_alg += static_cast<double>(pr->n_ref) * m * (m + 1);
+        ops_exec += 2.0 * p->kpad * kTile * kTile * (T * (T + 1) / 2);
+        chol_flops += m * static_cast<double>(m) * m / 3.0 + 2.0 * m * m;
+    }
+    p->n_nonempty = static_cast<int32_t>(row0.size());
+    p->n_slots = static_cast<int32_t>(slot_pos.size());
+    p->n_tiles = static_cast<int32_t>(tiles.size());
+    p->M_elems = moff;
+    p->h_ld = ldv;
+    // largest blocks first for the Cholesky launch (longest-processing-time order)
+    std::vector<int32_t> order(p->n_nonempty);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return mv[a] > mv[c]; });
+    const double n_snp = static_cast<double>(p->n_s + p->n_l);
+    p->wl[0] = n_snp;
+    p->wl[1] = n_snp * bps;
+    p->wl[2] = static_cast<double>(p->n_slots) * p->kpad;
+    p->wl[3] = ops_alg;
+    p->wl[4] = ops_exec;
+    p->wl[5] = chol_flops;
+    p->wl[6] = p->n_nonempty;
+    p->wl[7] = p->n_tiles;
+
+    // ---- device allocations
+    hipError_t e = hipSetDevice(ctx->device);
+    auto fail = [&](const char* what) {
+        ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+        dbslmm_plan_destroy(p);
+        return DBSLMM_E_HIP;
+    };
+    if (e != hipSuccess) return fail("hipSetDevice");
+    if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
+    if ((e = hipMemset(p->d_bed, 0, pr->bed_len + 16)) != hipSuccess) return fail("hipMemset bed");
+    if ((e = hipMemcpy(p->d_bed, pr->bed, pr->bed_len, hipMemcpyHostToDevice)) != hipSuccess) return fail("upload bed");
+    const int64_t g_bytes = std::max<int64_t>(64, static_cast<int64_t>(p->n_slots) * p->kpad);
+    if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
+    if ((e = dev_upload(&p->d_slot_pos, slot_pos)) != hipSuccess) return fail("upload slots");
+    if ((e = dev_upload(&p->d_slot_block, slot_block)) != hipSuccess) return fail("upload slots");
+    if ((e = dev_upload(&p->d_slot_out, slot_out)) != hipSuccess) return fail("upload slots");
+    if ((e = dev_upload(&p->d_z, z)) != hipSuccess) return fail("upload z");
+    if ((e = dev_upload(&p->d_row0, row0)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_m, mv)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_ms, msv)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_ld, ldv)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_matoff, matoff)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_blk_id, blk_id)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_order, order)) != hipSuccess) return fail("upload order");
+    if ((e = dev_upload(&p->d_tiles, tiles)) != hipSuccess) return fail("upload tiles");
+    const size_t ns = std::max<size_t>(1, p->n_slots);
+    if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
+    if ((e = hipMalloc(&p->d_mu, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
+    if ((e = hipMalloc(&p->d_rsd, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
+    if ((e = hipMalloc(&p->d_y, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc y");
+    const size_t nbk = std::max<int32_t>(1, std::max(p->n_nonempty, p->num_block));
+    if ((e = hipMalloc(&p->d_flags, nbk * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc flags");
+    if ((e = hipMalloc(&p->d_status, nbk * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc status");
+    if ((e = hipMalloc(&p->d_M, std::max<int64_t>(1, p->M_elems) * sizeof(double))) != hipSuccess) return fail("hipMalloc M");
+    if ((e = hipMemset(p->d_M, 0, std::max<int64_t>(1, p->M_elems) * sizeof(double))) != hipSuccess) return fail("hipMemset M");
+    if ((e = hipMalloc(&p->d_beta_s, std::max<int64_t>(1, p->n_s) * sizeof(double))) != hipSuccess) return fail("hipMalloc beta");
+    if ((e = hipMalloc(&p->d_beta_l, std::max<int64_t>(1, p->n_l) * sizeof(double))) != hipSuccess) return fail("hipMalloc beta");
+    *out = p;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_set_sigma(dbslmm_plan* p, double sigma_s) {
+    if (!p) return DBSLMM_E_ARG;
+    ARG_CHECK(p->ctx, sigma_s > 0.0 && std::isfinite(sigma_s), "sigma_s must be > 0");
+    p->sigma_s = sigma_s;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_enable_timing(dbslmm_plan* p, int enable) {
+    if (!p) return DBSLMM_E_ARG;
+    p->timing = enable != 0;
+    p->ms_acc[0] = p->ms_acc[1] = p->ms_acc[2] = 0.0;
+    p->ms_runs = 0;
+    return DBSLMM_OK;
+}
+
+static int collect_timing(dbslmm_plan* p) {
+    dbslmm_ctx* ctx = p->ctx;
+    for (int r = 0; r < p->runs_pending; ++r) {
+        hipEvent_t* e = &p->ev[4 * r];
+        for (int k = 0; k < DBSLMM_K_COUNT; ++k) {
+            float ms = 0.f;
+            HIP_TRY(ctx, hipEventElapsedTime(&ms, e[k], e[k + 1]));
+            p->ms_acc[k] += ms;
+        }
+        p->ms_runs++;
+    }
+    p->runs_pending = 0;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_run(dbslmm_plan* p) {
+    if (!p) return DBSLMM_E_ARG;
+    dbslmm_ctx* ctx = p->ctx;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    hipEvent_t* ev = nullptr;
+    if (p->timing) {
+        const size_t need = 4 * static_cast<size_t>(p->runs_pending + 1);
+        while (p->ev.size() < need) {
+            hipEvent_t e;
+            HIP_TRY(ctx, hipEventCreate(&e));
+            p->ev.push_back(e);
+        }
+        ev = &p->ev[4 * p->runs_pending];
+        p->runs_pending++;
+    }
+    const size_t nbk = std::max<int32_t>(1, std::max(p->n_nonempty, p->num_block));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, nbk * sizeof(int32_t), s));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], s));
+    if (p->n_slots > 0) {
+        const int wpb = 4;
+        dim3 grid((p->n_slots + wpb - 1) / wpb);
+        hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, s, p->d_bed, p->n_ref,
+                           p->bytes_per_snp, p->d_slot_pos, p->d_slot_block, p->n_slots, p->d_G,
+                           p->kpad, p->d_S, p->d_mu, p->d_rsd, nullptr, p->d_flags);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], s));
+    if (p->n_tiles > 0) {
+        dim3 grid((p->n_tiles + 3) / 4);
+        hipLaunchKernelGGL(dbslmm_gram_i8, grid, dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
+                           p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
+                           p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
+                           static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
+    if (p->n_nonempty > 0) {
+        const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
+        const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
+        hipLaunchKernelGGL(dbslmm_chol_solve, dim3(p->n_nonempty), dim3(256), kCholLdsBig, s, p->d_M,
+                           p->d_order, p->n_nonempty, p->d_row0, p->d_m, p->d_ms, p->d_ld,
+                           p->d_matoff, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn, p->d_y,
+                           p->d_beta_s, p->d_beta_l, p->d_status, p->d_blk_id);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
+    p->ran = true;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_sync(dbslmm_plan* p) {
+    if (!p) return DBSLMM_E_ARG;
+    HIP_TRY(p->ctx, hipSetDevice(p->ctx->device));
+    HIP_TRY(p->ctx, hipStreamSynchronize(p->ctx->stream));
+    if (p->timing) return collect_timing(p);
+    p->runs_pending = 0;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_kernel_ms(dbslmm_plan* p, double* ms_out, int32_t* launches_out) {
+    if (!p || !ms_out) return DBSLMM_E_ARG;
+    for (int k = 0; k < DBSLMM_K_COUNT; ++k) ms_out[k] = p->ms_runs ? p->ms_acc[k] / p->ms_runs : 0.0;
+    if (launches_out) *launches_out = p->ms_runs;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
+    if (!p || !out) return DBSLMM_E_ARG;
+    for (int i = 0; i < 8; ++i) out[i] = p->wl[i];
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_download(dbslmm_plan* p, double* beta_s, double* beta_l, int32_t* block_status) {
+    if (!p) return DBSLMM_E_ARG;
+    dbslmm_ctx* ctx = p->ctx;
+    if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (beta_s && p->n_s)
+        HIP_TRY(ctx, hipMemcpy(beta_s, p->d_beta_s, p->n_s * sizeof(double), hipMemcpyDeviceToHost));
+    if (beta_l && p->n_l)
+        HIP_TRY(ctx, hipMemcpy(beta_l, p->d_beta_l, p->n_l * sizeof(double), hipMemcpyDeviceToHost));
+    if (block_status && p->num_block) {
+        HIP_TRY(ctx, hipMemcpy(block_status, p->d_status, p->num_block * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int32_t b : p->h_empty) block_status[b] = DBSLMM_BLOCK_EMPTY;
+    }
+    return DBSLMM_OK;
+}
+
+int dbslmm_est(dbslmm_ctx* ctx, const dbslmm_problem* pr, double* beta_s, double* beta_l,
+               int32_t* block_status) {
+    if (!ctx) return DBSLMM_E_ARG;
+    dbslmm_plan* p = nullptr;
+    int rc = dbslmm_plan_create(ctx, pr, &p);
+    if (rc) return rc;
+    rc = dbslmm_plan_run(p);
+    if (!rc) rc = dbslmm_plan_sync(p);
+    if (!rc) rc = dbslmm_plan_download(p, beta_s, beta_l, block_status);
+    dbslmm_plan_destroy(p);
+    return rc;
+}
+
+// MAF pass over the first n_snp rows (IO::readBim, dtpr.cpp:93-102).
+int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
+                   int64_t n_snp, double* maf) {
+    if (!ctx) return DBSLMM_E_ARG;
+    ARG_CHECK(ctx, bed && maf && n_ref > 1 && n_snp >= 0 && n_snp < INT32_MAX, "bad arguments");
+    const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
+    ARG_CHECK(ctx, bed_len >= 3 + n_snp * bps, "bed image shorter than n_snp rows");
+    if (n_snp == 0) return DBSLMM_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint8_t* d_bed = nullptr;
+    int32_t* d_pos = nullptr;
+    double* d_maf = nullptr;
+    std::vector<int32_t> pos(n_snp);
+    std::iota(pos.begin(), pos.end(), 0);
+    int rc = DBSLMM_OK;
+    do {
+        hipError_t e;
+        if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
+            (e = hipMemset(d_bed, 0, bed_len + 16)) != hipSuccess ||
+            (e = hipMemcpy(d_bed, bed, bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = dev_upload(&d_pos, pos)) != hipSuccess ||
+            (e = hipMalloc(&d_maf, n_snp * sizeof(double))) != hipSuccess) {
+            ctx->err = std::string("bed_maf alloc/upload: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+            break;
+        }
+        dim3 grid(static_cast<unsigned>((n_snp + 3) / 4));
+        hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, ctx->stream, d_bed, n_ref, bps,
+                           d_pos, d_pos, static_cast<int32_t>(n_snp), nullptr, round_up(n_ref, 64),
+                           nullptr, nullptr, nullptr, d_maf, nullptr);
+        if ((e = hipGetLastError()) != hipSuccess ||
+            (e = hipStreamSynchronize(ctx->stream)) != hipSuccess ||
+            (e = hipMemcpy(maf, d_maf, n_snp * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) {
+            ctx->err = std::string("bed_maf run: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+        }
+    } while (0);
+    (void)hipFree(d_bed);
+    (void)hipFree(d_pos);
+    (void)hipFree(d_maf);
+    return rc;
+}
+
+int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
+                        const int32_t* pos, int32_t n_rows, double* out, double* maf) {
+    if (!ctx) return DBSLMM_E_ARG;
+    ARG_CHECK(ctx, bed && pos && out && n_ref > 1 && n_rows >= 0, "bad arguments");
+    const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
+    for (int32_t j = 0; j < n_rows; ++j)
+        ARG_CHECK(ctx, pos[j] >= 0 && 3 + (pos[j] + 1) * bps <= bed_len, "row out of range");
+    if (n_rows == 0) return DBSLMM_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint8_t* d_bed = nullptr;
+    int32_t* d_pos = nullptr;
+    double *d_mu = nullptr, *d_rsd = nullptr, *d_maf = nullptr, *d_out = nullptr;
+    std::vector<int32_t> hp(pos, pos + n_rows);
+    const int64_t n_out = static_cast<int64_t>(n_rows) * n_ref;
+    int rc = DBSLMM_OK;
+    do {
+        hipError_t e;
+        if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
+            (e = hipMemset(d_bed, 0, bed_len + 16)) != hipSuccess ||
+            (e = hipMemcpy(d_bed, bed, bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = dev_upload(&d_pos, hp)) != hipSuccess ||
+            (e = hipMalloc(&d_mu, n_rows * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_rsd, n_rows * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_maf, n_rows * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_out, n_out * sizeof(double))) != hipSuccess) {
+            ctx->err = std::string("read_snp_std alloc/upload: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+            break;
+        }
+        hipLaunchKernelGGL(dbslmm_unpack_stats, dim3((n_rows + 3) / 4), dim3(256), 0, ctx->stream,
+                           d_bed, n_ref, bps, d_pos, d_pos, n_rows, nullptr, round_up(n_ref, 64),
+                           nullptr, d_mu, d_rsd, d_maf, nullptr);
+        hipLaunchKernelGGL(dbslmm_std_columns, dim3(static_cast<unsigned>((n_out + 255) / 256)),
+                           dim3(256), 0, ctx->stream, d_bed, n_ref, bps, d_pos, n_rows, d_mu, d_rsd,
+                           d_out);
+        if ((e = hipGetLastError()) != hipSuccess ||
+            (e = hipStreamSynchronize(ctx->stream)) != hipSuccess ||
+            (e = hipMemcpy(out, d_out, n_out * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess ||
+            (maf && (e = hipMemcpy(maf, d_maf, n_rows * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)) {
+            ctx->err = std::string("read_snp_std run: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+        }
+    } while (0);
+    (void)hipFree(d_bed);
+    (void)hipFree(d_pos);
+    (void)hipFree(d_mu);
+    (void)hipFree(d_rsd);
+    (void)hipFree(d_maf);
+    (void)hipFree(d_out);
+    return rc;
+}
+
+}  // extern "C"

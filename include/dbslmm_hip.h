@@ -1,0 +1,140 @@
+/*
+ * dbslmm_hip.h -- C-ABI of the MI355X (gfx950) per-LD-block effect-size solver.
+ *
+ * Drop-in boundary for the hot path of fboehm/DBSLMM.  Every entry point below replaces one
+ * reference interface (paths relative to the reference's scr/):
+ *
+ *   dbslmm_est            DBSLMMFIT::est (large+small, dbslmmfit.hpp:38-53, dbslmmfit.cpp:56-244)
+ *                         and DBSLMMFIT::est (small only, dbslmmfit.hpp:55-66, :247-363):
+ *                         l_ptr == NULL selects the LMM-only overload.  Called where
+ *                         DBSLMM::BatchRun calls est (dbslmm.cpp:334-348, 375-386).
+ *   dbslmm_plan_*         the same call split into upload / run / download so the solve can be
+ *                         repeated with inputs resident in HBM (bench, h2f tuning).
+ *   dbslmm_bed_maf        the MAF pass of IO::readBim (dtpr.cpp:93-102) = readSNPIm over every
+ *                         reference SNP, maf only.
+ *   dbslmm_read_snp_std   IO::readSNPIm + SNPPROC::nomalizeVec (dtpr.cpp:285-364, 375-380) for a
+ *                         list of bed rows: standardised fp64 columns (parity / diagnostics).
+ *
+ * Conventions: plain pointers and sizes, no C++ types, no exceptions across the boundary.
+ * Every call returns 0 on success or a negative DBSLMM_E* code; dbslmm_last_error(ctx) then
+ * holds a message.  The caller owns every buffer; inputs are read-only for the call.  One call
+ * at a time per context; distinct contexts are independent (one context drives one GPU).
+ */
+#ifndef DBSLMM_HIP_H_
+#define DBSLMM_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DBSLMM_ABI_VERSION 1
+
+enum {
+    DBSLMM_OK = 0,
+    DBSLMM_E_ARG = -1,      /* invalid argument (sizes, NULL, ranges) */
+    DBSLMM_E_HIP = -2,      /* HIP runtime error (no device, OOM, launch failure) */
+    DBSLMM_E_STATE = -3     /* call sequence error (plan not run, ...) */
+};
+
+/* Per-block status written by dbslmm_est / dbslmm_plan_download. */
+enum {
+    DBSLMM_BLOCK_OK = 0,
+    DBSLMM_BLOCK_EMPTY = 1,        /* no SNP in this block */
+    DBSLMM_BLOCK_NOT_PD = 2,       /* joint LD matrix not positive definite -> beta = NaN
+                                      (reference: PCG "Matrix is Singular!", dbslmmfit.cpp:664) */
+    DBSLMM_BLOCK_MONOMORPHIC = 3   /* a SNP with zero variance -> NaN column in the reference
+                                      (dtpr.cpp:375-380); beta = NaN for the whole block */
+};
+
+typedef struct dbslmm_ctx dbslmm_ctx;
+typedef struct dbslmm_plan dbslmm_plan;
+
+/* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.
+ *
+ * bed       the whole PLINK .bed image INCLUDING its 3 magic bytes (host memory); row r of
+ *           SNP-major data starts at byte 3 + r*ceil(n_ref/4) (dtpr.cpp:302).
+ * n_ref     individuals in the reference .fam (getRow, dbslmm.cpp:232).
+ * n_obs     GWAS sample size (-n).
+ * sigma_s   h / nsnp (dbslmm.cpp:332).
+ * tau       LD shrinkage; the reference hard-codes 0.8 (dbslmmfit.cpp:697,751).
+ * num_block number of LD blocks (addBlock's return, dtpr.cpp:455-481).
+ * s_ptr     num_block+1 offsets; small SNPs of block b are s_pos[s_ptr[b]..s_ptr[b+1]) (bed
+ *           rows, INFO::pos) with z-scores z_s[...] (INFO::z); order = the reference's
+ *           info_s order.
+ * l_ptr     same for large SNPs, or NULL for the LMM-only path.
+ */
+typedef struct dbslmm_problem {
+    const uint8_t* bed;
+    int64_t bed_len;
+    int32_t n_ref;
+    int32_t n_obs;
+    double sigma_s;
+    double tau;
+    int32_t num_block;
+    const int64_t* s_ptr;
+    const int32_t* s_pos;
+    const double* z_s;
+    const int64_t* l_ptr;
+    const int32_t* l_pos;
+    const double* z_l;
+} dbslmm_problem;
+
+/* Kernel timing slots reported by dbslmm_plan_kernel_ms. */
+enum {
+    DBSLMM_K_UNPACK = 0,   /* dbslmm_unpack_stats: 2-bit .bed rows -> int8 dosages + stats */
+    DBSLMM_K_GRAM = 1,     /* dbslmm_gram_i8: i8-MFMA grouped syrk + fp64 standardising epilogue */
+    DBSLMM_K_CHOL = 2,     /* dbslmm_chol_solve: per-block fp64 Cholesky + triangular solves */
+    DBSLMM_K_COUNT = 3
+};
+
+int dbslmm_abi_version(void);
+
+/* Create a context on HIP device `device` (ordinal as seen by this process). */
+int dbslmm_ctx_create(int device, dbslmm_ctx** out);
+void dbslmm_ctx_destroy(dbslmm_ctx* ctx);
+const char* dbslmm_last_error(const dbslmm_ctx* ctx);
+
+/* DBSLMMFIT::est replacement: upload, solve, download, free.  beta_s has s_ptr[num_block]
+ * entries, beta_l l_ptr[num_block] (ignored when l_ptr == NULL); block_status (optional) has
+ * num_block entries.  Blocking. */
+int dbslmm_est(dbslmm_ctx* ctx, const dbslmm_problem* p, double* beta_s, double* beta_l,
+               int32_t* block_status);
+
+/* Split form.  plan_create copies the .bed image and block metadata into HBM and sizes the
+ * workspace; plan_run enqueues the three kernels on the context's stream (asynchronous);
+ * plan_sync waits; plan_download copies beta / status to the caller. */
+int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* p, dbslmm_plan** out);
+int dbslmm_plan_run(dbslmm_plan* plan);
+int dbslmm_plan_sync(dbslmm_plan* plan);
+int dbslmm_plan_download(dbslmm_plan* plan, double* beta_s, double* beta_l, int32_t* block_status);
+/* Change sigma_s (h2f tuning, software/DBSLMM.R:205-219) without re-uploading. */
+int dbslmm_plan_set_sigma(dbslmm_plan* plan, double sigma_s);
+void dbslmm_plan_destroy(dbslmm_plan* plan);
+
+/* Kernel timing (HIP events recorded around each launch on the plan's stream).  Enable before
+ * plan_run; after plan_sync, ms_out[k] = average duration in ms of kernel k over the runs since
+ * enabling, launches_out = number of runs averaged. */
+int dbslmm_plan_enable_timing(dbslmm_plan* plan, int enable);
+int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/, int32_t* launches_out);
+
+/* Workload figures of the plan (for rooflines): [0] SNPs, [1] packed bytes read by the unpack,
+ * [2] int8 bytes written by the unpack, [3] Gram int8 ops (2 per MAC, algorithmic
+ * sum_b n_ref*m_b*(m_b+1)), [4] Gram ops as executed on padded tiles, [5] Cholesky+solve fp64
+ * flops (sum_b m_b^3/3 + 2 m_b^2), [6] blocks, [7] gram tiles. */
+int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[8]*/);
+
+/* MAF pass: maf[r] for every bed row r < n_snp (readSNPIm with an all-ones indicator). */
+int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
+                   int64_t n_snp, double* maf);
+
+/* readSNPIm + nomalizeVec for rows pos[0..n_rows): out is n_ref x n_rows column-major fp64
+ * (column j = standardised dosages of bed row pos[j]); maf (optional) n_rows entries. */
+int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
+                        const int32_t* pos, int32_t n_rows, double* out, double* maf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DBSLMM_HIP_H_ */

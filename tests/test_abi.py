@@ -1,0 +1,60 @@
+"""CPU tests of the C-ABI library: it loads, and exports every symbol include/dbslmm_hip.h
+declares.  No compute call is made without a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from _common import ROOT
+
+HEADER = os.path.join(ROOT, "include", "dbslmm_hip.h")
+LIB = os.path.join(ROOT, "dbslmm_amd", "libdbslmm_hip.so")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(dbslmm_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "dbslmm_est" in syms and "dbslmm_plan_run" in syms and len(syms) >= 14
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "build first: __graft_entry__.build()"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+
+
+def test_python_binding_lists_all_exports():
+    from dbslmm_amd import _lib
+    assert sorted(_lib.EXPORTS) == declared_symbols()
+
+
+def test_library_loads_and_reports_abi():
+    from dbslmm_amd import _lib
+    L = _lib.load()
+    assert L.dbslmm_abi_version() == 1
+
+
+def test_kernels_are_gfx950_code_objects():
+    """The fat binary carries a gfx950 code object (and no other target)."""
+    data = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in data
+
+
+def test_ctx_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from dbslmm_amd import Context, DbslmmError
+    with pytest.raises(DbslmmError):
+        Context(0)
