@@ -264,212 +264,6 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 3: per-block fp64 Cholesky of the joint matrix + forward/back substitution.
-// One workgroup (256 threads, 4 waves) per block, blocks visited largest first (order[]).
-// M is row-major, lower triangle valid (tile (I,J), I >= J); tiles of 32.
-// LDS: D (diag tile, 32x33) + red (8x32) + per-wave staging (2 x 32x33 doubles) when
-// the block has more than one tile (dynamic LDS size chosen by the host per launch).
-// ------------------------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(256) void dbslmm_chol_solve(
-    double* __restrict__ M, const int32_t* __restrict__ order, int32_t n_blocks,
-    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
-    const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
-    const int64_t* __restrict__ blk_matoff,
-    const double* __restrict__ z_slot, const int32_t* __restrict__ slot_out,
-    const double* __restrict__ rsd, double dshift, double inv_sqrt_n,
-    double* __restrict__ y, double* __restrict__ beta_s, double* __restrict__ beta_l,
-    int32_t* __restrict__ status, int32_t* __restrict__ blk_id) {
-    // one dynamic LDS array (no static __shared__: keeps the fp64 carve 16-B aligned)
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    int* s_fail = reinterpret_cast<int*>(lds);  // 16 B header
-    double* D = lds + 2;                       // 32 x 33
-    double* red = D + kTile * kLdsStride;      // 8 x 32
-    double* stage = red + 8 * kTile;           // 4 waves x 2 x 32 x 33 (only when T > 1)
-
-    if (blockIdx.x >= static_cast<unsigned>(n_blocks)) return;
-    const int b = order[blockIdx.x];
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    const int wave = tid / kWave;
-    const int row0 = blk_row0[b];
-    const int m = blk_m[b];
-    const int ms = blk_ms[b];
-    const int ld = blk_ld[b];
-    const int T = ld / kTile;
-    double* A = M + blk_matoff[b];
-    if (tid == 0) *s_fail = 0;
-    __syncthreads();
-
-    for (int kb = 0; kb < T; ++kb) {
-        // (1) diagonal tile -> LDS, with the 1/(sigma_s n) shift on small SNPs, identity padding
-        for (int e = tid; e < kTile * kTile; e += 256) {
-            const int r = e >> 5, c = e & 31;
-            const int gr = kTile * kb + r, gc = kTile * kb + c;
-            double v;
-            if (gr < m && gc < m) {
-                v = A[static_cast<int64_t>(gr) * ld + gc];
-                if (gr == gc && gr < ms) v += dshift;
-            } else {
-                v = (r == c) ? 1.0 : 0.0;
-            }
-            D[r * kLdsStride + c] = v;
-        }
-        __syncthreads();
-        // (2) unblocked right-looking Cholesky of D (lower)
-        for (int jj = 0; jj < kTile; ++jj) {
-            __syncthreads();                            // previous trailing update complete
-            const double djj = D[jj * kLdsStride + jj];
-            const double d = sqrt(djj);
-            if (!(djj > 0.0) && tid == 0 && *s_fail == 0) *s_fail = kTile * kb + jj + 1;
-            if (tid > jj && tid < kTile) D[tid * kLdsStride + jj] /= d;
-            __syncthreads();                            // every thread has read D[jj][jj]
-            if (tid == 0) D[jj * kLdsStride + jj] = d;
-            const int rem = kTile - 1 - jj;            // trailing rows jj+1..31
-            for (int e = tid; e < rem * rem; e += 256) {
-                const int i = jj + 1 + e / rem, k = jj + 1 + e % rem;
-                if (k <= i) D[i * kLdsStride + k] -= D[i * kLdsStride + jj] * D[k * kLdsStride + jj];
-            }
-        }
-        __syncthreads();
-        for (int e = tid; e < kTile * kTile; e += 256) {
-            const int r = e >> 5, c = e & 31;
-            const int gr = kTile * kb + r, gc = kTile * kb + c;
-            if (c <= r && gr < m && gc < m) A[static_cast<int64_t>(gr) * ld + gc] = D[r * kLdsStride + c];
-        }
-        // (3) panel: rows below the diagonal tile solve x * L_kk^T = a (one thread per row)
-        for (int row = kTile * (kb + 1) + tid; row < kTile * T; row += 256) {
-            if (row >= m) continue;
-            double x[kTile];
-            double* prow = A + static_cast<int64_t>(row) * ld + kTile * kb;
-#pragma unroll
-            for (int c = 0; c < kTile; ++c) x[c] = (kTile * kb + c < m) ? prow[c] : 0.0;
-#pragma unroll
-            for (int c = 0; c < kTile; ++c) {
-                double s = x[c];
-#pragma unroll
-                for (int c2 = 0; c2 < c; ++c2) s -= x[c2] * D[c * kLdsStride + c2];
-                x[c] = s / D[c * kLdsStride + c];
-            }
-#pragma unroll
-            for (int c = 0; c < kTile; ++c)
-                if (kTile * kb + c < m) prow[c] = x[c];
-        }
-        __syncthreads();
-        // (4) trailing update C_IJ -= L_I L_J^T over pairs kb < J <= I < T
-        const int nt = T - kb - 1;
-        if (nt > 0) {
-            double* WI = stage + wave * 2 * kTile * kLdsStride;
-            double* WJ = WI + kTile * kLdsStride;
-            const int npairs = nt * (nt + 1) / 2;
-            for (int p = wave; p < npairs; p += 4) {
-                // p -> (I, J) with 0 <= J <= I < nt (row-wise enumeration)
-                int I = static_cast<int>((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
-                while ((I + 1) * (I + 2) / 2 <= p) ++I;
-                while (I * (I + 1) / 2 > p) --I;
-                const int J = p - I * (I + 1) / 2;
-                const int gI = kb + 1 + I, gJ = kb + 1 + J;
-                for (int e = lane; e < kTile * kTile; e += kWave) {
-                    const int r = e >> 5, c = e & 31;
-                    const int rI = kTile * gI + r, rJ = kTile * gJ + r;
-                    WI[r * kLdsStride + c] = rI < m ? A[static_cast<int64_t>(rI) * ld + kTile * kb + c] : 0.0;
-                    WJ[r * kLdsStride + c] = rJ < m ? A[static_cast<int64_t>(rJ) * ld + kTile * kb + c] : 0.0;
-                }
-                wave_sync();
-                const int c = lane & 31;
-                const int rb = 16 * (lane >> 5);
-                double acc[16];
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr) acc[rr] = 0.0;
-#pragma unroll 4
-                for (int k = 0; k < kTile; ++k) {
-                    const double bj = WJ[c * kLdsStride + k];
-#pragma unroll
-                    for (int rr = 0; rr < 16; ++rr) acc[rr] += WI[(rb + rr) * kLdsStride + k] * bj;
-                }
-                const int gc = kTile * gJ + c;
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr) {
-                    const int gr = kTile * gI + rb + rr;
-                    if (gr < m && gc < m && gc <= gr) A[static_cast<int64_t>(gr) * ld + gc] -= acc[rr];
-                }
-                wave_sync();
-            }
-        }
-        __syncthreads();
-    }
-
-    const int fail = *s_fail;
-    double* yb = y + row0;
-    if (fail == 0) {
-        // forward: L y = z
-        for (int I = 0; I < T; ++I) {
-            // partial dot products of rows of tile I with y[0 .. 32I): wave w -> rows w, w+4, ..
-            for (int rr = wave; rr < kTile; rr += 4) {
-                const int gr = kTile * I + rr;
-                double s = 0.0;
-                if (gr < m) {
-                    const double* prow = A + static_cast<int64_t>(gr) * ld;
-                    for (int c = lane; c < kTile * I; c += kWave) s += prow[c] * yb[c];
-                }
-                s = wave_sum_f64(s);
-                if (lane == 0) red[rr] = s;
-            }
-            __syncthreads();
-            if (tid < kTile) {
-                const int gr = kTile * I + tid;
-                double v = gr < m ? z_slot[row0 + gr] - red[tid] : 0.0;
-                // diag tile solve with lanes 0..31 (wave 0)
-                for (int c = 0; c < kTile; ++c) {
-                    const int gc = kTile * I + c;
-                    const double Lcc = gc < m ? A[static_cast<int64_t>(gc) * ld + gc] : 1.0;
-                    const double xc = __shfl(v, c, kWave) / Lcc;
-                    if (tid == c) v = xc;
-                    else if (tid > c && gr < m && gc < m) v -= A[static_cast<int64_t>(gr) * ld + gc] * xc;
-                }
-                if (gr < m) yb[gr] = v;
-            }
-            __syncthreads();
-        }
-        // backward: L^T x = y
-        for (int I = T - 1; I >= 0; --I) {
-            const int c = tid & 31, g = tid >> 5;
-            double s = 0.0;
-            const int gc = kTile * I + c;
-            for (int row = kTile * (I + 1) + g; row < m; row += 8)
-                s += A[static_cast<int64_t>(row) * ld + gc] * yb[row];
-            red[g * kTile + c] = s;
-            __syncthreads();
-            if (tid < kTile) {
-                double acc = 0.0;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) acc += red[q * kTile + tid];
-                double v = gc < m ? yb[gc] - acc : 0.0;
-                for (int cc = kTile - 1; cc >= 0; --cc) {
-                    const int gcc = kTile * I + cc;
-                    const double Lcc = gcc < m ? A[static_cast<int64_t>(gcc) * ld + gcc] : 1.0;
-                    const double xc = __shfl(v, cc, kWave) / Lcc;
-                    if (tid == cc) v = xc;
-                    else if (tid < cc && gcc < m && gc < m) v -= A[static_cast<int64_t>(gcc) * ld + gc] * xc;
-                }
-                if (gc < m) yb[gc] = v;
-            }
-            __syncthreads();
-        }
-    }
-    // scatter beta = x / sqrt(n) to the caller's small / large order; NaN block on failure
-    bool mono = false;
-    for (int i = tid; i < m; i += 256) mono |= !(rsd[row0 + i] < INFINITY);
-    const double nanv = __builtin_nan("");
-    for (int i = tid; i < m; i += 256) {
-        const double v = fail == 0 ? yb[i] * inv_sqrt_n : nanv;
-        const int o = slot_out[row0 + i];
-        if (o >= 0) beta_s[o] = v;
-        else beta_l[-1 - o] = v;
-    }
-    if (fail != 0 || mono) atomicMax(status + blk_id[b], mono ? 3 : 2);
-}
-
-// ------------------------------------------------------------------------------------------
 // readSNPIm + nomalizeVec for a list of rows in ORIGINAL individual order (diagnostics and
 // parity): out[j * n_ref + i] = (g_ij - mu_j) * rsd_j with missing calls at the mean (0).
 // ------------------------------------------------------------------------------------------

@@ -3,11 +3,12 @@
 //
 // HBM layout of a plan (one context = one GPU):
 //   bed       the .bed image as-is (3 magic bytes kept, rows at 3 + r*ceil(n/4)), +16 B pad
-//   slots     non-empty blocks, in block order, each padded to a multiple of 32 slots:
+//   slots     non-empty blocks, in block order, each padded to ld = roundup(m + 1, 32) slots:
 //             [small SNPs | large SNPs | padding]; per slot: bed row (-1 = pad), block,
-//             z-score, output index (>= 0 small, -1-i large)
+//             z-score, output index (>= 0 small, -1-i large); slot m of a block doubles as
+//             the row that carries z through the bordered Cholesky
 //   G         int8 [n_slots][kpad] dosages, kpad = roundup(n_ref, 64)
-//   M         fp64 per block ld x ld row-major (ld = padded block size), lower triangle
+//   M         fp64 per block ld x ld row-major, lower triangle; row m = z (written by the solve)
 //   stats     S, mu, 1/sd per slot; y (solve scratch) per slot; flags/status per block
 // The whole problem stays resident; plan_run re-executes unpack -> gram -> chol from the
 // packed genotypes (nothing cached between runs except the uploaded inputs).
@@ -25,10 +26,10 @@
 
 // The kernels are compiled in this translation unit (no relocatable device code needed).
 #include "kernels.hip"
+#include "chol.hip"
 
 namespace {
-constexpr size_t kCholLdsSmall = sizeof(double) * (2 + kTile * kLdsStride + 8 * kTile);
-constexpr size_t kCholLdsBig = kCholLdsSmall + sizeof(double) * (4 * 2 * kTile * kLdsStride);
+constexpr size_t kCholLds = sizeof(double) * chol::kLdsDoubles;
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 }  // namespace
@@ -52,6 +53,7 @@ struct dbslmm_plan {
     int32_t *d_slot_pos = nullptr, *d_slot_block = nullptr, *d_slot_out = nullptr;
     double *d_z = nullptr, *d_S = nullptr, *d_mu = nullptr, *d_rsd = nullptr, *d_y = nullptr;
     int32_t *d_flags = nullptr, *d_status = nullptr, *d_order = nullptr, *d_blk_id = nullptr;
+    int32_t n_large = 0, n_small = 0;   // Cholesky paths (ld > 64 / ld <= 64); d_order = [large | small]
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
     GramTile* d_tiles = nullptr;
@@ -101,6 +103,10 @@ extern "C" {
 int dbslmm_abi_version(void) { return DBSLMM_ABI_VERSION; }
 
 int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
+    static const hipError_t lds_attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(dbslmm_chol_solve), hipFuncAttributeMaxDynamicSharedMemorySize,
+        static_cast<int>(kCholLds));
+    (void)lds_attr;
     if (!out) return DBSLMM_E_ARG;
     *out = nullptr;
     int n = 0;
@@ -179,7 +185,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         const int64_t m = ms + ml;
         if (m == 0) { p->h_empty.push_back(b); continue; }
         const int nb = static_cast<int>(row0.size());
-        const int64_t ld = round_up(m, kTile);
+        const int64_t ld = round_up(m + 1, kTile);    // + the z row of the bordered matrix
         row0.push_back(static_cast<int32_t>(slot_pos.size()));
         mv.push_back(static_cast<int32_t>(m));
         msv.push_back(static_cast<int32_t>(ms));
@@ -209,7 +215,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             slot_out.push_back(INT32_MIN);
             z.push_back(0.0);
         }
-        const int T = static_cast<int>(ld / kTile);
+        const int T = static_cast<int>((m + kTile - 1) / kTile);   // tiles holding SNP rows
         for (int ti = 0; ti < T; ++ti)
             for (int tj = 0; tj <= ti; ++tj) tiles.push_back({nb, ti, tj, 0});
         ops_alg += static_cast<double>(pr->n_ref) * m * (m + 1);
@@ -221,10 +227,12 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->n_tiles = static_cast<int32_t>(tiles.size());
     p->M_elems = moff;
     p->h_ld = ldv;
-    // largest blocks first for the Cholesky launch (longest-processing-time order)
+    // Cholesky work lists: large blocks (ld > 64, one workgroup each) then small blocks (one
+    // wave each), each largest first (longest-processing-time order)
     std::vector<int32_t> order(p->n_nonempty);
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return mv[a] > mv[c]; });
+    for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
     const double n_snp = static_cast<double>(p->n_s + p->n_l);
     p->wl[0] = n_snp;
     p->wl[1] = n_snp * bps;
@@ -347,10 +355,12 @@ int dbslmm_plan_run(dbslmm_plan* p) {
     if (p->n_nonempty > 0) {
         const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
-        hipLaunchKernelGGL(dbslmm_chol_solve, dim3(p->n_nonempty), dim3(256), kCholLdsBig, s, p->d_M,
-                           p->d_order, p->n_nonempty, p->d_row0, p->d_m, p->d_ms, p->d_ld,
-                           p->d_matoff, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn, p->d_y,
-                           p->d_beta_s, p->d_beta_l, p->d_status, p->d_blk_id);
+        const unsigned grid = static_cast<unsigned>(p->n_large + (p->n_small + 3) / 4);
+        hipLaunchKernelGGL(dbslmm_chol_solve, dim3(grid), dim3(256), kCholLds, s, p->d_M,
+                           p->d_order, p->n_large, p->d_order + p->n_large, p->n_small,
+                           p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id,
+                           p->d_z, p->d_slot_out, p->d_rsd, dshift, isn, p->d_y, p->d_beta_s,
+                           p->d_beta_l, p->d_status);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
