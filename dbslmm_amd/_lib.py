@@ -46,7 +46,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("DBSLMM_LIB_PATH") or LIB_PATH
     if not os.path.exists(p):
         raise DbslmmError(f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                           " (or `make -C dbslmm_amd/csrc`)")

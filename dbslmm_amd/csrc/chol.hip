@@ -12,45 +12,73 @@
 // (row-major, lower-triangular) block matrix, so the Cholesky of the bordered matrix leaves
 // y = L^{-1} z in row m.  Only the backward substitution L^T x = y remains.
 //
-// Two paths in ONE launch (workgroups [0, n_large) take one large block each, the rest take 4
-// small blocks, one per wave):
-//   small (ld <= 64): one wave per block; the bordered (m+1) x m matrix lives in LDS; Crout
-//                     column by column, wave-synchronous (no workgroup barriers).
-//   large (ld > 64):  one 256-thread workgroup per block; right-looking blocked Cholesky on
-//                     32 x 32 tiles in global memory (L2-resident): wave 0 factors the diagonal
-//                     tile (Crout) and inverts it; the panel TRSM is a product with that inverse
-//                     and the trailing update C -= L_I L_J^T, both on v_mfma_f64_16x16x4_f64
-//                     from LDS-staged tiles.  The inverse of each diagonal tile is kept (in the
-//                     tile's upper triangle) for the backward substitution.
+// Two kernels, launched concurrently on two streams:
+//   dbslmm_chol_small (ld <= 64, m <= 63): one wave per block; the bordered matrix lives in LDS
+//       as a packed lower triangle; Crout column by column, wave-synchronous (no barriers).
+//   dbslmm_chol_large (ld > 64): one 512-thread workgroup per block; right-looking blocked
+//       Cholesky on 32 x 32 tiles of the block matrix in global memory (L2-resident).  Wave 0
+//       factors and inverts the diagonal tile; the panel TRSM (product with that inverse) and
+//       the trailing update C -= L_I L_J^T run on v_mfma_f64_16x16x4_f64 with the panel kept
+//       in LDS.  The inverse of each diagonal tile is kept (in the tile's upper triangle) for
+//       the backward substitution.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace chol {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
 
 constexpr int kWave = 64;
-constexpr int kT = 32;        // tile edge
-constexpr int kTS = 34;       // LDS row stride for MFMA operand tiles (conflict-free 16x4 reads)
-constexpr int kSmallLd = 64;  // small path: ld <= 64 (m <= 63)
-constexpr int kSS = 65;       // LDS row stride of the small path
+constexpr int kT = 32;          // tile edge
+constexpr int kTS = 34;         // LDS row stride of MFMA operand tiles (conflict-free 16x4 reads)
+constexpr int kSmallLd = 64;    // small path: ld <= 64 (m <= 63)
+constexpr int kSmallWaves = 2;  // small kernel: 2 waves (blocks) per workgroup
+constexpr int kSmallTri = kSmallLd * (kSmallLd + 1) / 2;   // packed bordered triangle
+constexpr int kSmallDoublesPerWave = kSmallTri + kSmallLd;  // + reciprocal pivots
+constexpr int kLargeThreads = 256;
+constexpr int kLargeWaves = kLargeThreads / kWave;
 
-// LDS carve (doubles) of the large path
-constexpr int kHdr = 2;
-constexpr int kOffD = kHdr;
-constexpr int kOffX = kOffD + kT * kTS;          // inverse of the diagonal tile
-constexpr int kOffRed = kOffX + kT * kTS;        // 8 x 32 partial sums
-constexpr int kOffV = kOffRed + 8 * kT;          // 32 (backward substitution vector)
-constexpr int kOffStage = kOffV + kT;            // 4 waves x 2 tiles x 32 x 34
-constexpr int kLargeDoubles = kOffStage + 4 * 2 * kT * kTS;
-constexpr int kSmallDoubles = 4 * kSmallLd * kSS;
-constexpr int kLdsDoubles = kLargeDoubles > kSmallDoubles ? kLargeDoubles : kSmallDoubles;
+// LDS carve (doubles) of the large kernel
+constexpr int kPanelMax = 16;                    // panel tiles kept resident
+constexpr int kTileD = kT * kTS;                 // one 32x32 tile, stride 34
+constexpr int kOffX = 2;                         // [0,2): flags; X = inverse of the diagonal tile
+constexpr int kOffCol = kOffX + kTileD;          // broadcast column buffer (32) + pivots (32)
+constexpr int kOffRed = kOffCol + 2 * kT;        // 16 x 32 partial sums
+constexpr int kOffLb = kOffRed + 16 * kT;        // diagonal tile being factored (red: <= 16 x 32)
+constexpr int kOffPanel = kOffLb + kTileD;       // kPanelMax tiles (also the x / v vector)
+constexpr int kLargeDoubles = kOffPanel + kPanelMax * kTileD;
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(bits), lane);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(bits >> 32), lane);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+// 1/sqrt(p) to full fp64 accuracy: v_rsq_f64 + one Newton step
+__device__ __forceinline__ double rsqrt_f64(double p) {
+    double rs = __builtin_amdgcn_rsq(p);
+    return rs * (1.5 - 0.5 * p * rs * rs);
+}
+
+#ifdef DBSLMM_STAMPS
+// diagnostic build only: accumulated 100 MHz ticks per phase of the large path
+__device__ unsigned long long g_stamp[8];
+#define STAMP_DECL unsigned long long st_t0 = 0;
+#define STAMP_BEGIN() do { if (threadIdx.x == 0) st_t0 = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define STAMP_END(k) do { if (threadIdx.x == 0) atomicAdd(&g_stamp[k], __builtin_amdgcn_s_memrealtime() - st_t0); } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP_END(k) do {} while (0)
+#endif
 
 struct BlockArgs {
     const int32_t* blk_row0;
@@ -69,77 +97,91 @@ struct BlockArgs {
     int32_t* status;
 };
 
-__device__ __forceinline__ void scatter_beta(const BlockArgs& a, int b, int row0, int i, double x,
-                                             bool fail) {
+__device__ __forceinline__ void scatter_beta(const BlockArgs& a, int row0, int i, double x, bool fail) {
     const double v = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
     const int o = a.slot_out[row0 + i];
     if (o >= 0) a.beta_s[o] = v;
     else a.beta_l[-1 - o] = v;
 }
 
-__device__ __forceinline__ void report_status(const BlockArgs& a, int b, int row0, int m, int lane0,
+__device__ __forceinline__ void report_status(const BlockArgs& a, int b, int row0, int m, int i0,
                                               int stride, bool fail) {
     bool mono = false;
-    for (int i = lane0; i < m; i += stride) mono |= !(a.rsd[row0 + i] < INFINITY);
+    for (int i = i0; i < m; i += stride) mono |= !(a.rsd[row0 + i] < INFINITY);
     if (fail || mono) atomicMax(a.status + a.blk_id[b], mono ? 3 : 2);
 }
 
-// ------------------------------------------------------------------ small path: one wave
+// ================================================================== small path: one wave
+// Packed bordered lower triangle: element (r, k <= r) at r(r+1)/2 + k, rows 0..m (row m = z).
+__device__ __forceinline__ int tri(int r) { return r * (r + 1) / 2; }
+
 __device__ void small_block(const BlockArgs& a, const double* __restrict__ M, int b, double* L,
-                            int lane) {
+                            double* rdg, int lane) {
     const int row0 = a.blk_row0[b], m = a.blk_m[b], ms = a.blk_ms[b], ld = a.blk_ld[b];
     const double* A = M + a.blk_matoff[b];
-    // rows 0..m-1: lower triangle of M (+ d shift on small diagonal); row m: z
     for (int r = 0; r < m; ++r) {
         if (lane <= r) {
             double v = A[static_cast<int64_t>(r) * ld + lane];
             if (lane == r && r < ms) v += a.dshift;
-            L[r * kSS + lane] = v;
+            L[tri(r) + lane] = v;
         }
     }
-    if (lane < m) L[m * kSS + lane] = a.z_slot[row0 + lane];
+    if (lane < m) L[tri(m) + lane] = a.z_slot[row0 + lane];
     wave_sync();
     bool fail = false;
+    const int my = tri(lane);
     for (int j = 0; j < m; ++j) {
         double s = 0.0;
         if (lane >= j && lane <= m) {
-            const double* lr = L + lane * kSS;
-            const double* lj = L + j * kSS;
-            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+            const double* lr = L + my;
+            const double* lj = L + tri(j);
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0, a6 = 0.0, a7 = 0.0;
             int k = 0;
-            for (; k + 4 <= j; k += 4) {
+            for (; k + 8 <= j; k += 8) {
                 a0 += lr[k] * lj[k];
                 a1 += lr[k + 1] * lj[k + 1];
                 a2 += lr[k + 2] * lj[k + 2];
                 a3 += lr[k + 3] * lj[k + 3];
+                a4 += lr[k + 4] * lj[k + 4];
+                a5 += lr[k + 5] * lj[k + 5];
+                a6 += lr[k + 6] * lj[k + 6];
+                a7 += lr[k + 7] * lj[k + 7];
             }
             for (; k < j; ++k) a0 += lr[k] * lj[k];
-            s = lr[j] - ((a0 + a1) + (a2 + a3));
+            s = lr[j] - (((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7)));
         }
-        const double djj = __shfl(s, j, kWave);
-        fail |= !(djj > 0.0);
-        const double dj = sqrt(djj);
-        if (lane > j && lane <= m) L[lane * kSS + j] = s / dj;
-        if (lane == j) L[j * kSS + j] = dj;
+        const double p = __shfl(s, j, kWave);
+        fail |= !(p > 0.0);
+        const double rs = rsqrt_f64(p);
+        if (lane > j && lane <= m) L[my + j] = s * rs;
+        if (lane == j) { L[my + j] = p * rs; rdg[j] = rs; }
         wave_sync();
     }
     // backward substitution L^T x = y, y = row m
-    double v = lane < m ? L[m * kSS + lane] : 0.0;
+    double v = lane < m ? L[tri(m) + lane] : 0.0;
     for (int j = m - 1; j >= 0; --j) {
-        const double xj = __shfl(v, j, kWave) / L[j * kSS + j];
+        const double xj = __shfl(v, j, kWave) * rdg[j];
+        const double lj = lane < j ? L[tri(j) + lane] : 0.0;
         if (lane == j) v = xj;
-        else if (lane < j) v -= L[j * kSS + lane] * xj;
+        else if (lane < j) v -= lj * xj;
     }
-    if (lane < m) scatter_beta(a, b, row0, lane, v, fail);
+    if (lane < m) scatter_beta(a, row0, lane, v, fail);
     report_status(a, b, row0, m, lane, kWave, fail);
 }
 
-// ------------------------------------------------------------------ large path: one workgroup
+// ================================================================== large path helpers
 // Stage a 32x32 tile (rows r0.., cols c0..) of the row-major block matrix into LDS (stride kTS).
 __device__ __forceinline__ void stage_tile(double* W, const double* A, int ld, int r0, int c0, int lane) {
-    for (int e = lane; e < kT * kT; e += kWave) {
-        const int r = e >> 5, c = e & 31;
-        W[r * kTS + c] = A[static_cast<int64_t>(r0 + r) * ld + c0 + c];
+    double v[kT * kT / kWave];
+#pragma unroll
+    for (int it = 0; it < kT * kT / kWave; ++it) {   // all 16 loads in flight before any write
+        const int e = it * kWave + lane;
+        v[it] = A[static_cast<int64_t>(r0 + (e >> 5)) * ld + c0 + (e & 31)];
+    }
+#pragma unroll
+    for (int it = 0; it < kT * kT / kWave; ++it) {
+        const int e = it * kWave + lane;
+        W[(e >> 5) * kTS + (e & 31)] = v[it];
     }
 }
 
@@ -183,167 +225,294 @@ __device__ __forceinline__ void store_acc(const v4d (&acc)[2][2], double* A, int
                 A[static_cast<int64_t>(r0 + 16 * si + (lane >> 4) + 4 * q) * ld + c0 + 16 * sj + (lane & 15)] = acc[si][sj][q];
 }
 
+__device__ __forceinline__ void acc_to_lds(const v4d (&acc)[2][2], double* W, int lane) {
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                W[(16 * si + (lane >> 4) + 4 * q) * kTS + 16 * sj + (lane & 15)] = acc[si][sj][q];
+}
+
+// Wave 0: factor the diagonal tile (c0, c0) and invert it.
+//   Coalesced load into Lb (LDS); lane r < 32 keeps row r in registers and factors
+//   right-looking.  Per column j: pivot from lane j (readlane), 1/sqrt by rsq + Newton, the
+//   scaled column is written to LDS once and read back by every lane as 16 broadcast
+//   ds_read_b128 (no per-element round trips).  X = L^{-1} is formed column-per-lane from
+//   broadcast row reads, published to Xl (LDS), and written back: lower = L, diagonal + upper
+//   (r, c >= r) = X[c][r].  Returns true when a pivot was not positive.
+__device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, int ms, double dshift,
+                                            double* Xl, double* Lb, double* colb, int lane) {
+    const int r = lane & 31;
+    const int jmax = min(kT, m - c0);
+#pragma unroll
+    for (int it = 0; it < kT * kT / kWave; ++it) {
+        const int e = it * kWave + lane;
+        const int rr = e >> 5, cc = e & 31;
+        double v = 0.0;
+        if (cc <= rr && c0 + rr <= m) v = A[static_cast<int64_t>(c0 + rr) * ld + c0 + cc];
+        if (cc == rr && c0 + rr < ms) v += dshift;
+        Lb[rr * kTS + cc] = v;
+    }
+    wave_sync();
+    double d[kT];
+#pragma unroll
+    for (int c = 0; c < kT; ++c) d[c] = Lb[r * kTS + c];
+    bool fail = false;
+    double* rdl = colb + kT;           // reciprocal pivots (LDS, 32)
+#pragma unroll
+    for (int j = 0; j < kT; ++j) {
+        if (j < jmax) {
+            const double p = readlane_f64(d[j], j);
+            fail |= !(p > 0.0);
+            const double rs = rsqrt_f64(p);
+            d[j] = (r == j) ? p * rs : ((r > j) ? d[j] * rs : 0.0);
+            if (lane < kT) {
+                colb[r] = d[j];
+                Lb[r * kTS + j] = d[j];
+            }
+            if (lane == 0) rdl[j] = rs;
+            wave_sync();
+#pragma unroll
+            for (int k0 = (j + 1) & ~7; k0 < kT; k0 += 8) {   // broadcast reads, 8 at a time
+                double col[8];
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    const v2d t = *reinterpret_cast<const v2d*>(colb + k0 + k);
+                    col[k] = t[0];
+                    col[k + 1] = t[1];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k0 + k > j) d[k0 + k] -= d[j] * col[k];
+            }
+            wave_sync();
+        }
+    }
+    // X = L^{-1}, lane c owns column c: x[q] = (delta_qc - sum_{k<q} L[q][k] x[k]) / L[q][q]
+    double x[kT];
+#pragma unroll
+    for (int q = 0; q < kT; ++q) {
+        double s0 = (q == r) ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+        for (int k0 = 0; k0 < q; k0 += 8) {      // broadcast row reads, 8 at a time
+            double row[8];
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const v2d t = *reinterpret_cast<const v2d*>(Lb + q * kTS + k0 + k);
+                row[k] = t[0];
+                row[k + 1] = t[1];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k0 + k < q) {
+                    if (k & 1) s1 -= row[k] * x[k0 + k];
+                    else s0 -= row[k] * x[k0 + k];
+                }
+            }
+        }
+        x[q] = (q < jmax) ? (s0 + s1) * rdl[q] : ((q == r) ? 1.0 : 0.0);
+    }
+    if (lane < kT) {
+#pragma unroll
+        for (int q = 0; q < kT; ++q) Xl[q * kTS + r] = x[q];
+    }
+    wave_sync();
+#pragma unroll
+    for (int it = 0; it < kT * kT / kWave; ++it) {
+        const int e = it * kWave + lane;
+        const int rr = e >> 5, cc = e & 31;
+        if (c0 + rr > m) continue;
+        if (cc < rr) {
+            if (cc < jmax) A[static_cast<int64_t>(c0 + rr) * ld + c0 + cc] = Lb[rr * kTS + cc];
+        } else if (rr < jmax) {
+            A[static_cast<int64_t>(c0 + rr) * ld + c0 + cc] = Xl[cc * kTS + rr];
+        }
+    }
+    return fail;
+}
+
+__device__ __forceinline__ void decode_pair(int p, int tri_n, int kb, int Tz, int& I, int& J) {
+    if (p < tri_n) {
+        int i = static_cast<int>((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+        while ((i + 1) * (i + 2) / 2 <= p) ++i;
+        while (i * (i + 1) / 2 > p) --i;
+        I = kb + 1 + i;
+        J = kb + 1 + (p - i * (i + 1) / 2);
+    } else {
+        I = Tz;
+        J = kb + 1 + (p - tri_n);
+    }
+}
+
 __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* __restrict__ y,
                             int b, double* lds) {
+    constexpr int NT = kLargeThreads, NW = kLargeWaves;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
     const int row0 = a.blk_row0[b], m = a.blk_m[b], ms = a.blk_ms[b], ld = a.blk_ld[b];
     double* A = M + a.blk_matoff[b];
     int* s_fail = reinterpret_cast<int*>(lds);
-    double* D = lds + kOffD;
-    double* X = lds + kOffX;
+    double* Xl = lds + kOffX;
+    double* colb = lds + kOffCol;
     double* red = lds + kOffRed;
-    double* vv = lds + kOffV;
-    double* WI = lds + kOffStage + wave * 2 * kT * kTS;
-    double* WJ = WI + kT * kTS;
+    double* Lb = lds + kOffLb;
+    double* panel = lds + kOffPanel;
     const int Tm = (m + kT - 1) / kT;   // tiles holding SNP columns
     const int Tz = m / kT;              // tile holding the z row
+    STAMP_DECL
     if (tid == 0) *s_fail = 0;
-    for (int c = tid; c < m; c += 256) A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];
+    for (int c = tid; c < m; c += NT) A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];
     __syncthreads();
 
     for (int kb = 0; kb < Tm; ++kb) {
         const int c0 = kT * kb;
-        const int jmax = min(kT, m - c0);
-        // (1) diagonal tile: Crout + inverse by wave 0
+        // (1) diagonal tile: factor + inverse, wave 0
+        STAMP_BEGIN();
         if (wave == 0) {
-            for (int e = lane; e < kT * kT; e += kWave) {
-                const int r = e >> 5, c = e & 31;
-                double v = 0.0;
-                if (c <= r && c0 + r <= m) {
-                    v = A[static_cast<int64_t>(c0 + r) * ld + c0 + c];
-                    if (r == c && c0 + r < ms) v += a.dshift;
-                }
-                D[r * kTS + c] = v;
-            }
-            wave_sync();
-            bool fail = false;
-            for (int j = 0; j < jmax; ++j) {
-                double s = 0.0;
-                if (lane >= j && lane < kT) {
-                    const double* lr = D + lane * kTS;
-                    const double* lj = D + j * kTS;
-                    double a0 = 0.0, a1 = 0.0;
-                    int k = 0;
-                    for (; k + 2 <= j; k += 2) { a0 += lr[k] * lj[k]; a1 += lr[k + 1] * lj[k + 1]; }
-                    if (k < j) a0 += lr[k] * lj[k];
-                    s = lr[j] - (a0 + a1);
-                }
-                const double djj = __shfl(s, j, kWave);
-                fail |= !(djj > 0.0);
-                const double dj = sqrt(djj);
-                if (lane > j && lane < kT) D[lane * kTS + j] = s / dj;
-                if (lane == j) D[j * kTS + j] = dj;
-                wave_sync();
-            }
-            if (fail && lane == 0) *s_fail = 1;
-            // X = D^{-1} (lower), identity beyond jmax; lane c owns column c
-            if (lane < kT) {
-                const int c = lane;
-                for (int r = 0; r < kT; ++r) {
-                    double v = 0.0;
-                    if (r >= c) {
-                        if (r < jmax) {
-                            double s = (r == c) ? 1.0 : 0.0;
-                            for (int k = c; k < r; ++k) s -= D[r * kTS + k] * X[k * kTS + c];
-                            v = s / D[r * kTS + r];
-                        } else {
-                            v = (r == c) ? 1.0 : 0.0;
-                        }
-                    }
-                    X[r * kTS + c] = v;
-                }
-            }
-            wave_sync();
-            // write back: lower = L, diagonal = 1/L_cc, upper (c > r) = X[c][r] (= X^T)
-            for (int e = lane; e < kT * kT; e += kWave) {
-                const int r = e >> 5, c = e & 31;
-                if (c0 + r > m) continue;
-                double v;
-                if (c < r) v = D[r * kTS + c];
-                else if (r < jmax) v = X[c * kTS + r];
-                else continue;
-                A[static_cast<int64_t>(c0 + r) * ld + c0 + c] = v;
-            }
+            const bool f = factor_diag(A, ld, c0, m, ms, a.dshift, Xl, Lb, colb, lane);
+            if (f && lane == 0) *s_fail = 1;
         }
         __syncthreads();
+        STAMP_END(0);
         if (*s_fail) break;
-        // (2) panel: L_I = A_I X^T for tile rows I = kb+1 .. Tz
-        for (int I = kb + 1 + wave; I <= Tz; I += 4) {
-            stage_tile(WI, A, ld, kT * I, c0, lane);
+        STAMP_BEGIN();
+        // (2) panel: L_I = A_I X^T for tile rows I = kb+1 .. Tz; kept in LDS when they fit
+        const int P = Tz - kb;
+        const bool fits = P <= kPanelMax;
+        for (int I = kb + 1 + wave; I <= Tz; I += NW) {
+            double* W = fits ? panel + (I - kb - 1) * kTileD : panel + 2 * wave * kTileD;
+            stage_tile(W, A, ld, kT * I, c0, lane);
             wave_sync();
             v4d acc[2][2] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
-            mfma_tile(acc, WI, X, 1.0, lane);
+            mfma_tile(acc, W, Xl, 1.0, lane);
             store_acc(acc, A, ld, kT * I, c0, lane);
             wave_sync();
+            if (fits) acc_to_lds(acc, W, lane);
         }
         __syncthreads();
-        // (3) trailing update C_IJ -= L_I L_J^T, kb < J <= I <= Tz, J < Tm
+        STAMP_END(1);
+        STAMP_BEGIN();
+        // (3) trailing update C_IJ -= L_I L_J^T, kb < J <= I <= Tz, J < Tm; the next pair's C
+        //     tile is prefetched into registers while the current one is on the MFMA pipe
         const int nJ = Tm - 1 - kb;
         if (nJ > 0) {
-            const int tri = nJ * (nJ + 1) / 2;
-            const int npairs = tri + (Tz == Tm ? nJ : 0);
-            for (int p = wave; p < npairs; p += 4) {
-                int I, J;
-                if (p < tri) {
-                    int i = static_cast<int>((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
-                    while ((i + 1) * (i + 2) / 2 <= p) ++i;
-                    while (i * (i + 1) / 2 > p) --i;
-                    I = kb + 1 + i;
-                    J = kb + 1 + (p - i * (i + 1) / 2);
-                } else {
-                    I = Tz;
-                    J = kb + 1 + (p - tri);
+            const int tri_n = nJ * (nJ + 1) / 2;
+            const int npairs = tri_n + (Tz == Tm ? nJ : 0);
+            int p = wave, I = 0, J = 0;
+            v4d cur[2][2], nxt[2][2];
+            if (p < npairs) {
+                decode_pair(p, tri_n, kb, Tz, I, J);
+                load_acc(cur, A, ld, kT * I, kT * J, lane);
+            }
+            while (p < npairs) {
+                const int pn = p + NW;
+                int In = 0, Jn = 0;
+                if (pn < npairs) {
+                    decode_pair(pn, tri_n, kb, Tz, In, Jn);
+                    load_acc(nxt, A, ld, kT * In, kT * Jn, lane);
                 }
-                stage_tile(WI, A, ld, kT * I, c0, lane);
-                if (I != J) stage_tile(WJ, A, ld, kT * J, c0, lane);
-                wave_sync();
-                v4d acc[2][2];
-                load_acc(acc, A, ld, kT * I, kT * J, lane);
-                mfma_tile(acc, WI, I != J ? WJ : WI, -1.0, lane);
-                store_acc(acc, A, ld, kT * I, kT * J, lane);
-                wave_sync();
+                const double* LI;
+                const double* LJ;
+                if (fits) {
+                    LI = panel + (I - kb - 1) * kTileD;
+                    LJ = panel + (J - kb - 1) * kTileD;
+                } else {
+                    double* WI = panel + 2 * wave * kTileD;
+                    double* WJ = WI + kTileD;
+                    stage_tile(WI, A, ld, kT * I, c0, lane);
+                    if (I != J) stage_tile(WJ, A, ld, kT * J, c0, lane);
+                    wave_sync();
+                    LI = WI;
+                    LJ = I != J ? WJ : WI;
+                }
+                mfma_tile(cur, LI, LJ, -1.0, lane);
+                store_acc(cur, A, ld, kT * I, kT * J, lane);
+                if (!fits) wave_sync();
+#pragma unroll
+                for (int si = 0; si < 2; ++si)
+#pragma unroll
+                    for (int sj = 0; sj < 2; ++sj) cur[si][sj] = nxt[si][sj];
+                I = In;
+                J = Jn;
+                p = pn;
             }
         }
         __syncthreads();
+        STAMP_END(2);
     }
+    STAMP_BEGIN();
     const bool fail = *s_fail != 0;
-    double* x = y + row0;
+    double* v = panel;   // v / x vector
+    if (m > kPanelMax * kTileD) v = y + row0;
     if (!fail) {
-        // backward substitution L^T x = y (y = row m of the factor), tile by tile
-        for (int I = Tm - 1; I >= 0; --I) {
-            const int c = tid & 31, g = tid >> 5;
-            const int gc = kT * I + c;
-            double s = 0.0;
-            for (int r = kT * (I + 1) + g; r < m; r += 8) s += A[static_cast<int64_t>(r) * ld + gc] * x[r];
-            red[g * kT + c] = s;
+        // backward substitution L^T x = y, right-looking over tile rows J = Tm-1 .. 0
+        for (int c = tid; c < m; c += NT) v[c] = A[static_cast<int64_t>(m) * ld + c];
+        __syncthreads();
+        for (int J = Tm - 1; J >= 0; --J) {
+            const int c1 = kT * J;
+            const int jmax = min(kT, m - c1);
+            constexpr int NG = NT / kT;                        // thread groups of 32
+            {   // x_J = X_JJ^T v_J with X^T stored in the tile's diagonal + upper triangle
+                const int c = tid & 31, g = tid >> 5;
+                double s = 0.0;
+                if (c < jmax)
+                    for (int k = c + g; k < jmax; k += NG)
+                        s += A[static_cast<int64_t>(c1 + c) * ld + c1 + k] * v[c1 + k];
+                red[g * kT + c] = s;
+            }
             __syncthreads();
-            if (tid < kT) {
-                const int jmax = min(kT, m - kT * I);
-                double acc = 0.0;
+            if (tid < jmax) {
+                double s = 0.0;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) acc += red[q * kT + tid];
-                vv[tid] = tid < jmax ? A[static_cast<int64_t>(m) * ld + gc] - acc : 0.0;
-                wave_sync();
-                // x_c = sum_{k >= c} X[k][c] v_k ; X[k][c] stored at (c, k) of the diagonal tile
-                double xc = 0.0;
-                if (tid < jmax)
-                    for (int k = tid; k < jmax; ++k) xc += A[static_cast<int64_t>(gc) * ld + kT * I + k] * vv[k];
-                if (tid < jmax) x[gc] = xc;
+                for (int q = 0; q < NG; ++q) s += red[q * kT + tid];
+                v[c1 + tid] = s;
+            }
+            __syncthreads();
+            // v[col] -= sum_r L[c1 + r][col] x[c1 + r] for col < c1 (row strip of tile row J)
+            for (int col = tid; col < c1; col += NT) {
+                double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                for (int rr = 0; rr < kT; rr += 2) {
+                    const double l0 = A[static_cast<int64_t>(c1 + rr) * ld + col];
+                    const double l1 = A[static_cast<int64_t>(c1 + rr + 1) * ld + col];
+                    if (rr < jmax) s0 += l0 * v[c1 + rr];
+                    if (rr + 1 < jmax) s1 += l1 * v[c1 + rr + 1];
+                }
+                v[col] -= s0 + s1;
             }
             __syncthreads();
         }
     }
-    for (int i = tid; i < m; i += 256) scatter_beta(a, b, row0, i, fail ? 0.0 : x[i], fail);
-    report_status(a, b, row0, m, tid, 256, fail);
+    STAMP_END(3);
+    for (int i = tid; i < m; i += NT) scatter_beta(a, row0, i, fail ? 0.0 : v[i], fail);
+    report_status(a, b, row0, m, tid, NT, fail);
 }
 
 }  // namespace chol
 
-// One launch: workgroups [0, n_large) -> large blocks (order_large), the rest -> 4 small blocks
-// each (order_small).  Dynamic LDS = chol::kLdsDoubles doubles.
-extern "C" __global__ __launch_bounds__(256) void dbslmm_chol_solve(
-    double* __restrict__ M, const int32_t* __restrict__ order_large, int32_t n_large,
-    const int32_t* __restrict__ order_small, int32_t n_small,
+// Blocks with ld <= 64: one wave each, kSmallWaves per workgroup.
+extern "C" __global__ __launch_bounds__(chol::kSmallWaves * chol::kWave) void dbslmm_chol_small(
+    const double* __restrict__ M, const int32_t* __restrict__ order, int32_t n_blocks,
+    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
+    const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
+    const int64_t* __restrict__ blk_matoff, const int32_t* __restrict__ blk_id,
+    const double* __restrict__ z_slot, const int32_t* __restrict__ slot_out,
+    const double* __restrict__ rsd, double dshift, double inv_sqrt_n,
+    double* __restrict__ beta_s, double* __restrict__ beta_l, int32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) double lds[chol::kSmallWaves * chol::kSmallDoublesPerWave];
+    const chol::BlockArgs a{blk_row0, blk_m, blk_ms, blk_ld, blk_matoff, blk_id, z_slot, slot_out,
+                            rsd, dshift, inv_sqrt_n, beta_s, beta_l, status};
+    const int wave = threadIdx.x / chol::kWave, lane = threadIdx.x & (chol::kWave - 1);
+    const int idx = blockIdx.x * chol::kSmallWaves + wave;
+    if (idx >= n_blocks) return;     // whole wave leaves; this kernel has no workgroup barrier
+    double* L = lds + wave * chol::kSmallDoublesPerWave;
+    chol::small_block(a, M, order[idx], L, L + chol::kSmallTri, lane);
+}
+
+// Blocks with ld > 64: one 512-thread workgroup each.  Dynamic LDS = kLargeDoubles doubles.
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_large(
+    double* __restrict__ M, const int32_t* __restrict__ order, int32_t n_blocks,
     const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
     const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
     const int64_t* __restrict__ blk_matoff, const int32_t* __restrict__ blk_id,
@@ -353,12 +522,6 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_chol_solve(
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const chol::BlockArgs a{blk_row0, blk_m, blk_ms, blk_ld, blk_matoff, blk_id, z_slot, slot_out,
                             rsd, dshift, inv_sqrt_n, beta_s, beta_l, status};
-    if (static_cast<int>(blockIdx.x) < n_large) {
-        chol::large_block(a, M, y, order_large[blockIdx.x], lds);
-        return;
-    }
-    const int wave = threadIdx.x / chol::kWave, lane = threadIdx.x & (chol::kWave - 1);
-    const int idx = (static_cast<int>(blockIdx.x) - n_large) * 4 + wave;
-    if (idx >= n_small) return;      // whole wave leaves; the small path has no workgroup barrier
-    chol::small_block(a, M, order_small[idx], lds + wave * chol::kSmallLd * chol::kSS, lane);
+    if (static_cast<int>(blockIdx.x) >= n_blocks) return;
+    chol::large_block(a, M, y, order[blockIdx.x], lds);
 }

@@ -29,14 +29,16 @@
 #include "chol.hip"
 
 namespace {
-constexpr size_t kCholLds = sizeof(double) * chol::kLdsDoubles;
+constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 }  // namespace
 
 struct dbslmm_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;    // main stream (unpack, gram, large-block Cholesky)
+    hipStream_t stream2 = nullptr;   // small-block Cholesky, forked from / joined into `stream`
+    hipEvent_t fork = nullptr, join = nullptr;
     std::string err;
 };
 
@@ -103,10 +105,6 @@ extern "C" {
 int dbslmm_abi_version(void) { return DBSLMM_ABI_VERSION; }
 
 int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
-    static const hipError_t lds_attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(dbslmm_chol_solve), hipFuncAttributeMaxDynamicSharedMemorySize,
-        static_cast<int>(kCholLds));
-    (void)lds_attr;
     if (!out) return DBSLMM_E_ARG;
     *out = nullptr;
     int n = 0;
@@ -115,8 +113,14 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
     auto* c = new dbslmm_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kCholLargeLds)) != hipSuccess) {
+        dbslmm_ctx_destroy(c);
         return DBSLMM_E_HIP;
     }
     *out = c;
@@ -127,6 +131,9 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+    if (ctx->join) (void)hipEventDestroy(ctx->join);
     delete ctx;
 }
 
@@ -355,13 +362,27 @@ int dbslmm_plan_run(dbslmm_plan* p) {
     if (p->n_nonempty > 0) {
         const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
-        const unsigned grid = static_cast<unsigned>(p->n_large + (p->n_small + 3) / 4);
-        hipLaunchKernelGGL(dbslmm_chol_solve, dim3(grid), dim3(256), kCholLds, s, p->d_M,
-                           p->d_order, p->n_large, p->d_order + p->n_large, p->n_small,
-                           p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id,
-                           p->d_z, p->d_slot_out, p->d_rsd, dshift, isn, p->d_y, p->d_beta_s,
-                           p->d_beta_l, p->d_status);
-        HIP_TRY(ctx, hipGetLastError());
+        // fork: small blocks on stream2 while the large blocks run on the main stream
+        HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+        if (p->n_large > 0) {
+            hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
+                               kCholLargeLds, s, p->d_M, p->d_order, p->n_large, p->d_row0, p->d_m,
+                               p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z, p->d_slot_out,
+                               p->d_rsd, dshift, isn, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+        if (p->n_small > 0) {
+            const unsigned g = static_cast<unsigned>((p->n_small + chol::kSmallWaves - 1) / chol::kSmallWaves);
+            hipLaunchKernelGGL(dbslmm_chol_small, dim3(g), dim3(chol::kSmallWaves * chol::kWave), 0,
+                               ctx->stream2, p->d_M, p->d_order + p->n_large, p->n_small, p->d_row0,
+                               p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
+                               p->d_slot_out, p->d_rsd, dshift, isn, p->d_beta_s, p->d_beta_l,
+                               p->d_status);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+        HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
     }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
     p->ran = true;
@@ -514,5 +535,16 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
     (void)hipFree(d_out);
     return rc;
 }
+
+#ifdef DBSLMM_STAMPS
+// diagnostic build only (libdbslmm_hip_stamps.so): read + clear the per-phase tick counters
+int dbslmm_debug_stamps(double* out8) {
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(chol::g_stamp), sizeof(h)) != hipSuccess) return -2;
+    for (int i = 0; i < 8; ++i) out8[i] = static_cast<double>(h[i]) * 10.0;  // ns (100 MHz clock)
+    unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(chol::g_stamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 }  // extern "C"
