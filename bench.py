@@ -57,10 +57,27 @@ def kernel_roofline(name, ms, wl):
         return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_I8_TOPS, unit="TFLOP/s",
                     frac=a / PEAK_I8_TOPS, algorithmic=wl["gram_ops_alg"], ms=ms,
                     note="int8 ops (2/MAC), algorithmic sum_b n_ref*m_b*(m_b+1)")
-    a = wl["chol_flops"] / s / 1e12
+    fl = wl["chol_flops_large"] if name == "dbslmm_chol_large" else wl["chol_flops_small"]
+    a = fl / s / 1e12 if s > 0 else 0.0
     return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
-                frac=a / PEAK_F64_TFLOPS, algorithmic=wl["chol_flops"], ms=ms,
-                note="fp64 flops sum_b m^3/3 + 2m^2 vs the fp64 peak")
+                frac=a / PEAK_F64_TFLOPS, algorithmic=fl, ms=ms,
+                note="fp64 flops sum_b m^3/3 + 2m^2 over its blocks vs the fp64 MFMA peak; "
+                     "latency-bound (sequential column chain), see DESIGN.md")
+
+
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
+    WRITE_SIZE, tools/pmc_traffic.py) of this same default workload, or None."""
+    import glob
+    default = (args.snps, args.n_ref, args.pop, args.lmm_only) == (50000, 2000, "EUR", False)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not default or not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -117,10 +134,11 @@ def main():
     total_snps = float(snps.item())
     value = total_snps * args.steps / elapsed
 
-    kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl) for k in range(3)]
+    kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl) for k in range(len(KERNEL_NAMES))]
     dom = max(kernels, key=lambda r: r["ms"])
+    traffic, tsrc = pmc_traffic(dom["kernel"], args)
     roof = dict(bound=dom["bound"], achieved=dom["achieved"], peak=dom["peak"], unit=dom["unit"],
-                frac=dom["frac"], traffic=None, kernel=dom["kernel"])
+                frac=dom["frac"], traffic=traffic, kernel=dom["kernel"], traffic_source=tsrc)
 
     cpu = None
     dbeta = None

@@ -130,16 +130,17 @@ class Plan:
         self.ctx.check(self.ctx.lib.dbslmm_plan_enable_timing(self.h, int(on)), "plan_enable_timing")
 
     def kernel_ms(self):
-        out = np.zeros(3)
+        out = np.zeros(len(KERNEL_NAMES))
         n = np.zeros(1, dtype=np.int32)
         self.ctx.check(self.ctx.lib.dbslmm_plan_kernel_ms(self.h, _ptr(out), _ptr(n)), "plan_kernel_ms")
         return out, int(n[0])
 
     def workload(self) -> dict:
-        w = np.zeros(8)
+        w = np.zeros(10)
         self.ctx.check(self.ctx.lib.dbslmm_plan_workload(self.h, _ptr(w)), "plan_workload")
         keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
-                "gram_ops_exec", "chol_flops", "blocks", "gram_tiles")
+                "gram_ops_exec", "chol_flops_large", "blocks", "gram_tiles", "chol_flops_small",
+                "blocks_large")
         return dict(zip(keys, w.tolist()))
 
     def download(self):

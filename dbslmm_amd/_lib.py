@@ -20,8 +20,8 @@ EXPORTS = (
     "dbslmm_bed_maf", "dbslmm_read_snp_std",
 )
 
-K_UNPACK, K_GRAM, K_CHOL = 0, 1, 2
-KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_solve")
+K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL = 0, 1, 2, 3
+KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small")
 BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC = 0, 1, 2, 3
 
 

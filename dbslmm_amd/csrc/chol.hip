@@ -74,7 +74,11 @@ __device__ unsigned long long g_stamp[8];
 #define STAMP_DECL unsigned long long st_t0 = 0;
 #define STAMP_BEGIN() do { if (threadIdx.x == 0) st_t0 = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define STAMP_END(k) do { if (threadIdx.x == 0) atomicAdd(&g_stamp[k], __builtin_amdgcn_s_memrealtime() - st_t0); } while (0)
+#define FSTAMP(k) do { if (lane == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); atomicAdd(&g_stamp[k], t_ - fst); fst = t_; } } while (0)
+#define FSTAMP_DECL unsigned long long fst = __builtin_amdgcn_s_memrealtime();
 #else
+#define FSTAMP(k) do {} while (0)
+#define FSTAMP_DECL
 #define STAMP_DECL
 #define STAMP_BEGIN() do {} while (0)
 #define STAMP_END(k) do {} while (0)
@@ -191,17 +195,23 @@ __device__ __forceinline__ void stage_tile(double* W, const double* A, int ld, i
 __device__ __forceinline__ void mfma_tile(v4d (&acc)[2][2], const double* P, const double* Q,
                                           double sign, int lane) {
     const int ri = lane & 15, kq = lane >> 4;
+    // all 32 operand reads first (one LDS latency for the whole tile), then 32 MFMAs
+    double p0[kT / 4], p1[kT / 4], q0[kT / 4], q1[kT / 4];
 #pragma unroll
     for (int kk = 0; kk < kT / 4; ++kk) {
         const int k = 4 * kk + kq;
-        const double p0 = sign * P[ri * kTS + k];
-        const double p1 = sign * P[(16 + ri) * kTS + k];
-        const double q0 = Q[ri * kTS + k];
-        const double q1 = Q[(16 + ri) * kTS + k];
-        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
+        p0[kk] = P[ri * kTS + k];
+        p1[kk] = P[(16 + ri) * kTS + k];
+        q0[kk] = Q[ri * kTS + k];
+        q1[kk] = Q[(16 + ri) * kTS + k];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kT / 4; ++kk) {
+        const double a0 = sign * p0[kk], a1 = sign * p1[kk];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q0[kk], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q1[kk], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, q0[kk], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, q1[kk], acc[1][1], 0, 0, 0);
     }
 }
 
@@ -243,15 +253,20 @@ __device__ __forceinline__ void acc_to_lds(const v4d (&acc)[2][2], double* W, in
 //   broadcast row reads, published to Xl (LDS), and written back: lower = L, diagonal + upper
 //   (r, c >= r) = X[c][r].  Returns true when a pivot was not positive.
 __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, int ms, double dshift,
-                                            double* Xl, double* Lb, double* colb, int lane) {
+                                            double* Xl, double* Lb, double* colb, int lane,
+                                            bool from_lds) {
+    FSTAMP_DECL
     const int r = lane & 31;
     const int jmax = min(kT, m - c0);
+    // tile -> Lb: from global (coalesced), or already in Lb (lookahead: the updating wave put it
+    // there); keep the lower triangle of rows <= m, add 1/(sigma_s n) on the small diagonal
 #pragma unroll
     for (int it = 0; it < kT * kT / kWave; ++it) {
         const int e = it * kWave + lane;
         const int rr = e >> 5, cc = e & 31;
         double v = 0.0;
-        if (cc <= rr && c0 + rr <= m) v = A[static_cast<int64_t>(c0 + rr) * ld + c0 + cc];
+        if (cc <= rr && c0 + rr <= m)
+            v = from_lds ? Lb[rr * kTS + cc] : A[static_cast<int64_t>(c0 + rr) * ld + c0 + cc];
         if (cc == rr && c0 + rr < ms) v += dshift;
         Lb[rr * kTS + cc] = v;
     }
@@ -259,6 +274,7 @@ __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, in
     double d[kT];
 #pragma unroll
     for (int c = 0; c < kT; ++c) d[c] = Lb[r * kTS + c];
+    FSTAMP(4);
     bool fail = false;
     double* rdl = colb + kT;           // reciprocal pivots (LDS, 32)
 #pragma unroll
@@ -290,6 +306,7 @@ __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, in
             wave_sync();
         }
     }
+    FSTAMP(5);
     // X = L^{-1}, lane c owns column c: x[q] = (delta_qc - sum_{k<q} L[q][k] x[k]) / L[q][q]
     double x[kT];
 #pragma unroll
@@ -319,6 +336,7 @@ __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, in
         for (int q = 0; q < kT; ++q) Xl[q * kTS + r] = x[q];
     }
     wave_sync();
+    FSTAMP(6);
 #pragma unroll
     for (int it = 0; it < kT * kT / kWave; ++it) {
         const int e = it * kWave + lane;
@@ -330,6 +348,7 @@ __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, in
             A[static_cast<int64_t>(c0 + rr) * ld + c0 + cc] = Xl[cc * kTS + rr];
         }
     }
+    FSTAMP(7);
     return fail;
 }
 
@@ -365,17 +384,20 @@ __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* 
     for (int c = tid; c < m; c += NT) A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];
     __syncthreads();
 
+    int* s_next = s_fail + 1;   // dynamic pair counter of the trailing update
+    // diagonal tile 0; every later diagonal tile is factored by lookahead inside the previous
+    // step's trailing update (wave 0 updates it first, then factors it while the other waves
+    // finish the remaining pairs)
+    STAMP_BEGIN();
+    if (wave == 0) {
+        const bool f = factor_diag(A, ld, 0, m, ms, a.dshift, Xl, Lb, colb, lane, false);
+        if (f && lane == 0) *s_fail = 1;
+    }
+    __syncthreads();
+    STAMP_END(0);
     for (int kb = 0; kb < Tm; ++kb) {
-        const int c0 = kT * kb;
-        // (1) diagonal tile: factor + inverse, wave 0
-        STAMP_BEGIN();
-        if (wave == 0) {
-            const bool f = factor_diag(A, ld, c0, m, ms, a.dshift, Xl, Lb, colb, lane);
-            if (f && lane == 0) *s_fail = 1;
-        }
-        __syncthreads();
-        STAMP_END(0);
         if (*s_fail) break;
+        const int c0 = kT * kb;
         STAMP_BEGIN();
         // (2) panel: L_I = A_I X^T for tile rows I = kb+1 .. Tz; kept in LDS when they fit
         const int P = Tz - kb;
@@ -390,42 +412,57 @@ __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* 
             wave_sync();
             if (fits) acc_to_lds(acc, W, lane);
         }
+        if (tid == 0) *s_next = 1;
         __syncthreads();
         STAMP_END(1);
         STAMP_BEGIN();
-        // (3) trailing update C_IJ -= L_I L_J^T, kb < J <= I <= Tz, J < Tm; the next pair's C
-        //     tile is prefetched into registers while the current one is on the MFMA pipe
+        // (3) trailing update C_IJ -= L_I L_J^T, kb < J <= I <= Tz, J < Tm.  Pair 0 is the next
+        //     diagonal tile (kb+1, kb+1): wave 0 updates it into LDS and factors it (lookahead);
+        //     pairs 1.. are handed out dynamically; the next pair's C tile is prefetched.
         const int nJ = Tm - 1 - kb;
         if (nJ > 0) {
             const int tri_n = nJ * (nJ + 1) / 2;
             const int npairs = tri_n + (Tz == Tm ? nJ : 0);
-            int p = wave, I = 0, J = 0;
+            auto tile_ptr = [&](int I, double* stage_slot) -> const double* {
+                if (fits) return panel + (I - kb - 1) * kTileD;
+                stage_tile(stage_slot, A, ld, kT * I, c0, lane);
+                return stage_slot;
+            };
+            if (wave == 0) {
+                const int d0 = kT * (kb + 1);
+                v4d acc[2][2];
+                load_acc(acc, A, ld, d0, d0, lane);
+                const double* LI = tile_ptr(kb + 1, panel + 0 * kTileD);
+                wave_sync();
+                mfma_tile(acc, LI, LI, -1.0, lane);
+                wave_sync();
+                acc_to_lds(acc, Lb, lane);
+                wave_sync();
+                const bool f = factor_diag(A, ld, d0, m, ms, a.dshift, Xl, Lb, colb, lane, true);
+                if (f && lane == 0) *s_fail = 1;
+            }
+            auto grab = [&]() -> int {
+                int q = 0;
+                if (lane == 0) q = atomicAdd(s_next, 1);
+                return __shfl(q, 0, kWave);
+            };
+            int p = grab(), I = 0, J = 0;
             v4d cur[2][2], nxt[2][2];
             if (p < npairs) {
                 decode_pair(p, tri_n, kb, Tz, I, J);
                 load_acc(cur, A, ld, kT * I, kT * J, lane);
             }
             while (p < npairs) {
-                const int pn = p + NW;
+                const int pn = grab();
                 int In = 0, Jn = 0;
                 if (pn < npairs) {
                     decode_pair(pn, tri_n, kb, Tz, In, Jn);
                     load_acc(nxt, A, ld, kT * In, kT * Jn, lane);
                 }
-                const double* LI;
-                const double* LJ;
-                if (fits) {
-                    LI = panel + (I - kb - 1) * kTileD;
-                    LJ = panel + (J - kb - 1) * kTileD;
-                } else {
-                    double* WI = panel + 2 * wave * kTileD;
-                    double* WJ = WI + kTileD;
-                    stage_tile(WI, A, ld, kT * I, c0, lane);
-                    if (I != J) stage_tile(WJ, A, ld, kT * J, c0, lane);
-                    wave_sync();
-                    LI = WI;
-                    LJ = I != J ? WJ : WI;
-                }
+                double* WI = panel + 2 * wave * kTileD;
+                const double* LI = tile_ptr(I, WI);
+                const double* LJ = (I == J) ? LI : tile_ptr(J, WI + kTileD);
+                if (!fits) wave_sync();
                 mfma_tile(cur, LI, LJ, -1.0, lane);
                 store_acc(cur, A, ld, kT * I, kT * J, lane);
                 if (!fits) wave_sync();

@@ -1,0 +1,417 @@
+// dbslmm_main.cpp -- drop-in `dbslmm` command line on top of libdbslmm_hip.so.
+//
+// Same flags, files and output formats as the reference binary (scr/main_dbslmm.cpp,
+// scr/dbslmm.cpp:67-398).  The host steps (argument parsing, .fam/.bim/block/summary readers,
+// allele + MAF matching, block assignment, output writers) are restated here in plain C++
+// (reference: scr/dtpr.cpp:47-220, 383-481); the hot path -- the MAF pass of readBim and
+// DBSLMMFIT::est -- goes through the C-ABI (include/dbslmm_hip.h) to the GPU.
+//
+// Extensions (not in the reference): --gpu N (HIP device), --tau T (default 0.8 as hard-coded at
+// scr/dbslmmfit.cpp:697,751), --precise-out (17 significant digits), --dry-run (stop after
+// matching; prints counts, no GPU).  -dat_str / -test_indicator_file are accepted; the test-set
+// variance file (variance.txt, scr/calc_asymptotic_variance.cpp) is not produced yet.
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/time.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/dbslmm_hip.h"
+
+using std::string;
+using std::vector;
+
+namespace {
+
+struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised here)
+    string s, l, r, b, eff, test_indicator_file, dat_str;
+    int n = 0, nsnp = 0, t = 1;
+    double mafMax = 1.0, h = -1.0;
+    // extensions
+    int gpu = 0;
+    double tau = 0.8;
+    bool precise = false, dry_run = false;
+};
+
+struct Allele { int64_t pos; string a1, a2; double maf; };                 // ALLELE
+struct Block { string chr; long start, end; };                              // BLOCK
+struct Summ { string snp; long ps; string a1, a2; double maf, z; };        // SUMM (P unused)
+struct Info { string snp; long ps; int64_t pos; int block; string a1; double maf, z; };  // INFO
+
+double walltime() {
+    struct timeval tv;
+    gettimeofday(&tv, nullptr);
+    return static_cast<double>(tv.tv_sec) + tv.tv_usec * 1e-6;
+}
+
+void print_header() {
+    std::cout << "\n*************************************************************\n"
+              << "  Deterministic Bayesian Sparse Linear Mixed Model (DBSLMM)  \n"
+              << "  MI355X (gfx950) build of the per-LD-block solver          \n"
+              << "  For Help, Type ./dbslmm -h                                 \n"
+              << "*************************************************************\n\n";
+}
+
+void print_help() {
+    std::cout << " FILE I/O RELATED OPTIONS\n"
+              << " -s        [filename]   specify input the summary data for the small effect SNPs.\n"
+              << " -l        [filename]   specify input the summary data for the large effect SNPs.\n"
+              << " -r        [filename]   specify input the bfile of reference data.\n"
+              << " -n        [num]        specify input the sample size of the summary data.\n"
+              << " -mafMax   [num]        specify input the maximium of the difference between reference panel and summary data.\n"
+              << " -nsnp     [num]   specify input the number of snp.\n"
+              << " -b        [num]        specify input the block information.\n"
+              << " -h        [num]        specify input the heritability.\n"
+              << " -t        [filename]   specify input thread.\n"
+              << " -eff      [filename]   specify output the estimate effect SNPs.\n"
+              << " --gpu     [num]        HIP device (extension)\n"
+              << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
+              << " --precise-out          17 significant digits in <eff>.txt (extension)\n";
+}
+
+// DBSLMM::Assign (scr/dbslmm.cpp:67-172): a flag's value is skipped when it starts with '-'.
+void assign(int argc, char** argv, Param& p) {
+    auto take = [&](int& i) -> const char* {
+        if (i + 1 >= argc || argv[i + 1] == nullptr || argv[i + 1][0] == '-') return nullptr;
+        return argv[++i];
+    };
+    for (int i = 0; i < argc; ++i) {
+        const char* a = argv[i];
+        const char* v = nullptr;
+        auto is = [&](const char* x, const char* y) { return !strcmp(a, x) || !strcmp(a, y); };
+        if (is("--smallEff", "-s")) { if ((v = take(i))) p.s = v; }
+        else if (is("--largeEff", "-l")) { if ((v = take(i))) p.l = v; }
+        else if (is("--reference", "-r")) { if ((v = take(i))) p.r = v; }
+        else if (is("--N", "-n")) { if ((v = take(i))) p.n = atoi(v); }
+        else if (is("--mafMax", "-mafMax")) { if ((v = take(i))) p.mafMax = atof(v); }
+        else if (is("--numSNP", "-nsnp")) { if ((v = take(i))) p.nsnp = atoi(v); }
+        else if (is("--block", "-b")) { if ((v = take(i))) p.b = v; }
+        else if (is("--Heritability", "-h")) { if ((v = take(i))) p.h = atof(v); }
+        else if (is("--Thread", "-t")) { if ((v = take(i))) p.t = atoi(v); }
+        else if (is("--EFF", "-eff")) { if ((v = take(i))) p.eff = v; }
+        else if (is("--test_indicator_file", "-test_indicator_file")) { if ((v = take(i))) p.test_indicator_file = v; }
+        else if (is("--dat_str", "-dat_str")) { if ((v = take(i))) p.dat_str = v; }
+        else if (!strcmp(a, "--gpu")) { if ((v = take(i))) p.gpu = atoi(v); }
+        else if (!strcmp(a, "--tau")) { if ((v = take(i))) p.tau = atof(v); }
+        else if (!strcmp(a, "--precise-out")) p.precise = true;
+        else if (!strcmp(a, "--dry-run")) p.dry_run = true;
+    }
+}
+
+vector<string> split(const string& line, char sep) {
+    vector<string> out;
+    string e;
+    std::stringstream ss(line);
+    while (std::getline(ss, e, sep)) out.push_back(e);
+    return out;
+}
+
+// IO::getRow (scr/dtpr.cpp:71-80)
+int get_row(const string& path) {
+    std::ifstream f(path);
+    string line;
+    int n = 0;
+    while (std::getline(f, line)) ++n;
+    return n;
+}
+
+// IO::readBlock (scr/dtpr.cpp:47-68)
+vector<Block> read_block(const string& path) {
+    vector<Block> out;
+    std::ifstream f(path);
+    string line;
+    while (std::getline(f, line)) {
+        auto t = split(line, '\t');
+        if (t.size() < 3) continue;
+        out.push_back({t[0], atol(t[1].c_str()), atol(t[2].c_str())});
+    }
+    return out;
+}
+
+// mmap'd .bed image
+struct Mapped {
+    const uint8_t* p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    bool open(const string& path) {
+        fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) return false;
+        struct stat st;
+        if (fstat(fd, &st) != 0) return false;
+        n = static_cast<size_t>(st.st_size);
+        void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) return false;
+        p = static_cast<const uint8_t*>(m);
+        return true;
+    }
+    ~Mapped() {
+        if (p) munmap(const_cast<uint8_t*>(p), n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+// IO::readBim (scr/dtpr.cpp:83-123): maf from the GPU MAF pass when constr.
+bool read_bim(const string& ref, const vector<double>& maf, std::unordered_map<string, Allele>& bim,
+              vector<string>& order) {
+    std::ifstream f(ref + ".bim");
+    if (!f) return false;
+    string line;
+    int64_t count = 0;
+    while (std::getline(f, line)) {
+        auto t = split(line, '\t');
+        if (t.size() < 6) { ++count; continue; }
+        const double m = count < static_cast<int64_t>(maf.size()) ? maf[count] : 0.0;
+        if (bim.find(t[1]) == bim.end()) {                 // std::map::insert keeps the first
+            bim.emplace(t[1], Allele{count, t[4], t[5], m});
+            order.push_back(t[1]);
+        }
+        ++count;
+    }
+    return true;
+}
+
+// IO::readSumm (scr/dtpr.cpp:178-220): GEMMA, no header; z = beta/se when se starts with a digit
+// and > 1e-20, else 0.
+vector<Summ> read_summ(const string& path) {
+    vector<Summ> out;
+    std::ifstream f(path);
+    string line;
+    while (std::getline(f, line)) {
+        auto t = split(line, '\t');
+        if (t.size() < 11) continue;
+        Summ s;
+        s.z = 0.0;
+        if (isdigit(static_cast<unsigned char>(t[9].c_str()[0]))) {
+            const double se = atof(t[9].c_str());
+            if (se - 0.0 > 1e-20) s.z = atof(t[8].c_str()) / se;
+        }
+        s.snp = t[1];
+        s.ps = atol(t[2].c_str());
+        s.a1 = t[5];
+        s.a2 = t[6];
+        const double af = atof(t[7].c_str());
+        s.maf = std::min(af, 1.0 - af);
+        out.push_back(s);
+    }
+    return out;
+}
+
+struct Pos { string snp; long ps; int64_t pos; string a1; double maf, z; };
+
+// SNPPROC::matchRef (scr/dtpr.cpp:383-408): strict allele equality, |maf_ref - maf| < mafMax.
+// A SNP absent from the .bim compares against a default ALLELE ("", "", 0.0) as the reference's
+// operator[] does, and is never kept.
+vector<Pos> match_ref(const vector<Summ>& summ, const std::unordered_map<string, Allele>& bim,
+                      double maf_max, vector<char>& good) {
+    vector<Pos> inter;
+    good.assign(summ.size(), 0);
+    int dis = 0, mafc = 0;
+    static const Allele empty{0, "", "", 0.0};
+    for (size_t i = 0; i < summ.size(); ++i) {
+        auto it = bim.find(summ[i].snp);
+        const Allele& b = it == bim.end() ? empty : it->second;
+        const bool a1 = b.a1 == summ[i].a1, a2 = b.a2 == summ[i].a2;
+        const bool mb = std::fabs(b.maf - summ[i].maf) < maf_max;
+        if (!a1 || !a2) ++dis;
+        if (!mb) ++mafc;
+        if (a1 && a2 && mb && it != bim.end()) {
+            inter.push_back({summ[i].snp, summ[i].ps, b.pos, summ[i].a1, summ[i].maf, summ[i].z});
+            good[i] = 1;
+        }
+    }
+    std::cout << "Number of allele discrepency: " << dis << "\n";
+    std::cout << "Number of maf discrepency:    " << mafc << "\n";
+    return inter;
+}
+
+// SNPPROC::addBlock (scr/dtpr.cpp:455-481): [start, end), sequential scan; unassigned SNPs are
+// dropped.
+vector<Info> add_block(const vector<Pos>& inter, const vector<Block>& blocks) {
+    vector<Info> out;
+    size_t count = 0;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+        for (size_t j = count; j < inter.size(); ++j) {
+            if (inter[j].ps >= blocks[i].start && inter[j].ps < blocks[i].end) {
+                out.push_back({inter[j].snp, inter[j].ps, inter[j].pos, static_cast<int>(i),
+                               inter[j].a1, inter[j].maf, inter[j].z});
+                ++count;
+            } else {
+                break;
+            }
+        }
+    }
+    return out;
+}
+
+void to_csr(const vector<Info>& info, int nb, vector<int64_t>& ptr, vector<int32_t>& pos, vector<double>& z) {
+    ptr.assign(nb + 1, 0);
+    for (const auto& e : info) ptr[e.block + 1]++;
+    for (int b = 0; b < nb; ++b) ptr[b + 1] += ptr[b];
+    pos.resize(info.size());
+    z.resize(info.size());
+    for (size_t i = 0; i < info.size(); ++i) {   // info is in block order (addBlock)
+        pos[i] = static_cast<int32_t>(info[i].pos);
+        z[i] = info[i].z;
+    }
+}
+
+int fail(const string& msg) {
+    std::cerr << "ERROR: " << msg << std::endl;
+    return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc <= 1) { print_header(); return 0; }
+    if (argc == 2 && argv[1][0] == '-' && argv[1][1] == 'h') { print_help(); return 0; }
+    Param p;
+    assign(argc, argv, p);
+
+    std::cout << "Options: \n-s:      " << p.s << "\n-l:      " << p.l << "\n-r:      " << p.r
+              << "\n-nsnp:   " << p.nsnp << "\n-n:      " << p.n << "\n-mafMax: " << p.mafMax
+              << "\n-b:      " << p.b << "\n-h:      " << p.h << "\n-t:      " << p.t
+              << "\n-eff:    " << p.eff << "\n";
+    // input checks of BatchRun (scr/dbslmm.cpp:195-227)
+    if (p.s.empty()) return fail("-s is no parameter!");
+    std::ifstream sf(p.s), lf(p.l), rf(p.r + ".fam"), bf(p.b);
+    if (!bf) return fail(p.b + " dose not exist!");
+    if (!sf) return fail(p.s + " dose not exist!");
+    if (!rf) return fail(p.r + " dose not exist!");
+    if (p.b.empty()) return fail("-b is no parameter!");
+    if (p.r.empty()) return fail(p.r + " dose not exist!");
+    if (p.h > 1 || p.h < 0) return fail("-h is not correct (0, 1)!");
+    if (p.t > 100 || p.t < 1) return fail("-t is not correct (1, 100)!");
+    if (p.eff.empty()) return fail("-eff is no parameter!");
+    if (p.nsnp <= 0 || p.n <= 0) return fail("-n and -nsnp must be positive!");
+
+    std::cout << "Reading reference PLINK FAM file from [" << p.r << ".fam]\n";
+    const int n_ref = get_row(p.r + ".fam");
+    std::cout << n_ref << " individuals to be included from reference FAM file.\n";
+    std::cout << "Reading reference PLINK BIM file from [" << p.r << ".bim]\n";
+    const int n_snp_bim = get_row(p.r + ".bim");
+    const bool constr = !(std::fabs(p.mafMax - 1.0) < 1e-10);
+
+    dbslmm_ctx* ctx = nullptr;
+    Mapped bed;
+    if (!p.dry_run) {
+        if (!bed.open(p.r + ".bed")) return fail(p.r + ".bed cannot be opened");
+        if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) return fail("no usable HIP device (dbslmm_ctx_create)");
+    } else if (constr) {
+        return fail("--dry-run needs -mafMax 1 (the MAF pass runs on the GPU)");
+    }
+    vector<double> maf;
+    if (constr) {
+        std::cout << "Calculating MAF of reference panel ...\n";
+        maf.resize(n_snp_bim);
+        if (dbslmm_bed_maf(ctx, bed.p, static_cast<int64_t>(bed.n), n_ref, n_snp_bim, maf.data()) != DBSLMM_OK)
+            return fail(string("MAF pass: ") + dbslmm_last_error(ctx));
+    } else {
+        std::cout << "[WARNING] Do not consider the difference between reference panel and summary data ...\n";
+    }
+    std::unordered_map<string, Allele> bim;
+    vector<string> bim_order;
+    read_bim(p.r, maf, bim, bim_order);
+    std::cout << bim.size() << " SNPs to be included from reference BIM file.\n";
+    const vector<Block> blocks = read_block(p.b);
+
+    std::cout << "Reading summary data of small effect SNPs from [" << p.s << "]\n";
+    const vector<Summ> summ_s = read_summ(p.s);
+    vector<char> good_s;
+    const vector<Pos> inter_s = match_ref(summ_s, bim, p.mafMax, good_s);
+    std::cout << "After filtering, " << inter_s.size() << " small effect SNPs are selected.\n";
+    const vector<Info> info_s = add_block(inter_s, blocks);
+    std::ofstream bad(p.eff + ".badsnps");
+    for (size_t i = 0; i < summ_s.size(); ++i)
+        if (!good_s[i]) bad << summ_s[i].snp << " " << 0 << "\n";
+
+    vector<Info> info_l;
+    bool has_l = false;
+    if (lf) {
+        std::cout << "Reading summary data of large effect SNPs from [" << p.l << "]\n";
+        const vector<Summ> summ_l = read_summ(p.l);
+        vector<char> good_l;
+        const vector<Pos> inter_l = match_ref(summ_l, bim, p.mafMax, good_l);
+        if (!inter_l.empty()) {
+            info_l = add_block(inter_l, blocks);
+            std::cout << "After filtering, " << inter_l.size() << " large effect SNPs are selected.\n";
+            has_l = true;
+        } else {
+            std::cout << "After filtering, no large effect SNP is selected.\n";
+        }
+        for (size_t i = 0; i < summ_l.size(); ++i)
+            if (!good_l[i]) bad << summ_l[i].snp << " " << 1 << "\n";
+    }
+    bad.close();
+    if (!p.dat_str.empty() || !p.test_indicator_file.empty())
+        std::cout << "[NOTE] -dat_str / -test_indicator_file accepted; variance.txt is not produced by this build.\n";
+
+    const int nb = static_cast<int>(blocks.size());
+    vector<int64_t> s_ptr, l_ptr;
+    vector<int32_t> s_pos, l_pos;
+    vector<double> z_s, z_l;
+    to_csr(info_s, nb, s_ptr, s_pos, z_s);
+    if (has_l) to_csr(info_l, nb, l_ptr, l_pos, z_l);
+    if (p.dry_run) {
+        std::cout << "dry-run: blocks " << nb << " small " << info_s.size() << " large " << info_l.size() << "\n";
+        return 0;
+    }
+
+    const double sigma_s = p.h / static_cast<double>(p.nsnp);                 // dbslmm.cpp:332
+    dbslmm_problem prob{};
+    prob.bed = bed.p;
+    prob.bed_len = static_cast<int64_t>(bed.n);
+    prob.n_ref = n_ref;
+    prob.n_obs = p.n;
+    prob.sigma_s = sigma_s;
+    prob.tau = p.tau;
+    prob.num_block = nb;
+    prob.s_ptr = s_ptr.data();
+    prob.s_pos = s_pos.data();
+    prob.z_s = z_s.data();
+    if (has_l) {
+        prob.l_ptr = l_ptr.data();
+        prob.l_pos = l_pos.data();
+        prob.z_l = z_l.data();
+    }
+    vector<double> beta_s(info_s.size()), beta_l(info_l.size());
+    vector<int32_t> status(std::max(nb, 1));
+    std::cout << "Fitting model...\n";
+    const double t0 = walltime();
+    const int rc = dbslmm_est(ctx, &prob, beta_s.data(), beta_l.data(), status.data());
+    if (rc != DBSLMM_OK) return fail(string("dbslmm_est: ") + dbslmm_last_error(ctx));
+    std::cout << "Fitting time: " << walltime() - t0 << " seconds.\n";
+    int n_bad = 0;
+    for (int b = 0; b < nb; ++b)
+        if (status[b] == DBSLMM_BLOCK_NOT_PD || status[b] == DBSLMM_BLOCK_MONOMORPHIC) ++n_bad;
+    if (n_bad) std::cerr << "ERROR: Matrix is Singular! (" << n_bad << " LD blocks, beta = nan)\n";
+
+    // output writer (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small rows
+    std::ofstream out(p.eff + ".txt");
+    if (p.precise) out.precision(17);
+    auto emit = [&](const vector<Info>& info, const vector<double>& beta, int flag) {
+        for (size_t i = 0; i < info.size(); ++i) {
+            const double noscl = beta[i] / std::sqrt(2 * info[i].maf * (1 - info[i].maf));
+            if (std::isinf(noscl)) continue;
+            out << info[i].snp << " " << info[i].a1 << " " << beta[i] << " " << noscl << " " << flag << "\n";
+        }
+    };
+    emit(info_l, beta_l, 1);
+    emit(info_s, beta_s, 0);
+    out.close();
+    dbslmm_ctx_destroy(ctx);
+    return 0;
+}

@@ -29,6 +29,9 @@
 #include "chol.hip"
 
 namespace {
+// events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large
+// (main stream), [4] / [5] around chol_small (second stream)
+constexpr int kEvPerRun = 6;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -64,12 +67,12 @@ struct dbslmm_plan {
     std::vector<int32_t> h_ld;  // per non-empty block
     std::vector<int32_t> h_empty;  // original ids of empty blocks
     // workload figures
-    double wl[8] = {0};
+    double wl[DBSLMM_WORKLOAD_LEN] = {0};
     // timing
     bool timing = false;
-    std::vector<hipEvent_t> ev;  // 4 per run
+    std::vector<hipEvent_t> ev;  // kEvPerRun per run
     int runs_pending = 0;
-    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0};
+    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0};
     int32_t ms_runs = 0;
     bool ran = false;
 };
@@ -184,7 +187,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<int64_t> matoff;
     std::vector<GramTile> tiles;
     int64_t moff = 0;
-    double ops_alg = 0, ops_exec = 0, chol_flops = 0;
+    double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0;
     for (int b = 0; b < pr->num_block; ++b) {
         const int64_t s0 = pr->s_ptr[b], ms = pr->s_ptr[b + 1] - s0;
         const int64_t l0 = has_l ? pr->l_ptr[b] : 0, ml = has_l ? pr->l_ptr[b + 1] - l0 : 0;
@@ -227,7 +230,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             for (int tj = 0; tj <= ti; ++tj) tiles.push_back({nb, ti, tj, 0});
         ops_alg += static_cast<double>(pr->n_ref) * m * (m + 1);
         ops_exec += 2.0 * p->kpad * kTile * kTile * (T * (T + 1) / 2);
-        chol_flops += m * static_cast<double>(m) * m / 3.0 + 2.0 * m * m;
+        (ld > chol::kSmallLd ? chol_flops_large : chol_flops_small) +=
+            m * static_cast<double>(m) * m / 3.0 + 2.0 * m * m;
     }
     p->n_nonempty = static_cast<int32_t>(row0.size());
     p->n_slots = static_cast<int32_t>(slot_pos.size());
@@ -246,9 +250,11 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[2] = static_cast<double>(p->n_slots) * p->kpad;
     p->wl[3] = ops_alg;
     p->wl[4] = ops_exec;
-    p->wl[5] = chol_flops;
+    p->wl[5] = chol_flops_large;
     p->wl[6] = p->n_nonempty;
     p->wl[7] = p->n_tiles;
+    p->wl[8] = chol_flops_small;
+    p->wl[9] = p->n_large;
 
     // ---- device allocations
     hipError_t e = hipSetDevice(ctx->device);
@@ -301,7 +307,7 @@ int dbslmm_plan_set_sigma(dbslmm_plan* p, double sigma_s) {
 int dbslmm_plan_enable_timing(dbslmm_plan* p, int enable) {
     if (!p) return DBSLMM_E_ARG;
     p->timing = enable != 0;
-    p->ms_acc[0] = p->ms_acc[1] = p->ms_acc[2] = 0.0;
+    for (double& v : p->ms_acc) v = 0.0;
     p->ms_runs = 0;
     return DBSLMM_OK;
 }
@@ -309,10 +315,11 @@ int dbslmm_plan_enable_timing(dbslmm_plan* p, int enable) {
 static int collect_timing(dbslmm_plan* p) {
     dbslmm_ctx* ctx = p->ctx;
     for (int r = 0; r < p->runs_pending; ++r) {
-        hipEvent_t* e = &p->ev[4 * r];
+        hipEvent_t* e = &p->ev[kEvPerRun * r];
+        const int from[DBSLMM_K_COUNT] = {0, 1, 2, 4}, to[DBSLMM_K_COUNT] = {1, 2, 3, 5};
         for (int k = 0; k < DBSLMM_K_COUNT; ++k) {
             float ms = 0.f;
-            HIP_TRY(ctx, hipEventElapsedTime(&ms, e[k], e[k + 1]));
+            HIP_TRY(ctx, hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
             p->ms_acc[k] += ms;
         }
         p->ms_runs++;
@@ -328,13 +335,13 @@ int dbslmm_plan_run(dbslmm_plan* p) {
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
     if (p->timing) {
-        const size_t need = 4 * static_cast<size_t>(p->runs_pending + 1);
+        const size_t need = kEvPerRun * static_cast<size_t>(p->runs_pending + 1);
         while (p->ev.size() < need) {
             hipEvent_t e;
             HIP_TRY(ctx, hipEventCreate(&e));
             p->ev.push_back(e);
         }
-        ev = &p->ev[4 * p->runs_pending];
+        ev = &p->ev[kEvPerRun * p->runs_pending];
         p->runs_pending++;
     }
     const size_t nbk = std::max<int32_t>(1, std::max(p->n_nonempty, p->num_block));
@@ -374,6 +381,7 @@ int dbslmm_plan_run(dbslmm_plan* p) {
         }
         if (p->n_small > 0) {
             const unsigned g = static_cast<unsigned>((p->n_small + chol::kSmallWaves - 1) / chol::kSmallWaves);
+            if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ctx->stream2));
             hipLaunchKernelGGL(dbslmm_chol_small, dim3(g), dim3(chol::kSmallWaves * chol::kWave), 0,
                                ctx->stream2, p->d_M, p->d_order + p->n_large, p->n_small, p->d_row0,
                                p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
@@ -381,10 +389,16 @@ int dbslmm_plan_run(dbslmm_plan* p) {
                                p->d_status);
             HIP_TRY(ctx, hipGetLastError());
         }
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[5], ctx->stream2));
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
         HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
         HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
     }
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
+    else if (ev) {   // no blocks: keep the event set complete
+        HIP_TRY(ctx, hipEventRecord(ev[3], s));
+        HIP_TRY(ctx, hipEventRecord(ev[4], s));
+        HIP_TRY(ctx, hipEventRecord(ev[5], s));
+    }
     p->ran = true;
     return DBSLMM_OK;
 }
@@ -407,7 +421,7 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* p, double* ms_out, int32_t* launches_out)
 
 int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     if (!p || !out) return DBSLMM_E_ARG;
-    for (int i = 0; i < 8; ++i) out[i] = p->wl[i];
+    for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = p->wl[i];
     return DBSLMM_OK;
 }
 

@@ -83,10 +83,12 @@ typedef struct dbslmm_problem {
 
 /* Kernel timing slots reported by dbslmm_plan_kernel_ms. */
 enum {
-    DBSLMM_K_UNPACK = 0,   /* dbslmm_unpack_stats: 2-bit .bed rows -> int8 dosages + stats */
-    DBSLMM_K_GRAM = 1,     /* dbslmm_gram_i8: i8-MFMA grouped syrk + fp64 standardising epilogue */
-    DBSLMM_K_CHOL = 2,     /* dbslmm_chol_solve: per-block fp64 Cholesky + triangular solves */
-    DBSLMM_K_COUNT = 3
+    DBSLMM_K_UNPACK = 0,      /* dbslmm_unpack_stats: 2-bit .bed rows -> int8 dosages + stats */
+    DBSLMM_K_GRAM = 1,        /* dbslmm_gram_i8: i8-MFMA grouped syrk + fp64 standardising epilogue */
+    DBSLMM_K_CHOL_LARGE = 2,  /* dbslmm_chol_large: blocks with > 63 SNPs, one workgroup each */
+    DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
+                                 (runs concurrently with CHOL_LARGE on a second stream) */
+    DBSLMM_K_COUNT = 4
 };
 
 int dbslmm_abi_version(void);
@@ -122,8 +124,10 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
 /* Workload figures of the plan (for rooflines): [0] SNPs, [1] packed bytes read by the unpack,
  * [2] int8 bytes written by the unpack, [3] Gram int8 ops (2 per MAC, algorithmic
  * sum_b n_ref*m_b*(m_b+1)), [4] Gram ops as executed on padded tiles, [5] Cholesky+solve fp64
- * flops (sum_b m_b^3/3 + 2 m_b^2), [6] blocks, [7] gram tiles. */
-int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[8]*/);
+ * flops of the large blocks (sum_b m_b^3/3 + 2 m_b^2), [6] non-empty blocks, [7] gram tiles,
+ * [8] the same fp64 flops for the small blocks, [9] large blocks. */
+#define DBSLMM_WORKLOAD_LEN 10
+int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
 
 /* MAF pass: maf[r] for every bed row r < n_snp (readSNPIm with an all-ones indicator). */
 int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,

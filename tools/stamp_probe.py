@@ -15,4 +15,4 @@ for name, mask in {"largest": m_blk == m_blk.max(), "m64-128": (m_blk > 63) & (m
     for _ in range(reps): plan.run()
     plan.sync(); L.dbslmm_debug_stamps(out.ctypes.data_as(C.c_void_p))
     nb = int(mask.sum())
-    print(name, "blocks", nb, "per-block us: diag %.1f panel %.1f trailing %.1f backward %.1f" % tuple(out[:4] / reps / nb / 1e3))
+    print(name, "blocks", nb, "per-block us: diag %.1f panel %.1f trailing %.1f backward %.1f | factor_diag: load %.1f factor %.1f inverse %.1f writeback %.1f" % tuple(out[:8] / reps / nb / 1e3))
