@@ -29,20 +29,36 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_I8_TOPS = 5000.0        # dense i8 MFMA = 2x the ~2.5 PF dense bf16 rate
 PEAK_F64_TFLOPS = 78.6       # fp64 (vector = matrix rate on gfx950)
 
+# BASELINE.json configs (1-based): synthetic panels; 3-5 are the scale configs
+CONFIGS = {
+    2: dict(snps=50000, n_ref=2000, pop="EUR", lmm_only=False, gen="numpy"),
+    3: dict(snps=500000, n_ref=5000, pop="EUR", lmm_only=False, gen="gpu"),
+    4: dict(snps=1000000, n_ref=10000, pop="EUR", lmm_only=False, gen="gpu"),
+    5: dict(snps=1000000, n_ref=10000, pop="AFR", lmm_only=True, gen="gpu"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--snps", type=int, default=50000)
-    ap.add_argument("--n-ref", type=int, default=2000)
-    ap.add_argument("--pop", default="EUR")
-    ap.add_argument("--lmm-only", action="store_true")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i-1] preset (2 = default single-GPU workload)")
+    ap.add_argument("--snps", type=int, default=None)
+    ap.add_argument("--n-ref", type=int, default=None)
+    ap.add_argument("--pop", default=None)
+    ap.add_argument("--lmm-only", action="store_true", default=None)
+    ap.add_argument("--gen", choices=("numpy", "gpu"), default=None,
+                    help="synthetic panel generator (default: numpy for config 2, gpu above)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def kernel_roofline(name, ms, wl):
@@ -57,19 +73,21 @@ def kernel_roofline(name, ms, wl):
         return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_I8_TOPS, unit="TFLOP/s",
                     frac=a / PEAK_I8_TOPS, algorithmic=wl["gram_ops_alg"], ms=ms,
                     note="int8 ops (2/MAC), algorithmic sum_b n_ref*m_b*(m_b+1)")
-    fl = wl["chol_flops_large"] if name == "dbslmm_chol_large" else wl["chol_flops_small"]
+    fl = {"dbslmm_chol_large": wl["chol_flops_large"], "dbslmm_chol_small": wl["chol_flops_small"],
+          "dbslmm_tchol": wl["chol_flops_tiled"]}[name]
     a = fl / s / 1e12 if s > 0 else 0.0
     return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
                 frac=a / PEAK_F64_TFLOPS, algorithmic=fl, ms=ms,
-                note="fp64 flops sum_b m^3/3 + 2m^2 over its blocks vs the fp64 MFMA peak; "
-                     "latency-bound (sequential column chain), see DESIGN.md")
+                note="fp64 flops sum_b m^3/3 + 2m^2 over its blocks vs the fp64 MFMA peak"
+                     + ("; multi-workgroup sequence, %d launches" % wl["tiled_launches"]
+                        if name == "dbslmm_tchol" else "; latency-bound (sequential column chain)"))
 
 
 def pmc_traffic(kernel, args):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
     WRITE_SIZE, tools/pmc_traffic.py) of this same default workload, or None."""
     import glob
-    default = (args.snps, args.n_ref, args.pop, args.lmm_only) == (50000, 2000, "EUR", False)
+    default = (args.snps, args.n_ref, args.pop, args.lmm_only, args.gen) == (50000, 2000, "EUR", False, "numpy")
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
     if not default or not files:
         return None, None
@@ -101,7 +119,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    panel = synth.simulate(args.snps, args.n_ref, pop=args.pop, seed=1 + rank)
+    panel = synth.simulate(args.snps, args.n_ref, pop=args.pop, seed=1 + rank, engine=args.gen,
+                           device=local if world > 1 else 0)
     prob = synth.make_problem(panel, lmm_only=args.lmm_only)
     ctx = Context(local if world > 1 else 0)
     plan = Plan(ctx, prob)
@@ -147,23 +166,61 @@ def main():
         import oracle as O
         blas = O.use_blas(True)
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        reps, tc = 0, 0.0
+        from dbslmm_amd.dist import sub_problem
+        # bounded sample: whole workload repeated if it fits the budget, else blocks in a fixed
+        # random order until the budget is spent (beta compared on exactly those blocks)
+        from dbslmm_amd.dist import block_cost
+        nblk = len(prob.s_ptr) - 1
+        m_b = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
+        cost = block_cost(m_b, prob.n_ref)
+        order = np.random.default_rng(0).permutation(nblk)
+        target = min(cost.sum(), 2e10)            # ~0.1-1 s of 16-thread CPU work per call
+        chunks, cur, acc = [], [], 0.0
+        skipped = int(np.sum(cost > 5 * target))
+        for b in order:
+            if cost[b] > 5 * target:           # keeps one call bounded (largest blocks skipped)
+                continue
+            cur.append(b)
+            acc += cost[b]
+            if acc >= target:
+                chunks.append(np.sort(np.array(cur)))
+                cur, acc = [], 0.0
+        if cur:
+            chunks.append(np.sort(np.array(cur)))
+        reps, tc, snps_done = 0, 0.0, 0
+        cmp_got, cmp_ref = [], []
+        full_once = False
+        i = 0
         while tc < args.cpu_seconds and reps < 50:
+            if i >= len(chunks):
+                full_once, i = True, 0
+            blocks = chunks[i]
+            i += 1
+            sub, s_idx, l_idx = sub_problem(prob, blocks)
             c0 = time.perf_counter()
-            rs, rl, _, _ = O.est(prob.bed, prob.n_ref, prob.n_obs, prob.sigma_s, prob.s_ptr,
-                                 prob.s_pos, prob.z_s, prob.l_ptr, prob.l_pos, prob.z_l,
+            rs, rl, _, _ = O.est(sub.bed, sub.n_ref, sub.n_obs, sub.sigma_s, sub.s_ptr,
+                                 sub.s_pos, sub.z_s, sub.l_ptr, sub.l_pos, sub.z_l,
                                  tau=prob.tau, method="pcg", threads=thr)
             tc += time.perf_counter() - c0
-            reps += 1
-        cpu = dict(value=wl["snps"] * reps / tc, unit="SNPs/s", cores=thr, kind="port",
-                   sample=f"full workload x{reps} ({tc:.1f} s): C restatement of the reference "
+            snps_done += len(s_idx) + len(l_idx)
+            if not full_once:
+                cmp_ref.append(np.concatenate([rs, rl]))
+                cmp_got.append(np.concatenate([beta_s[s_idx], beta_l[l_idx]]))
+            if i >= len(chunks):
+                reps += 1
+        what = (f"full workload x{reps}+" if reps else
+                f"{snps_done} of {int(wl['snps'])} SNPs (random block subset"
+                f"{f', {skipped} largest blocks excluded' if skipped else ''})")
+        cpu = dict(value=snps_done / tc, unit="SNPs/s", cores=thr, kind="port",
+                   sample=f"{what} in {tc:.1f} s: C restatement of the reference "
                           f"(byte-wise readSNPIm, N-1 standardise, {'OpenBLAS dsyrk/dgemm/dgemv' if blas else 'plain-loop Gram'}, "
                           f"Jacobi-PCG tol 1e-7), OpenMP over blocks x{thr}, BLAS 1 thread")
-        ref = np.concatenate([rs, rl])
-        got = np.concatenate([beta_s, beta_l])
+        ref = np.concatenate(cmp_ref)
+        got = np.concatenate(cmp_got)
         ok = np.isfinite(ref)
         dbeta = dict(max_abs=float(np.max(np.abs(got[ok] - ref[ok]))),
                      normwise=float(np.max(np.abs(got[ok] - ref[ok])) / np.max(np.abs(ref[ok]))),
+                     snps_compared=int(ok.sum()),
                      vs="CPU reference-faithful PCG (oracle)")
 
     if rank == 0:
@@ -175,7 +232,7 @@ def main():
             "data": "synthetic (AR(1)-LD PLINK panel, seed = 1 + rank)",
             "config": {"workload": f"synthetic {args.snps} SNP x {args.n_ref} indiv, 22 chr "
                                    f"{args.pop} LD blocks, {'LMM-only' if args.lmm_only else 'DBSLMM large+small'}, "
-                                   f"h2=0.5 (BASELINE configs[1])",
+                                   f"h2=0.5 (BASELINE configs[{args.config - 1}])", "generator": args.gen,
                        "snps_per_gpu": wl["snps"], "n_ref": args.n_ref, "blocks": wl["blocks"],
                        "gram": "exact int8 dosages on v_mfma_i32_32x32x32_i8, fp64 epilogue",
                        "solve": "fp64 Cholesky of the joint per-block matrix",

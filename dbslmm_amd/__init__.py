@@ -19,7 +19,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (BLOCK_EMPTY, BLOCK_MONOMORPHIC, BLOCK_NOT_PD, BLOCK_OK, KERNEL_NAMES,
+from ._lib import (WORKLOAD_LEN, BLOCK_EMPTY, BLOCK_MONOMORPHIC, BLOCK_NOT_PD, BLOCK_OK, KERNEL_NAMES,
                    DbslmmError)
 
 __all__ = ["Context", "Plan", "DBSLMMFIT", "BlockProblem", "bed_maf", "read_snp_std",
@@ -136,11 +136,11 @@ class Plan:
         return out, int(n[0])
 
     def workload(self) -> dict:
-        w = np.zeros(10)
+        w = np.zeros(WORKLOAD_LEN)
         self.ctx.check(self.ctx.lib.dbslmm_plan_workload(self.h, _ptr(w)), "plan_workload")
         keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
                 "gram_ops_exec", "chol_flops_large", "blocks", "gram_tiles", "chol_flops_small",
-                "blocks_large")
+                "blocks_large", "chol_flops_tiled", "blocks_tiled", "tiled_launches")
         return dict(zip(keys, w.tolist()))
 
     def download(self):

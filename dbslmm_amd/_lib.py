@@ -20,8 +20,11 @@ EXPORTS = (
     "dbslmm_bed_maf", "dbslmm_read_snp_std",
 )
 
-K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL = 0, 1, 2, 3
-KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small")
+ABI_VERSION = 2
+K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
+KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
+                "dbslmm_tchol")
+WORKLOAD_LEN = 13
 BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC = 0, 1, 2, 3
 
 
@@ -71,7 +74,7 @@ def load(path: str | None = None):
     L.dbslmm_plan_workload.argtypes = [V, V]
     L.dbslmm_bed_maf.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int64, V]
     L.dbslmm_read_snp_std.argtypes = [V, V, C.c_int64, C.c_int32, V, C.c_int32, V, V]
-    if L.dbslmm_abi_version() != 1:
+    if L.dbslmm_abi_version() != ABI_VERSION:
         raise DbslmmError("ABI version mismatch")
     _lib = L
     return L

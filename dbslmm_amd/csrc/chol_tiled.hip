@@ -1,0 +1,309 @@
+// chol_tiled.hip -- multi-workgroup Cholesky + solves for the big LD blocks (included by plan.hip
+// after chol.hip).  Same bordered system as chol.hip (z appended as row m, y = L^{-1} z left in
+// row m, beta = L^{-T} y / sqrt n), but every block with m >= the tiled threshold is spread over
+// many workgroups, batched across blocks, one launch per phase of a 64-wide panel step:
+//
+//   tchol_diag0          step 0 only: factor + invert diagonal tile (0, 0)
+//   tchol_panel(k)       L_ik = A_ik X_kk^T for every tile row i > k     (one workgroup per tile)
+//   tchol_trailing(k)    C_ij -= L_ik L_jk^T, k < j <= i, except (k+1, k+1) (one workgroup/tile)
+//   tchol_diag(k)        lookahead, concurrently on a 4th stream: update tile (k+1, k+1) and
+//                        factor + invert it (its 256 VGPRs stay out of the trailing kernel)
+//   tchol_backward(J)    x_J = X_JJ^T v_J, v_{<J} -= L_{J,<J}^T x_J        (one workgroup per
+//                        256 columns; x_J recomputed per workgroup, v_J is read-only in a launch)
+//
+// A 64 x 64 diagonal tile is factored as 2 x 2 tiles of 32 by chol::factor_diag:
+//   L00, X00 = L00^{-1};  L10 = A10 X00^T;  A11 -= L10 L10^T;  L11, X11;  X10 = -X11 L10 X00
+// and stored as: strict lower = L, diagonal + upper (r, c >= r) = X[c][r] (X = L_kk^{-1}).
+//
+// Work lists are per step: the blocks active at that step and the prefix of their work-item
+// counts; a workgroup finds its block by binary search (no per-item tables).
+namespace chol {
+
+constexpr int kBT = 64;                          // tiled-path tile edge (= panel width)
+constexpr int kSub = kT * kTS;                   // one 32x32 LDS sub-tile (stride 34)
+// LDS carve of the tiled kernels (doubles): 8 sub-tiles = two 64x64 operands
+constexpr int kTiledDoubles = 8 * kSub + 2 * kT + 8;
+
+struct TiledArgs {
+    double* M;
+    const int32_t* blk_row0;
+    const int32_t* blk_m;
+    const int32_t* blk_ms;
+    const int32_t* blk_ld;
+    const int64_t* blk_matoff;
+    const int32_t* blk_id;
+    const double* z_slot;
+    const int32_t* slot_out;
+    const double* rsd;
+    double dshift;
+    double inv_sqrt_n;
+    double* y;
+    double* beta_s;
+    double* beta_l;
+    int32_t* status;
+};
+
+// work list of one launch: act[0..n) = plan block indices, pfx[0..n] = prefix of item counts
+__device__ __forceinline__ int find_item(const int32_t* pfx, int n, int item) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pfx[mid] <= item) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void acc_to_lds_t(const v4d (&acc)[2][2], double* W, int lane) {
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                W[(16 * sj + (lane & 15)) * kTS + 16 * si + (lane >> 4) + 4 * q] = acc[si][sj][q];
+}
+
+__device__ __forceinline__ void zero_acc(v4d (&acc)[2][2]) {
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj) acc[si][sj] = v4d{0.0, 0.0, 0.0, 0.0};
+}
+
+// Wave-level factorisation + inversion of the 64x64 diagonal tile at (c0, c0) (rows <= m).
+// lds: >= 6 sub-tiles + 2*kT.  Returns true when a pivot was not positive.
+__device__ __forceinline__ bool factor_diag64(double* A, int ld, int c0, int m, int ms, double dshift,
+                              double* lds, int lane) {
+    double* Xl = lds;                 // X00, later X11
+    double* Lb = lds + kSub;
+    double* L10 = lds + 2 * kSub;
+    double* XT = lds + 3 * kSub;      // X00^T
+    double* TT = lds + 4 * kSub;      // (L10 X00)^T
+    double* W = lds + 5 * kSub;
+    double* colb = lds + 6 * kSub;
+    bool fail = factor_diag(A, ld, c0, m, ms, dshift, Xl, Lb, colb, lane, false);
+    if (c0 + kT > m) return fail;     // the tile ends inside its first half
+    // X00^T, A10 -> LDS
+    for (int e = lane; e < kT * kT; e += kWave) {
+        const int q = e >> 5, r = e & 31;
+        XT[r * kTS + q] = Xl[q * kTS + r];
+    }
+    stage_tile(W, A, ld, c0 + kT, c0, lane);
+    wave_sync();
+    v4d acc[2][2];
+    zero_acc(acc);
+    mfma_tile(acc, W, Xl, 1.0, lane);                  // L10 = A10 X00^T
+    store_acc(acc, A, ld, c0 + kT, c0, lane);
+    acc_to_lds(acc, L10, lane);
+    wave_sync();
+    v4d c11[2][2];
+    load_acc(c11, A, ld, c0 + kT, c0 + kT, lane);
+    mfma_tile(c11, L10, L10, -1.0, lane);              // A11 -= L10 L10^T
+    acc_to_lds(c11, Lb, lane);
+    wave_sync();
+    fail |= factor_diag(A, ld, c0 + kT, m, ms, dshift, Xl, Lb, colb, lane, true);   // Xl = X11
+    zero_acc(acc);
+    mfma_tile(acc, L10, XT, 1.0, lane);                // T = L10 X00
+    acc_to_lds_t(acc, TT, lane);
+    wave_sync();
+    zero_acc(acc);
+    mfma_tile(acc, Xl, TT, -1.0, lane);                // X10 = -X11 T
+    // X10^T -> sub-tile (0, 1): element (r, 32 + c) = X10[c][r]
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int R = 16 * si + (lane >> 4) + 4 * q, Cc = 16 * sj + (lane & 15);
+                A[static_cast<int64_t>(c0 + Cc) * ld + c0 + kT + R] = acc[si][sj][q];
+            }
+    return fail;
+}
+
+// 64x64 tile (r0, c0) -> 4 LDS sub-tiles: S[2a + b] = rows 32a.., cols 32b..
+__device__ __forceinline__ void stage64(double* S, const double* A, int ld, int r0, int c0, int tid) {
+    constexpr int NT = kLargeThreads;
+    double v[kBT * kBT / NT];
+#pragma unroll
+    for (int it = 0; it < kBT * kBT / NT; ++it) {
+        const int e = it * NT + tid;
+        v[it] = A[static_cast<int64_t>(r0 + (e >> 6)) * ld + c0 + (e & 63)];
+    }
+#pragma unroll
+    for (int it = 0; it < kBT * kBT / NT; ++it) {
+        const int e = it * NT + tid;
+        const int r = e >> 6, c = e & 63;
+        S[(2 * (r >> 5) + (c >> 5)) * kSub + (r & 31) * kTS + (c & 31)] = v[it];
+    }
+}
+
+}  // namespace chol
+
+// ---------------------------------------------------------------- kernels
+// step 0: factor + invert tile (0, 0) of each tiled block; flag monomorphic SNPs
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_diag0(
+    chol::TiledArgs a, const int32_t* __restrict__ blocks, int32_t n) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (static_cast<int>(blockIdx.x) >= n) return;
+    const int b = blocks[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b];
+    double* A = a.M + a.blk_matoff[b];
+    for (int c = tid; c < m; c += chol::kLargeThreads)
+        A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];   // z row of the bordered matrix
+    chol::BlockArgs ba{a.blk_row0, a.blk_m, a.blk_ms, a.blk_ld, a.blk_matoff, a.blk_id, a.z_slot,
+                       a.slot_out, a.rsd, a.dshift, a.inv_sqrt_n, a.beta_s, a.beta_l, a.status};
+    __syncthreads();
+    bool fail = false;
+    if (wave == 0) fail = chol::factor_diag64(A, ld, 0, m, a.blk_ms[b], a.dshift, lds, lane);
+    chol::report_status(ba, b, row0, m, tid, chol::kLargeThreads, fail && lane == 0);
+}
+
+// panel of step k: L_ik = A_ik X_kk^T, i = k+1 .. Tz
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_panel(
+    chol::TiledArgs a, int32_t k, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
+    int32_t n) {
+    using namespace chol;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int item = blockIdx.x;
+    if (item >= pfx[n]) return;
+    const int s = find_item(pfx, n, item);
+    const int b = act[s];
+    const int i = k + 1 + (item - pfx[s]);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ld = a.blk_ld[b];
+    double* A = a.M + a.blk_matoff[b];
+    const int c0 = kBT * k;
+    double* X = lds;               // 4 sub-tiles of X (row-major)
+    double* W = lds + 4 * kSub;    // 4 sub-tiles of A_ik
+    // X[q][r] = stored (r, q) for q >= r, else 0
+    for (int e = tid; e < kBT * kBT; e += kLargeThreads) {
+        const int r = e >> 6, q = e & 63;
+        const double v = q >= r ? A[static_cast<int64_t>(c0 + r) * ld + c0 + q] : 0.0;
+        X[(2 * (q >> 5) + (r >> 5)) * kSub + (q & 31) * kTS + (r & 31)] = v;
+    }
+    stage64(W, A, ld, kBT * i, c0, tid);
+    __syncthreads();
+    const int qi = wave >> 1, qj = wave & 1;
+    v4d acc[2][2];
+    zero_acc(acc);
+    mfma_tile(acc, W + (2 * qi + 0) * kSub, X + (2 * qj + 0) * kSub, 1.0, lane);
+    if (qj == 1) mfma_tile(acc, W + (2 * qi + 1) * kSub, X + (2 * qj + 1) * kSub, 1.0, lane);
+    store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);
+}
+
+// trailing update of step k: C_ij -= L_ik L_jk^T for every pair except the diagonal tile
+// (k+1, k+1), which dbslmm_tchol_diag updates and factors concurrently on another stream.
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_trailing(
+    chol::TiledArgs a, int32_t k, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
+    int32_t n) {
+    using namespace chol;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int item = blockIdx.x;
+    if (item >= pfx[n]) return;
+    const int s = find_item(pfx, n, item);
+    const int b = act[s];
+    const int m = a.blk_m[b], ld = a.blk_ld[b];
+    const int T = (m + kBT - 1) / kBT, Tz = m / kBT;
+    const int nJ = T - 1 - k, tri_n = nJ * (nJ + 1) / 2;
+    int I, J;
+    decode_pair(item - pfx[s] + 1, tri_n, k, Tz, I, J);   // pair 0 is the diagonal tile
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* A = a.M + a.blk_matoff[b];
+    const int c0 = kBT * k;
+    double* LI = lds;
+    double* LJ = lds + 4 * kSub;
+    stage64(LI, A, ld, kBT * I, c0, tid);
+    if (I != J) stage64(LJ, A, ld, kBT * J, c0, tid);
+    else LJ = LI;
+    __syncthreads();
+    const int qi = wave >> 1, qj = wave & 1;
+    if (I == J && qj > qi) return;
+    v4d acc[2][2];
+    const int r0 = kBT * I + kT * qi, cc0 = kBT * J + kT * qj;
+    load_acc(acc, A, ld, r0, cc0, lane);
+    mfma_tile(acc, LI + (2 * qi) * kSub, LJ + (2 * qj) * kSub, -1.0, lane);
+    mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJ + (2 * qj + 1) * kSub, -1.0, lane);
+    store_acc(acc, A, ld, r0, cc0, lane);
+}
+
+// lookahead of step k: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, then factor + invert it
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_diag(
+    chol::TiledArgs a, int32_t k, const int32_t* __restrict__ act, int32_t n) {
+    using namespace chol;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (static_cast<int>(blockIdx.x) >= n) return;
+    const int b = act[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = a.blk_m[b], ld = a.blk_ld[b];
+    double* A = a.M + a.blk_matoff[b];
+    const int d0 = kBT * (k + 1);
+    stage64(lds, A, ld, d0, kBT * k, tid);
+    __syncthreads();
+    const int qi = wave >> 1, qj = wave & 1;
+    if (qj <= qi) {
+        v4d acc[2][2];
+        load_acc(acc, A, ld, d0 + kT * qi, d0 + kT * qj, lane);
+        mfma_tile(acc, lds + (2 * qi) * kSub, lds + (2 * qj) * kSub, -1.0, lane);
+        mfma_tile(acc, lds + (2 * qi + 1) * kSub, lds + (2 * qj + 1) * kSub, -1.0, lane);
+        store_acc(acc, A, ld, d0 + kT * qi, d0 + kT * qj, lane);
+    }
+    __syncthreads();                  // the updated tile is in global memory
+    if (wave != 0) return;
+    const bool fail = factor_diag64(A, ld, d0, m, a.blk_ms[b], a.dshift, lds, lane);
+    if (fail && lane == 0) atomicMax(a.status + a.blk_id[b], DBSLMM_BLOCK_NOT_PD);
+}
+
+// backward step J: x_J = X_JJ^T v_J; v[c] -= sum_r L[J*64 + r][c] x_J[r] for c < 64 J.
+// v lives in y[row0 ..]; at a block's first backward step (J = T-1) v is read from row m.
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_backward(
+    chol::TiledArgs a, int32_t J, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
+    int32_t n) {
+    using namespace chol;
+    __shared__ double xs[kBT];
+    __shared__ double red[4][kBT];
+    const int item = blockIdx.x;
+    if (item >= pfx[n]) return;
+    const int s = find_item(pfx, n, item);
+    const int b = act[s];
+    const int chunk = item - pfx[s];
+    const int tid = threadIdx.x;
+    const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b];
+    const double* A = a.M + a.blk_matoff[b];
+    const int T = (m + kBT - 1) / kBT;
+    const bool first = J == T - 1;
+    const double* zrow = A + static_cast<int64_t>(m) * ld;
+    double* v = a.y + row0;
+    const int c1 = kBT * J, jmax = min(kBT, m - c1);
+    {   // x_J[r] = sum_{c >= r} stored(c1 + r, c1 + c) v_J[c]; 4 groups of 64 threads split c
+        const int r = tid & 63, g = tid >> 6;
+        double acc = 0.0;
+        if (r < jmax)
+            for (int c = r + g; c < jmax; c += 4)
+                acc += A[static_cast<int64_t>(c1 + r) * ld + c1 + c] * (first ? zrow[c1 + c] : v[c1 + c]);
+        red[g][r] = acc;
+    }
+    __syncthreads();
+    if (tid < kBT) xs[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    __syncthreads();
+    const bool fail = a.status[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
+    if (chunk == 0 && tid < jmax) {
+        const double x = xs[tid];
+        const double val = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
+        const int o = a.slot_out[row0 + c1 + tid];
+        if (o >= 0) a.beta_s[o] = val;
+        else a.beta_l[-1 - o] = val;
+    }
+    const int c = chunk * kLargeThreads + tid;
+    if (c < c1) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int r = 0; r + 1 < jmax; r += 2) {
+            s0 += A[static_cast<int64_t>(c1 + r) * ld + c] * xs[r];
+            s1 += A[static_cast<int64_t>(c1 + r + 1) * ld + c] * xs[r + 1];
+        }
+        if (jmax & 1) s0 += A[static_cast<int64_t>(c1 + jmax - 1) * ld + c] * xs[jmax - 1];
+        v[c] = (first ? zrow[c] : v[c]) - (s0 + s1);
+    }
+}

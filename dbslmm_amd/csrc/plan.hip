@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -27,12 +28,25 @@
 // The kernels are compiled in this translation unit (no relocatable device code needed).
 #include "kernels.hip"
 #include "chol.hip"
+#include "chol_tiled.hip"
 
 namespace {
 // events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large
-// (main stream), [4] / [5] around chol_small (second stream)
-constexpr int kEvPerRun = 6;
+// (main stream), [4] / [5] around chol_small (second stream), [6] / [7] around the tiled
+// sequence (third stream)
+constexpr int kEvPerRun = 8;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
+constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
+constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
+
+// one launch of the tiled sequence: the active blocks and the prefix of their work items
+struct TLaunch {
+    int kind;         // 0 diag0, 1 panel, 2 trailing, 3 backward, 4 diag (lookahead, 4th stream)
+    int step;
+    int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
+    int32_t n;
+    int32_t items;    // workgroups
+};
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 }  // namespace
@@ -41,7 +55,9 @@ struct dbslmm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // main stream (unpack, gram, large-block Cholesky)
     hipStream_t stream2 = nullptr;   // small-block Cholesky, forked from / joined into `stream`
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t stream3 = nullptr;   // tiled (multi-workgroup) Cholesky sequence
+    hipStream_t stream4 = nullptr;   // its lookahead diagonal factorisations
+    hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr, ev_panel = nullptr, ev_diag = nullptr;
     std::string err;
 };
 
@@ -59,6 +75,9 @@ struct dbslmm_plan {
     double *d_z = nullptr, *d_S = nullptr, *d_mu = nullptr, *d_rsd = nullptr, *d_y = nullptr;
     int32_t *d_flags = nullptr, *d_status = nullptr, *d_order = nullptr, *d_blk_id = nullptr;
     int32_t n_large = 0, n_small = 0;   // Cholesky paths (ld > 64 / ld <= 64); d_order = [large | small]
+    int32_t n_tiled = 0;                // blocks on the multi-workgroup path (not in d_order)
+    int32_t* d_tlist = nullptr;         // work lists of the tiled sequence
+    std::vector<TLaunch> tl;
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
     GramTile* d_tiles = nullptr;
@@ -72,7 +91,7 @@ struct dbslmm_plan {
     bool timing = false;
     std::vector<hipEvent_t> ev;  // kEvPerRun per run
     int runs_pending = 0;
-    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0};
+    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0, 0};
     int32_t ms_runs = 0;
     bool ran = false;
 };
@@ -118,11 +137,28 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_panel, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_diag, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kCholLargeLds)) != hipSuccess) {
+                            static_cast<int>(kCholLargeLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_diag0),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kTiledLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_panel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kTiledLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kTiledLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_diag),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kTiledLds)) != hipSuccess) {
         dbslmm_ctx_destroy(c);
         return DBSLMM_E_HIP;
     }
@@ -135,8 +171,13 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
+    if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
+    if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
+    if (ctx->ev_diag) (void)hipEventDestroy(ctx->ev_diag);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
+    if (ctx->join3) (void)hipEventDestroy(ctx->join3);
     delete ctx;
 }
 
@@ -148,7 +189,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
-                    p->d_M, p->d_beta_s, p->d_beta_l};
+                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -187,7 +228,10 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<int64_t> matoff;
     std::vector<GramTile> tiles;
     int64_t moff = 0;
-    double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0;
+    double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
+    int64_t tiled_min = kTiledMinDefault;
+    if (const char* env = getenv("DBSLMM_TILED_MIN")) tiled_min = std::max<int64_t>(64, atoll(env));
+    std::vector<char> is_tiled;
     for (int b = 0; b < pr->num_block; ++b) {
         const int64_t s0 = pr->s_ptr[b], ms = pr->s_ptr[b + 1] - s0;
         const int64_t l0 = has_l ? pr->l_ptr[b] : 0, ml = has_l ? pr->l_ptr[b + 1] - l0 : 0;
@@ -195,7 +239,10 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         const int64_t m = ms + ml;
         if (m == 0) { p->h_empty.push_back(b); continue; }
         const int nb = static_cast<int>(row0.size());
-        const int64_t ld = round_up(m + 1, kTile);    // + the z row of the bordered matrix
+        const bool tiled = m >= tiled_min;
+        is_tiled.push_back(tiled);
+        // + the z row of the bordered matrix; the tiled path works on 64 x 64 tiles
+        const int64_t ld = round_up(m + 1, tiled ? chol::kBT : kTile);
         row0.push_back(static_cast<int32_t>(slot_pos.size()));
         mv.push_back(static_cast<int32_t>(m));
         msv.push_back(static_cast<int32_t>(ms));
@@ -230,7 +277,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             for (int tj = 0; tj <= ti; ++tj) tiles.push_back({nb, ti, tj, 0});
         ops_alg += static_cast<double>(pr->n_ref) * m * (m + 1);
         ops_exec += 2.0 * p->kpad * kTile * kTile * (T * (T + 1) / 2);
-        (ld > chol::kSmallLd ? chol_flops_large : chol_flops_small) +=
+        (tiled ? chol_flops_tiled : ld > chol::kSmallLd ? chol_flops_large : chol_flops_small) +=
             m * static_cast<double>(m) * m / 3.0 + 2.0 * m * m;
     }
     p->n_nonempty = static_cast<int32_t>(row0.size());
@@ -243,7 +290,61 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<int32_t> order(p->n_nonempty);
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return mv[a] > mv[c]; });
+    order.erase(std::remove_if(order.begin(), order.end(), [&](int b) { return is_tiled[b] != 0; }),
+                order.end());
     for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
+    // tiled sequence: diag0, then per step k panel(k) + trailing(k), then backward(J) descending
+    std::vector<int32_t> tlist;
+    {
+        std::vector<int32_t> tb;
+        int Kmax = 0;
+        for (int b = 0; b < p->n_nonempty; ++b)
+            if (is_tiled[b]) {
+                tb.push_back(b);
+                Kmax = std::max<int>(Kmax, (mv[b] + chol::kBT - 1) / chol::kBT);
+            }
+        p->n_tiled = static_cast<int32_t>(tb.size());
+        auto add = [&](int kind, int step, const std::vector<int32_t>& act,
+                       const std::vector<int32_t>& cnt, int extra) {
+            if (act.empty()) return;
+            TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(act.size()), 0};
+            tlist.insert(tlist.end(), act.begin(), act.end());
+            int32_t acc = 0;
+            tlist.push_back(0);
+            for (int32_t c : cnt) tlist.push_back(acc += c);
+            L.items = acc + extra;
+            p->tl.push_back(L);
+        };
+        if (!tb.empty()) add(0, 0, tb, std::vector<int32_t>(tb.size(), 1), 0);
+        for (int k = 0; k < Kmax; ++k) {
+            std::vector<int32_t> pa, pc, ta, tc, dc;
+            for (int32_t b : tb) {
+                const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
+                if (Tz > k) { pa.push_back(b); pc.push_back(Tz - k); }
+                const int nJ = T - 1 - k;
+                if (nJ > 0) {
+                    const int npairs = nJ * (nJ + 1) / 2 + (Tz == T ? nJ : 0);
+                    ta.push_back(b);
+                    dc.push_back(1);
+                    tc.push_back(npairs - 1);     // the diagonal pair goes to tchol_diag
+                }
+            }
+            add(1, k, pa, pc, 0);
+            add(4, k, ta, dc, 0);
+            add(2, k, ta, tc, 0);
+        }
+        for (int J = Kmax - 1; J >= 0; --J) {
+            std::vector<int32_t> ba, bc;
+            for (int32_t b : tb) {
+                const int T = (mv[b] + chol::kBT - 1) / chol::kBT;
+                if (T > J) {
+                    ba.push_back(b);
+                    bc.push_back(std::max(1, (chol::kBT * J + chol::kLargeThreads - 1) / chol::kLargeThreads));
+                }
+            }
+            add(3, J, ba, bc, 0);
+        }
+    }
     const double n_snp = static_cast<double>(p->n_s + p->n_l);
     p->wl[0] = n_snp;
     p->wl[1] = n_snp * bps;
@@ -255,6 +356,9 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[7] = p->n_tiles;
     p->wl[8] = chol_flops_small;
     p->wl[9] = p->n_large;
+    p->wl[10] = chol_flops_tiled;
+    p->wl[11] = p->n_tiled;
+    p->wl[12] = static_cast<double>(p->tl.size());
 
     // ---- device allocations
     hipError_t e = hipSetDevice(ctx->device);
@@ -281,6 +385,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_blk_id, blk_id)) != hipSuccess) return fail("upload blocks");
     if ((e = dev_upload(&p->d_order, order)) != hipSuccess) return fail("upload order");
     if ((e = dev_upload(&p->d_tiles, tiles)) != hipSuccess) return fail("upload tiles");
+    if ((e = dev_upload(&p->d_tlist, tlist)) != hipSuccess) return fail("upload tiled lists");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
     if ((e = hipMalloc(&p->d_mu, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -316,7 +421,7 @@ static int collect_timing(dbslmm_plan* p) {
     dbslmm_ctx* ctx = p->ctx;
     for (int r = 0; r < p->runs_pending; ++r) {
         hipEvent_t* e = &p->ev[kEvPerRun * r];
-        const int from[DBSLMM_K_COUNT] = {0, 1, 2, 4}, to[DBSLMM_K_COUNT] = {1, 2, 3, 5};
+        const int from[DBSLMM_K_COUNT] = {0, 1, 2, 4, 6}, to[DBSLMM_K_COUNT] = {1, 2, 3, 5, 7};
         for (int k = 0; k < DBSLMM_K_COUNT; ++k) {
             float ms = 0.f;
             HIP_TRY(ctx, hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
@@ -369,9 +474,50 @@ int dbslmm_plan_run(dbslmm_plan* p) {
     if (p->n_nonempty > 0) {
         const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
-        // fork: small blocks on stream2 while the large blocks run on the main stream
+        // fork: small blocks on stream2 and tiled blocks on stream3 while the large blocks run
+        // on the main stream
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream3, ctx->fork, 0));
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream3));
+        if (!p->tl.empty()) {
+            const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
+                                     p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn,
+                                     p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
+            hipStream_t s3 = ctx->stream3, s4 = ctx->stream4;
+            bool diag_pending = false;
+            for (const TLaunch& L : p->tl) {
+                if (L.items == 0) continue;
+                if (L.kind == 1 && diag_pending) {        // panel(k) needs diag(k-1) on stream4
+                    HIP_TRY(ctx, hipStreamWaitEvent(s3, ctx->ev_diag, 0));
+                    diag_pending = false;
+                }
+                if (L.kind == 3 && diag_pending) {
+                    HIP_TRY(ctx, hipStreamWaitEvent(s3, ctx->ev_diag, 0));
+                    diag_pending = false;
+                }
+                const int32_t* act = p->d_tlist + L.off;
+                const int32_t* pfx = act + L.n;
+                const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
+                switch (L.kind) {
+                case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, s3, ta, act, L.n); break;
+                case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, s3, ta, L.step, act, pfx, L.n); break;
+                case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, s3, ta, L.step, act, pfx, L.n); break;
+                case 4:
+                    HIP_TRY(ctx, hipEventRecord(ctx->ev_panel, s3));
+                    HIP_TRY(ctx, hipStreamWaitEvent(s4, ctx->ev_panel, 0));
+                    hipLaunchKernelGGL(dbslmm_tchol_diag, g, blk, kTiledLds, s4, ta, L.step, act, L.n);
+                    HIP_TRY(ctx, hipEventRecord(ctx->ev_diag, s4));
+                    diag_pending = true;
+                    break;
+                default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, s3, ta, L.step, act, pfx, L.n); break;
+                }
+            }
+            if (diag_pending) HIP_TRY(ctx, hipStreamWaitEvent(s3, ctx->ev_diag, 0));
+            HIP_TRY(ctx, hipGetLastError());
+        }
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream3));
+        HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream3));
         if (p->n_large > 0) {
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M, p->d_order, p->n_large, p->d_row0, p->d_m,
@@ -393,11 +539,14 @@ int dbslmm_plan_run(dbslmm_plan* p) {
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
         HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
         HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
+        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join3, 0));
     }
     else if (ev) {   // no blocks: keep the event set complete
         HIP_TRY(ctx, hipEventRecord(ev[3], s));
         HIP_TRY(ctx, hipEventRecord(ev[4], s));
         HIP_TRY(ctx, hipEventRecord(ev[5], s));
+        HIP_TRY(ctx, hipEventRecord(ev[6], s));
+        HIP_TRY(ctx, hipEventRecord(ev[7], s));
     }
     p->ran = true;
     return DBSLMM_OK;

@@ -75,7 +75,9 @@ class SynthPanel:
 def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), seed: int = 1,
              rho: float = 0.9, miss_rate: float = 0.0, large_every: int = 20,
              large_z: float = 8.0, n_obs: int = 100000, h2: float = 0.5,
-             block_limit: int | None = None) -> SynthPanel:
+             block_limit: int | None = None, engine: str = "numpy", device: int = 0) -> SynthPanel:
+    """engine "numpy" (CPU, used by the parity fixtures) or "gpu" (libdbslmm_synth.so, same model
+    with a counter-hash RNG; for the 500k-1M SNP scale configs)."""
     rng = np.random.default_rng(seed)
     blocks = read_blocks(pop, chroms)
     if block_limit is not None:
@@ -114,13 +116,20 @@ def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), se
     af = rng.uniform(0.05, 0.5, size=m)
     thr = ndtri(af).astype(np.float32)
     nb = (n_ref + 3) // 4
-    rows = np.empty((m, nb), dtype=np.uint8)
+    bed = np.empty(3 + m * nb, dtype=np.uint8)
+    bed[:3] = np.frombuffer(BED_MAGIC, dtype=np.uint8)
+    rows = bed[3:].reshape(m, nb)
     a = np.float32(math.sqrt(1.0 - rho * rho))
     # AR(1) along the SNPs of each block, 2 haplotypes per individual
     bounds = np.flatnonzero(np.diff(blk)) + 1
     starts = np.concatenate([[0], bounds])
     ends = np.concatenate([bounds, [m]])
     chunk = 4096
+    if engine == "gpu":
+        _gpu_rows(rows, starts, ends, thr, n_ref, seed, rho, miss_rate, device)
+        starts = ends = []
+    elif engine != "numpy":
+        raise ValueError(f"engine {engine!r}")
     for s0, e0 in zip(starts, ends):
         for c0 in range(s0, e0, chunk):
             c1 = min(e0, c0 + chunk)
@@ -138,7 +147,6 @@ def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), se
             if miss_rate > 0:
                 dos[rng.random(dos.shape) < miss_rate] = -1
             rows[c0:c1] = pack_dosages(dos)
-    bed = np.concatenate([np.frombuffer(BED_MAGIC, dtype=np.uint8), rows.reshape(-1)])
     z = rng.standard_normal(m)
     large = np.zeros(m, dtype=bool)
     if large_every:
@@ -149,6 +157,23 @@ def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), se
                 large[j] = True
                 z[j] = large_z * (1 if rng.random() < 0.5 else -1)
     return SynthPanel(n_ref, blocks, chrom, ps, blk, af, bed, z, large, n_obs, h2)
+
+
+def _gpu_rows(rows, starts, ends, thr, n_ref, seed, rho, miss_rate, device):
+    import ctypes as C
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdbslmm_synth.so")
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not built (make -C dbslmm_amd/csrc)")
+    L = C.CDLL(path)
+    L.dbslmm_synth_bed.argtypes = [C.c_int, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
+                                   C.c_uint64, C.c_float, C.c_float, C.c_void_p]
+    L.dbslmm_synth_last_error.restype = C.c_char_p
+    ptr = np.ascontiguousarray(np.concatenate([starts, ends[-1:]]).astype(np.int64))
+    thr = np.ascontiguousarray(thr, dtype=np.float32)
+    rc = L.dbslmm_synth_bed(device, len(starts), ptr.ctypes.data, thr.ctypes.data, n_ref, seed,
+                            rho, miss_rate, rows.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("dbslmm_synth_bed: " + L.dbslmm_synth_last_error().decode())
 
 
 def make_problem(panel: SynthPanel, lmm_only: bool = False, tau: float = 0.8):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 1
+#define DBSLMM_ABI_VERSION 2
 
 enum {
     DBSLMM_OK = 0,
@@ -85,10 +85,14 @@ typedef struct dbslmm_problem {
 enum {
     DBSLMM_K_UNPACK = 0,      /* dbslmm_unpack_stats: 2-bit .bed rows -> int8 dosages + stats */
     DBSLMM_K_GRAM = 1,        /* dbslmm_gram_i8: i8-MFMA grouped syrk + fp64 standardising epilogue */
-    DBSLMM_K_CHOL_LARGE = 2,  /* dbslmm_chol_large: blocks with > 63 SNPs, one workgroup each */
+    DBSLMM_K_CHOL_LARGE = 2,  /* dbslmm_chol_large: blocks with 64 <= m+1 and m below the tiled
+                                 threshold, one workgroup each */
     DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
                                  (runs concurrently with CHOL_LARGE on a second stream) */
-    DBSLMM_K_COUNT = 4
+    DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold (env
+                                 DBSLMM_TILED_MIN, default 512), many workgroups per block,
+                                 one launch per panel phase (third stream); the whole sequence */
+    DBSLMM_K_COUNT = 5
 };
 
 int dbslmm_abi_version(void);
@@ -125,8 +129,9 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * [2] int8 bytes written by the unpack, [3] Gram int8 ops (2 per MAC, algorithmic
  * sum_b n_ref*m_b*(m_b+1)), [4] Gram ops as executed on padded tiles, [5] Cholesky+solve fp64
  * flops of the large blocks (sum_b m_b^3/3 + 2 m_b^2), [6] non-empty blocks, [7] gram tiles,
- * [8] the same fp64 flops for the small blocks, [9] large blocks. */
-#define DBSLMM_WORKLOAD_LEN 10
+ * [8] the same fp64 flops for the small blocks, [9] large blocks, [10] the same fp64 flops for
+ * the tiled blocks, [11] tiled blocks, [12] launches of the tiled sequence per run. */
+#define DBSLMM_WORKLOAD_LEN 13
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
 
 /* MAF pass: maf[r] for every bed row r < n_snp (readSNPIm with an all-ones indicator). */

@@ -39,8 +39,14 @@ def test_python_binding_lists_all_exports():
 
 def test_library_loads_and_reports_abi():
     from dbslmm_amd import _lib
+    import re
     L = _lib.load()
-    assert L.dbslmm_abi_version() == 1
+    hdr = open(os.path.join(ROOT, "include", "dbslmm_hip.h")).read()
+    ver = int(re.search(r"#define DBSLMM_ABI_VERSION (\d+)", hdr).group(1))
+    assert L.dbslmm_abi_version() == ver == _lib.ABI_VERSION
+    n = int(re.search(r"#define DBSLMM_WORKLOAD_LEN (\d+)", hdr).group(1))
+    assert n == _lib.WORKLOAD_LEN
+    assert len(_lib.KERNEL_NAMES) == int(re.search(r"DBSLMM_K_COUNT = (\d+)", hdr).group(1))
 
 
 def test_kernels_are_gfx950_code_objects():

@@ -1,0 +1,116 @@
+"""GPU parity of the multi-workgroup ("tiled") Cholesky path against the oracle's direct solve
+and against the single-workgroup path (the path is chosen per block by m >= DBSLMM_TILED_MIN).
+
+Block sizes put the z row (row m of the bordered matrix) at every position that matters inside
+its 64-row tile: m % 64 in {0, 1, 31, 32, 33, 63}, alone in its own tile (m % 64 == 0), plus
+blocks with large-effect SNPs and a monomorphic SNP."""
+import numpy as np
+import pytest
+
+import oracle as O
+from _common import normwise
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [128, 129, 159, 160, 161, 191, 192, 575, 640, 703, 1000]
+
+
+def _problem(seed=11, n_ref=256, with_large=True, mono_block=None):
+    from dbslmm_amd import BlockProblem, synth
+    total = sum(SIZES)
+    p = synth.simulate(total + 50, n_ref, pop="EUR", chroms=[1, 2], seed=seed, miss_rate=0.002,
+                       large_every=0)
+    rng = np.random.default_rng(seed)
+    rows = np.arange(total)
+    bid = np.repeat(np.arange(len(SIZES)), SIZES)
+    large = np.zeros(total, dtype=bool)
+    if with_large:
+        for b in range(1, len(SIZES), 2):
+            idx = np.flatnonzero(bid == b)
+            large[rng.choice(idx, size=1 + b % 3, replace=False)] = True
+    z = rng.standard_normal(total)
+    z[large] = 6.0 * np.sign(z[large])
+    bed = p.bed.copy()
+    if mono_block is not None:
+        j = int(np.flatnonzero(bid == mono_block)[5])
+        nb = (n_ref + 3) // 4
+        bed[3 + j * nb: 3 + (j + 1) * nb] = 0xFF
+    nbk = len(SIZES)
+
+    def csr(mask):
+        idx = np.flatnonzero(mask)
+        ptr = np.zeros(nbk + 1, dtype=np.int64)
+        np.add.at(ptr, bid[idx] + 1, 1)
+        return np.cumsum(ptr), rows[idx].astype(np.int32), z[idx]
+    s_ptr, s_pos, z_s = csr(~large)
+    kw = {}
+    if with_large:
+        l_ptr, l_pos, z_l = csr(large)
+        kw = dict(l_ptr=l_ptr, l_pos=l_pos, z_l=z_l)
+    return BlockProblem(bed=bed, n_ref=n_ref, n_obs=100000, sigma_s=0.5 / total, s_ptr=s_ptr,
+                        s_pos=s_pos, z_s=z_s, **kw)
+
+
+def _solve(prob, tiled_min, monkeypatch):
+    from dbslmm_amd import DBSLMMFIT
+    monkeypatch.setenv("DBSLMM_TILED_MIN", str(tiled_min))
+    bs, bl, st = DBSLMMFIT(0).est(prob)
+    return np.concatenate([bs, bl]), st
+
+
+def _oracle(prob):
+    O.use_blas(True)
+    bs, bl, st, _ = O.est(prob.bed, prob.n_ref, prob.n_obs, prob.sigma_s, prob.s_ptr, prob.s_pos,
+                          prob.z_s, prob.l_ptr, prob.l_pos, prob.z_l, tau=prob.tau,
+                          method="direct", threads=8)
+    return np.concatenate([bs, bl]), st
+
+
+@pytest.mark.parametrize("with_large", [True, False])
+def test_tiled_matches_oracle_and_single_workgroup(monkeypatch, with_large):
+    prob = _problem(with_large=with_large)
+    ref, _ = _oracle(prob)
+    tiled, st_t = _solve(prob, 64, monkeypatch)          # every block on the tiled path
+    single, st_s = _solve(prob, 10 ** 9, monkeypatch)    # none
+    assert np.all(np.isfinite(tiled))
+    assert np.all(st_t == 0) and np.all(st_s == 0)
+    assert normwise(tiled, ref) < 1e-10
+    assert normwise(tiled, single) < 1e-11
+    # per block as well (small blocks must not hide behind the big ones' scale)
+    off = 0
+    for b, m in enumerate(SIZES):
+        ms = int(prob.s_ptr[b + 1] - prob.s_ptr[b])
+        ml = m - ms
+        sl = np.r_[prob.s_ptr[b]:prob.s_ptr[b + 1]]
+        assert normwise(tiled[sl], ref[sl]) < 1e-9, (b, m)
+        if prob.l_ptr is not None and ml:
+            ll = prob.n_s + np.r_[prob.l_ptr[b]:prob.l_ptr[b + 1]]
+            assert normwise(tiled[ll], ref[ll]) < 1e-9, (b, m)
+        off += m
+
+
+def test_tiled_monomorphic_block_is_nan(monkeypatch):
+    prob = _problem(mono_block=8)
+    tiled, st = _solve(prob, 64, monkeypatch)
+    sl = np.r_[prob.s_ptr[8]:prob.s_ptr[9]]
+    assert st[8] == 3
+    assert np.all(np.isnan(tiled[sl]))
+    others = np.ones(prob.n_s, dtype=bool)
+    others[sl] = False
+    assert np.all(np.isfinite(tiled[:prob.n_s][others]))
+
+
+def test_tiled_plan_rerun_bit_identical(monkeypatch):
+    from dbslmm_amd import Context, Plan
+    monkeypatch.setenv("DBSLMM_TILED_MIN", "128")
+    prob = _problem(seed=3)
+    plan = Plan(Context(0), prob)
+    wl = plan.workload()
+    assert wl["blocks_tiled"] == len(SIZES) and wl["tiled_launches"] > 0
+    plan.run()
+    a = plan.download()
+    for _ in range(3):
+        plan.run()
+    b = plan.download()
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
