@@ -256,14 +256,41 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_d
     if (fail && lane == 0) atomicMax(a.status + a.blk_id[b], DBSLMM_BLOCK_NOT_PD);
 }
 
-// backward step J: x_J = X_JJ^T v_J; v[c] -= sum_r L[J*64 + r][c] x_J[r] for c < 64 J.
-// v lives in y[row0 ..]; at a block's first backward step (J = T-1) v is read from row m.
+// backward step J (launches J = Kmax-1 .. 0).  v lives in y[row0 ..]; x_J overwrites v_J once
+// it is known.  Workgroup = (block, 256 columns of [0, 64 J)):
+//   x_J: read from y (written by the previous launch) -- or, at a block's first backward step
+//        (J = T-1), computed by every workgroup from the z row;
+//   v[c] -= sum_r L[64 J + r][c] x_J[r]   (column per thread, 64 independent loads);
+//   the workgroup holding tile J-1 then has the final v_{J-1}: it forms x_{J-1} = X^T v_{J-1}
+//   from the stored inverse, writes it over v_{J-1} and scatters beta for tile J-1.
+namespace chol {
+__device__ __forceinline__ void tile_x(const double* A, int ld, int c1, int jmax, const double* vsrc,
+                                       double* D, double* vl, double* red, double* xs, int tid) {
+    // D = stored rows c1.. of the diagonal tile (diagonal + upper = X^T), vl = v_J
+    for (int e = tid; e < kBT * kBT; e += kLargeThreads) {
+        const int r = e >> 6, c = e & 63;
+        D[r * (kBT + 1) + c] = (r < jmax && c < jmax) ? A[static_cast<int64_t>(c1 + r) * ld + c1 + c] : 0.0;
+    }
+    if (tid < kBT) vl[tid] = tid < jmax ? vsrc[c1 + tid] : 0.0;
+    __syncthreads();
+    const int r = tid & 63, g = tid >> 6;
+    double acc = 0.0;
+    for (int c = r + g; c < kBT; c += 4) acc += D[r * (kBT + 1) + c] * vl[c];
+    red[g * kBT + r] = acc;
+    __syncthreads();
+    if (tid < kBT) xs[tid] = (red[tid] + red[kBT + tid]) + (red[2 * kBT + tid] + red[3 * kBT + tid]);
+    __syncthreads();
+}
+}  // namespace chol
+
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_backward(
     chol::TiledArgs a, int32_t J, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
     int32_t n) {
     using namespace chol;
+    __shared__ double D[kBT * (kBT + 1)];
+    __shared__ double vl[kBT];
+    __shared__ double red[4 * kBT];
     __shared__ double xs[kBT];
-    __shared__ double red[4][kBT];
     const int item = blockIdx.x;
     if (item >= pfx[n]) return;
     const int s = find_item(pfx, n, item);
@@ -277,33 +304,42 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_b
     const double* zrow = A + static_cast<int64_t>(m) * ld;
     double* v = a.y + row0;
     const int c1 = kBT * J, jmax = min(kBT, m - c1);
-    {   // x_J[r] = sum_{c >= r} stored(c1 + r, c1 + c) v_J[c]; 4 groups of 64 threads split c
-        const int r = tid & 63, g = tid >> 6;
-        double acc = 0.0;
-        if (r < jmax)
-            for (int c = r + g; c < jmax; c += 4)
-                acc += A[static_cast<int64_t>(c1 + r) * ld + c1 + c] * (first ? zrow[c1 + c] : v[c1 + c]);
-        red[g][r] = acc;
-    }
-    __syncthreads();
-    if (tid < kBT) xs[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-    __syncthreads();
     const bool fail = a.status[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
-    if (chunk == 0 && tid < jmax) {
-        const double x = xs[tid];
+    auto put_beta = [&](int c0, int i, double x) {
         const double val = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
-        const int o = a.slot_out[row0 + c1 + tid];
+        const int o = a.slot_out[row0 + c0 + i];
         if (o >= 0) a.beta_s[o] = val;
         else a.beta_l[-1 - o] = val;
+    };
+    if (first) {
+        tile_x(A, ld, c1, jmax, zrow, D, vl, red, xs, tid);
+        if (chunk == 0 && tid < jmax) put_beta(c1, tid, xs[tid]);
+    } else {
+        if (tid < kBT) xs[tid] = tid < jmax ? v[c1 + tid] : 0.0;
+        __syncthreads();
     }
     const int c = chunk * kLargeThreads + tid;
     if (c < c1) {
-        double s0 = 0.0, s1 = 0.0;
-        for (int r = 0; r + 1 < jmax; r += 2) {
-            s0 += A[static_cast<int64_t>(c1 + r) * ld + c] * xs[r];
-            s1 += A[static_cast<int64_t>(c1 + r + 1) * ld + c] * xs[r + 1];
+        const double* Lc = A + static_cast<int64_t>(c1) * ld + c;
+        double part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (jmax == kBT) {
+#pragma unroll
+            for (int r = 0; r < kBT; ++r) part[r & 7] += Lc[static_cast<int64_t>(r) * ld] * xs[r];
+        } else {
+            for (int r = 0; r < jmax; ++r) part[r & 7] += Lc[static_cast<int64_t>(r) * ld] * xs[r];
         }
-        if (jmax & 1) s0 += A[static_cast<int64_t>(c1 + jmax - 1) * ld + c] * xs[jmax - 1];
-        v[c] = (first ? zrow[c] : v[c]) - (s0 + s1);
+        const double sum = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
+        v[c] = (first ? zrow[c] : v[c]) - sum;
+    }
+    // the workgroup holding tile J-1 finishes it: x_{J-1} over v_{J-1}, beta
+    if (J >= 1 && (c1 - 1) / kLargeThreads == chunk) {
+        __syncthreads();
+        __threadfence_block();
+        const int c0 = c1 - kBT;
+        tile_x(A, ld, c0, kBT, v, D, vl, red, xs, tid);
+        if (tid < kBT) {
+            v[c0 + tid] = xs[tid];
+            put_beta(c0, tid, xs[tid]);
+        }
     }
 }

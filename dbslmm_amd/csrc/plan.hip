@@ -31,9 +31,8 @@
 #include "chol_tiled.hip"
 
 namespace {
-// events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large
-// (main stream), [4] / [5] around chol_small (second stream), [6] / [7] around the tiled
-// sequence (third stream)
+// events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large,
+// [4] / [5] around chol_small (main stream), [6] / [7] around the tiled sequence (stream2)
 constexpr int kEvPerRun = 8;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
@@ -54,9 +53,8 @@ int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 struct dbslmm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // main stream (unpack, gram, large-block Cholesky)
-    hipStream_t stream2 = nullptr;   // small-block Cholesky, forked from / joined into `stream`
-    hipStream_t stream3 = nullptr;   // tiled (multi-workgroup) Cholesky sequence
-    hipStream_t stream4 = nullptr;   // its lookahead diagonal factorisations
+    hipStream_t stream2 = nullptr;   // tiled (multi-workgroup) Cholesky sequence, forked/joined
+    hipStream_t stream3 = nullptr;   // its lookahead diagonal factorisations
     hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr, ev_panel = nullptr, ev_diag = nullptr;
     std::string err;
 };
@@ -78,6 +76,8 @@ struct dbslmm_plan {
     int32_t n_tiled = 0;                // blocks on the multi-workgroup path (not in d_order)
     int32_t* d_tlist = nullptr;         // work lists of the tiled sequence
     std::vector<TLaunch> tl;
+    hipGraphExec_t graph_exec = nullptr;   // captured tiled sequence
+    double graph_dshift = 0.0;
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
     GramTile* d_tiles = nullptr;
@@ -134,11 +134,12 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
     if (device < 0 || device >= n) return DBSLMM_E_ARG;
     auto* c = new dbslmm_ctx();
     c->device = device;
+    int prio_lo = 0, prio_hi = 0;   // the tiled sequence is the critical path: high priority
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess ||
+        hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_panel, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_diag, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
@@ -172,7 +173,6 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
-    if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
     if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
     if (ctx->ev_diag) (void)hipEventDestroy(ctx->ev_diag);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
@@ -193,6 +193,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+    if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
     delete p;
 }
 
@@ -433,6 +434,42 @@ static int collect_timing(dbslmm_plan* p) {
     return DBSLMM_OK;
 }
 
+// Enqueue the tiled sequence on stream2 (lookahead factorisations on stream3, joined back).
+static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
+    dbslmm_ctx* ctx = p->ctx;
+    const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
+                             p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn,
+                             p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
+    hipStream_t st = ctx->stream2, sd = ctx->stream3;
+    bool diag_pending = false;
+    for (const TLaunch& L : p->tl) {
+        if (L.items == 0) continue;
+        if ((L.kind == 1 || L.kind == 3) && diag_pending) {   // needs the lookahead factor
+            HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->ev_diag, 0));
+            diag_pending = false;
+        }
+        const int32_t* act = p->d_tlist + L.off;
+        const int32_t* pfx = act + L.n;
+        const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
+        switch (L.kind) {
+        case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, st, ta, act, L.n); break;
+        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
+        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
+        case 4:
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_panel, st));
+            HIP_TRY(ctx, hipStreamWaitEvent(sd, ctx->ev_panel, 0));
+            hipLaunchKernelGGL(dbslmm_tchol_diag, g, blk, kTiledLds, sd, ta, L.step, act, L.n);
+            HIP_TRY(ctx, hipEventRecord(ctx->ev_diag, sd));
+            diag_pending = true;
+            break;
+        default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
+        }
+    }
+    if (diag_pending) HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->ev_diag, 0));
+    HIP_TRY(ctx, hipGetLastError());
+    return DBSLMM_OK;
+}
+
 int dbslmm_plan_run(dbslmm_plan* p) {
     if (!p) return DBSLMM_E_ARG;
     dbslmm_ctx* ctx = p->ctx;
@@ -474,50 +511,11 @@ int dbslmm_plan_run(dbslmm_plan* p) {
     if (p->n_nonempty > 0) {
         const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
-        // fork: small blocks on stream2 and tiled blocks on stream3 while the large blocks run
-        // on the main stream
+        // fork: the tiled sequence runs on stream2 (its lookahead factorisations on stream3)
+        // while the single-workgroup and single-wave kernels run on the main stream.  A process
+        // gets 4 hardware queues (null stream + these 3), so each of them has its own.
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
-        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream3, ctx->fork, 0));
-        if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream3));
-        if (!p->tl.empty()) {
-            const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
-                                     p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn,
-                                     p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
-            hipStream_t s3 = ctx->stream3, s4 = ctx->stream4;
-            bool diag_pending = false;
-            for (const TLaunch& L : p->tl) {
-                if (L.items == 0) continue;
-                if (L.kind == 1 && diag_pending) {        // panel(k) needs diag(k-1) on stream4
-                    HIP_TRY(ctx, hipStreamWaitEvent(s3, ctx->ev_diag, 0));
-                    diag_pending = false;
-                }
-                if (L.kind == 3 && diag_pending) {
-                    HIP_TRY(ctx, hipStreamWaitEvent(s3, ctx->ev_diag, 0));
-                    diag_pending = false;
-                }
-                const int32_t* act = p->d_tlist + L.off;
-                const int32_t* pfx = act + L.n;
-                const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
-                switch (L.kind) {
-                case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, s3, ta, act, L.n); break;
-                case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, s3, ta, L.step, act, pfx, L.n); break;
-                case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, s3, ta, L.step, act, pfx, L.n); break;
-                case 4:
-                    HIP_TRY(ctx, hipEventRecord(ctx->ev_panel, s3));
-                    HIP_TRY(ctx, hipStreamWaitEvent(s4, ctx->ev_panel, 0));
-                    hipLaunchKernelGGL(dbslmm_tchol_diag, g, blk, kTiledLds, s4, ta, L.step, act, L.n);
-                    HIP_TRY(ctx, hipEventRecord(ctx->ev_diag, s4));
-                    diag_pending = true;
-                    break;
-                default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, s3, ta, L.step, act, pfx, L.n); break;
-                }
-            }
-            if (diag_pending) HIP_TRY(ctx, hipStreamWaitEvent(s3, ctx->ev_diag, 0));
-            HIP_TRY(ctx, hipGetLastError());
-        }
-        if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream3));
-        HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream3));
         if (p->n_large > 0) {
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M, p->d_order, p->n_large, p->d_row0, p->d_m,
@@ -525,20 +523,50 @@ int dbslmm_plan_run(dbslmm_plan* p) {
                                p->d_rsd, dshift, isn, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status);
             HIP_TRY(ctx, hipGetLastError());
         }
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
+        // single-wave blocks: concurrently on stream2 when there is no tiled sequence, else
+        // behind the single-workgroup kernel (each stream keeps its own hardware queue)
+        hipStream_t ss = p->tl.empty() ? ctx->stream2 : s;
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ss));
         if (p->n_small > 0) {
             const unsigned g = static_cast<unsigned>((p->n_small + chol::kSmallWaves - 1) / chol::kSmallWaves);
-            if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ctx->stream2));
             hipLaunchKernelGGL(dbslmm_chol_small, dim3(g), dim3(chol::kSmallWaves * chol::kWave), 0,
-                               ctx->stream2, p->d_M, p->d_order + p->n_large, p->n_small, p->d_row0,
+                               ss, p->d_M, p->d_order + p->n_large, p->n_small, p->d_row0,
                                p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
                                p->d_slot_out, p->d_rsd, dshift, isn, p->d_beta_s, p->d_beta_l,
                                p->d_status);
             HIP_TRY(ctx, hipGetLastError());
         }
-        if (ev) HIP_TRY(ctx, hipEventRecord(ev[5], ctx->stream2));
-        if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
-        HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
-        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[5], ss));
+        if (ss != s) HIP_TRY(ctx, hipEventRecord(ctx->join, ss));
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
+        if (!p->tl.empty()) {
+            // the tiled sequence (~3 launches per 64-column step) is replayed from a graph
+            // captured on first use; re-captured when sigma (a kernel argument) changes
+            if (p->graph_exec && p->graph_dshift != dshift) {
+                (void)hipGraphExecDestroy(p->graph_exec);
+                p->graph_exec = nullptr;
+            }
+            if (!p->graph_exec) {
+                hipGraph_t gr = nullptr;
+                HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
+                const int rc = enqueue_tiled(p, dshift, isn);
+                hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
+                if (rc != DBSLMM_OK) {
+                    if (gr) (void)hipGraphDestroy(gr);
+                    return rc;
+                }
+                HIP_TRY(ctx, ce);
+                hipError_t ie = hipGraphInstantiate(&p->graph_exec, gr, nullptr, nullptr, 0);
+                (void)hipGraphDestroy(gr);
+                HIP_TRY(ctx, ie);
+                p->graph_dshift = dshift;
+            }
+            HIP_TRY(ctx, hipGraphLaunch(p->graph_exec, ctx->stream2));
+        }
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));
+        HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
+        if (ss != s) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
         HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join3, 0));
     }
     else if (ev) {   // no blocks: keep the event set complete

@@ -88,7 +88,7 @@ enum {
     DBSLMM_K_CHOL_LARGE = 2,  /* dbslmm_chol_large: blocks with 64 <= m+1 and m below the tiled
                                  threshold, one workgroup each */
     DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
-                                 (runs concurrently with CHOL_LARGE on a second stream) */
+                                 (concurrent with CHOL_LARGE when there are no tiled blocks) */
     DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold (env
                                  DBSLMM_TILED_MIN, default 512), many workgroups per block,
                                  one launch per panel phase (third stream); the whole sequence */
