@@ -167,27 +167,15 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
 // ------------------------------------------------------------------------------------------
 struct GramTile { int32_t block, ti, tj, pad; };
 
-extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
-    const int8_t* __restrict__ G, int64_t kpad,
-    const GramTile* __restrict__ tiles, int32_t n_tiles,
-    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
-    const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
-    const int32_t* __restrict__ block_flags,
-    const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
-    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int t = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-    if (t >= n_tiles) return;
-    const GramTile tile = tiles[t];
-    const int b = tile.block;
-    const int row0 = blk_row0[b];
-    const int m = blk_m[b];
-    const int ld = blk_ld[b];
-    const int64_t moff = blk_matoff[b];
-    const bool missing = (block_flags[b] & 1) != 0;
-
-    const int8_t* pa = G + static_cast<int64_t>(row0 + kTile * tile.ti + (lane & 31)) * kpad + 16 * (lane >> 5);
-    const int8_t* pb = G + static_cast<int64_t>(row0 + kTile * tile.tj + (lane & 31)) * kpad + 16 * (lane >> 5);
+// One 32 x 32 output tile (rows r0.., cols c0.. of block-local slots) on one wave, K over all
+// kpad individuals with operands straight from G (L2).  missing: the four products GG, GO, OG,
+// OO of the observed-call expansion.
+__device__ __forceinline__ void gram_tile32(
+    const int8_t* __restrict__ G, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
+    int r0, int c0, int lane, const double* __restrict__ S, const double* __restrict__ mu,
+    const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    const int8_t* pa = G + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kpad + 16 * (lane >> 5);
+    const int8_t* pb = G + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kpad + 16 * (lane >> 5);
 
     v16i acc = {0};
     v16i acc_go = {0}, acc_og = {0}, acc_oo = {0};
@@ -236,7 +224,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
 
     // fp64 epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
     const int j = lane & 31;
-    const int lj = kTile * tile.tj + j;
+    const int lj = c0 + j;
     const int sj = row0 + lj;
     const double Sj = lj < m ? S[sj] : 0.0;
     const double muj = lj < m ? mu[sj] : 0.0;
@@ -245,7 +233,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int i = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int li = kTile * tile.ti + i;
+        const int li = r0 + i;
         if (li >= m || lj >= m) continue;
         const int si = row0 + li;
         double c;
@@ -260,6 +248,153 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
         double v = scale * (c * rsd[si] * rj);
         if (li == lj) v += 1.0 - tau;
         M[moff + static_cast<int64_t>(li) * ld + lj] = v;
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
+    const int8_t* __restrict__ G, int64_t kpad,
+    const GramTile* __restrict__ tiles, int32_t n_tiles,
+    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
+    const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
+    const int32_t* __restrict__ block_flags,
+    const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int t = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    if (t >= n_tiles) return;
+    const GramTile tile = tiles[t];
+    const int b = tile.block;
+    gram_tile32(G, kpad, blk_row0[b], blk_m[b], blk_ld[b], blk_matoff[b], (block_flags[b] & 1) != 0,
+                kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M);
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 2b: the same Gram for blocks without missing calls, 128 x 128 output tile per
+// 256-thread workgroup (wave w: 64 x 64 quadrant (w >> 1, w & 1) = 2 x 2 MFMA 32x32x32 i8).
+// K runs in stages of 128 individuals through double-buffered LDS (row stride 144 B: the 16 rows
+// of a ds_read_b128 lane group land on 16 distinct 16-B bank groups); the next stage's global
+// loads are in flight while the current stage's 16 MFMAs per wave run.  Diagonal tiles stage
+// one operand and skip the strictly-upper quadrant.  Tiles come in per-XCD queues (entry e runs
+// on XCD e % 8) so a block's rows stay in one L2; entries with block < 0 are padding.
+// Blocks with a missing call (flag set by the unpack) take the exact 4-product 32 x 32 path.
+// ------------------------------------------------------------------------------------------
+namespace gram {
+constexpr int kGT = 128;                  // output tile edge
+constexpr int kKS = 128;                  // individuals (bytes) per K stage
+constexpr int kRS = kKS + 16;             // LDS row stride (bytes)
+constexpr int kOpBytes = kGT * kRS;       // one operand stage
+constexpr int kLdsBytes = 2 * 2 * kOpBytes;   // 2 stages x (A, B) = 73,728 B
+}  // namespace gram
+
+extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
+    const int8_t* __restrict__ G, int64_t kpad,
+    const GramTile* __restrict__ tiles, int32_t n_tiles,
+    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
+    const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
+    const int32_t* __restrict__ block_flags,
+    const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    using namespace gram;
+    extern __shared__ __attribute__((aligned(16))) int8_t glds[];
+    if (static_cast<int>(blockIdx.x) >= n_tiles) return;
+    const GramTile tile = tiles[blockIdx.x];
+    const int b = tile.block;
+    if (b < 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row0 = blk_row0[b], m = blk_m[b], ld = blk_ld[b];
+    const int64_t moff = blk_matoff[b];
+    const bool diag = tile.ti == tile.tj;
+    if (block_flags[b] & 1) {   // missing calls: 4-product form, 4 x 4 sub-tiles of 32, 4 per wave
+        for (int q = wave; q < 16; q += 4) {
+            const int si = q >> 2, sj = q & 3;
+            if (diag && sj > si) continue;
+            const int r0 = kGT * tile.ti + 32 * si, c0 = kGT * tile.tj + 32 * sj;
+            if (r0 >= m || c0 >= m) continue;
+            gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
+                        tau, M);
+        }
+        return;
+    }
+    const int8_t* ga = G + static_cast<int64_t>(row0 + kGT * tile.ti) * kpad;
+    const int8_t* gb = G + static_cast<int64_t>(row0 + kGT * tile.tj) * kpad;
+    // staging map: 128 rows x 8 chunks of 16 B per operand; thread t moves chunks t + 256 q
+    v4i ra[4], rb[4];
+    auto gload = [&](int64_t k0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = q * 256 + tid, r = e >> 3, c = e & 7;
+            ra[q] = *reinterpret_cast<const v4i*>(ga + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
+            if (!diag) rb[q] = *reinterpret_cast<const v4i*>(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
+        }
+    };
+    auto lstore = [&](int buf) {
+        int8_t* A = glds + buf * 2 * kOpBytes;
+        int8_t* B = A + kOpBytes;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = q * 256 + tid, r = e >> 3, c = e & 7;
+            *reinterpret_cast<v4i*>(A + r * kRS + 16 * c) = ra[q];
+            if (!diag) *reinterpret_cast<v4i*>(B + r * kRS + 16 * c) = rb[q];
+        }
+    };
+    const int wr = wave >> 1, wc = wave & 1;
+    const bool idle = diag && wc > wr;            // strictly-upper quadrant of a diagonal tile
+    v16i acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = v16i{0};
+    const int nst = static_cast<int>(kpad / kKS);
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    // operand read offsets: lane l -> row (l & 31) of a 32-row group, k bytes 16 (l >> 5) of a
+    // 32-byte k-step
+    const int rsub = lane & 31, ksub = 16 * (lane >> 5);
+    for (int st = 0; st < nst; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nst) gload(static_cast<int64_t>(st + 1) * kKS);
+        if (!idle) {
+            const int8_t* A = glds + buf * 2 * kOpBytes;
+            const int8_t* B = diag ? A : A + kOpBytes;
+            const int8_t* pa = A + (64 * wr + rsub) * kRS + ksub;
+            const int8_t* pb = B + (64 * wc + rsub) * kRS + ksub;
+#pragma unroll
+            for (int kk = 0; kk < kKS; kk += 32) {
+                const v4i a0 = *reinterpret_cast<const v4i*>(pa + kk);
+                const v4i a1 = *reinterpret_cast<const v4i*>(pa + 32 * kRS + kk);
+                const v4i b0 = *reinterpret_cast<const v4i*>(pb + kk);
+                const v4i b1 = *reinterpret_cast<const v4i*>(pb + 32 * kRS + kk);
+                acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
+            }
+        }
+        if (st + 1 < nst) lstore(buf ^ 1);
+        __syncthreads();
+    }
+    if (idle) return;
+    // fp64 epilogue (as dbslmm_gram_i8, no-missing form): C/D col = lane & 31,
+    // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    const double scale = tau / n_ref_d;
+#pragma unroll
+    for (int sj = 0; sj < 2; ++sj) {
+        const int lj = kGT * tile.tj + 64 * wc + 32 * sj + (lane & 31);
+        if (lj >= m) continue;
+        const double Sj = S[row0 + lj], rj = rsd[row0 + lj];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int li = kGT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (li >= m) continue;
+                const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
+                double v = scale * (c * rsd[row0 + li] * rj);
+                if (li == lj) v += 1.0 - tau;
+                M[moff + static_cast<int64_t>(li) * ld + lj] = v;
+            }
+        }
     }
 }
 

@@ -7,7 +7,7 @@
 //             [small SNPs | large SNPs | padding]; per slot: bed row (-1 = pad), block,
 //             z-score, output index (>= 0 small, -1-i large); slot m of a block doubles as
 //             the row that carries z through the bordered Cholesky
-//   G         int8 [n_slots][kpad] dosages, kpad = roundup(n_ref, 64)
+//   G         int8 [n_slots + 128][kpad] dosages, kpad = roundup(n_ref, 128)
 //   M         fp64 per block ld x ld row-major, lower triangle; row m = z (written by the solve)
 //   stats     S, mu, 1/sd per slot; y (solve scratch) per slot; flags/status per block
 // The whole problem stays resident; plan_run re-executes unpack -> gram -> chol from the
@@ -37,6 +37,8 @@ constexpr int kEvPerRun = 8;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
+constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
+constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
@@ -80,7 +82,9 @@ struct dbslmm_plan {
     double graph_dshift = 0.0;
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
-    GramTile* d_tiles = nullptr;
+    GramTile* d_tiles = nullptr;       // 32 x 32 tiles of the small blocks (dbslmm_gram_i8)
+    GramTile* d_btiles = nullptr;      // 128 x 128 tiles of the other blocks, per-XCD queues
+    int32_t n_btiles = 0;
     double* d_M = nullptr;
     double *d_beta_s = nullptr, *d_beta_l = nullptr;
     std::vector<int32_t> h_ld;  // per non-empty block
@@ -148,6 +152,8 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kCholLargeLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_big),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_diag0),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kTiledLds)) != hipSuccess ||
@@ -189,7 +195,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
-                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist};
+                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -218,7 +224,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->sigma_s = pr->sigma_s;
     p->tau = pr->tau;
     p->bytes_per_snp = bps;
-    p->kpad = round_up(pr->n_ref, 64);
+    p->kpad = round_up(pr->n_ref, gram::kKS);
     p->bed_len = pr->bed_len;
     p->n_s = pr->s_ptr[pr->num_block];
     p->n_l = has_l ? pr->l_ptr[pr->num_block] : 0;
@@ -228,6 +234,10 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<double> z;
     std::vector<int64_t> matoff;
     std::vector<GramTile> tiles;
+    int64_t gram_big_min = kGramBigMinDefault;
+    if (const char* env = getenv("DBSLMM_GRAM_BIG_MIN")) gram_big_min = std::max<int64_t>(1, atoll(env));
+    std::vector<std::vector<GramTile>> xq(kXcd);
+    std::vector<double> xload(kXcd, 0.0);
     int64_t moff = 0;
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
@@ -273,17 +283,35 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             slot_out.push_back(INT32_MIN);
             z.push_back(0.0);
         }
-        const int T = static_cast<int>((m + kTile - 1) / kTile);   // tiles holding SNP rows
-        for (int ti = 0; ti < T; ++ti)
-            for (int tj = 0; tj <= ti; ++tj) tiles.push_back({nb, ti, tj, 0});
+        if (m >= gram_big_min) {   // 128 x 128 tiles, the block's queue on the least-loaded XCD
+            const int T = static_cast<int>((m + gram::kGT - 1) / gram::kGT);
+            const int x = static_cast<int>(std::min_element(xload.begin(), xload.end()) - xload.begin());
+            for (int ti = 0; ti < T; ++ti)
+                for (int tj = 0; tj <= ti; ++tj) xq[x].push_back({nb, ti, tj, 0});
+            xload[x] += T * (T + 1) / 2;
+            ops_exec += 2.0 * p->kpad * gram::kGT * gram::kGT * (T * (T + 1) / 2);
+        } else {
+            const int T = static_cast<int>((m + kTile - 1) / kTile);   // tiles holding SNP rows
+            for (int ti = 0; ti < T; ++ti)
+                for (int tj = 0; tj <= ti; ++tj) tiles.push_back({nb, ti, tj, 0});
+            ops_exec += 2.0 * p->kpad * kTile * kTile * (T * (T + 1) / 2);
+        }
         ops_alg += static_cast<double>(pr->n_ref) * m * (m + 1);
-        ops_exec += 2.0 * p->kpad * kTile * kTile * (T * (T + 1) / 2);
         (tiled ? chol_flops_tiled : ld > chol::kSmallLd ? chol_flops_large : chol_flops_small) +=
             m * static_cast<double>(m) * m / 3.0 + 2.0 * m * m;
     }
     p->n_nonempty = static_cast<int32_t>(row0.size());
     p->n_slots = static_cast<int32_t>(slot_pos.size());
     p->n_tiles = static_cast<int32_t>(tiles.size());
+    std::vector<GramTile> btiles;
+    {
+        size_t qmax = 0;
+        for (const auto& q : xq) qmax = std::max(qmax, q.size());
+        btiles.assign(qmax * kXcd, GramTile{-1, 0, 0, 0});
+        for (int x = 0; x < kXcd; ++x)
+            for (size_t i = 0; i < xq[x].size(); ++i) btiles[i * kXcd + x] = xq[x][i];
+        p->n_btiles = static_cast<int32_t>(btiles.size());
+    }
     p->M_elems = moff;
     p->h_ld = ldv;
     // Cholesky work lists: large blocks (ld > 64, one workgroup each) then small blocks (one
@@ -354,7 +382,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[4] = ops_exec;
     p->wl[5] = chol_flops_large;
     p->wl[6] = p->n_nonempty;
-    p->wl[7] = p->n_tiles;
+    p->wl[7] = p->n_tiles + p->n_btiles;
     p->wl[8] = chol_flops_small;
     p->wl[9] = p->n_large;
     p->wl[10] = chol_flops_tiled;
@@ -372,8 +400,10 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
     if ((e = hipMemset(p->d_bed, 0, pr->bed_len + 16)) != hipSuccess) return fail("hipMemset bed");
     if ((e = hipMemcpy(p->d_bed, pr->bed, pr->bed_len, hipMemcpyHostToDevice)) != hipSuccess) return fail("upload bed");
-    const int64_t g_bytes = std::max<int64_t>(64, static_cast<int64_t>(p->n_slots) * p->kpad);
+    // + kGT spare rows: a 128-row Gram tile may read past the last slot (results discarded)
+    const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kGT) * p->kpad;
     if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
+    if ((e = hipMemset(p->d_G, 0, g_bytes)) != hipSuccess) return fail("hipMemset G");
     if ((e = dev_upload(&p->d_slot_pos, slot_pos)) != hipSuccess) return fail("upload slots");
     if ((e = dev_upload(&p->d_slot_block, slot_block)) != hipSuccess) return fail("upload slots");
     if ((e = dev_upload(&p->d_slot_out, slot_out)) != hipSuccess) return fail("upload slots");
@@ -386,6 +416,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_blk_id, blk_id)) != hipSuccess) return fail("upload blocks");
     if ((e = dev_upload(&p->d_order, order)) != hipSuccess) return fail("upload order");
     if ((e = dev_upload(&p->d_tiles, tiles)) != hipSuccess) return fail("upload tiles");
+    if ((e = dev_upload(&p->d_btiles, btiles)) != hipSuccess) return fail("upload tiles");
     if ((e = dev_upload(&p->d_tlist, tlist)) != hipSuccess) return fail("upload tiled lists");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -505,6 +536,14 @@ int dbslmm_plan_run(dbslmm_plan* p) {
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
                            static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (p->n_btiles > 0) {
+        hipLaunchKernelGGL(dbslmm_gram_big, dim3(p->n_btiles), dim3(256), gram::kLdsBytes, s, p->d_G,
+                           p->kpad, p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld,
+                           p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
+                           static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
+                           p->tau, p->d_M);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));

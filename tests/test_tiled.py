@@ -114,3 +114,21 @@ def test_tiled_plan_rerun_bit_identical(monkeypatch):
     b = plan.download()
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("miss", [0.0, 0.01])
+@pytest.mark.parametrize("n_ref", [200, 333])
+def test_gram_kernels_bit_identical(monkeypatch, miss, n_ref):
+    """128x128 LDS-staged Gram (m >= DBSLMM_GRAM_BIG_MIN) and the per-wave 32x32 Gram compute
+    the same exact integers and the same fp64 epilogue: beta must agree bit for bit."""
+    from dbslmm_amd import DBSLMMFIT, synth
+    p = synth.simulate(6000, n_ref, pop="EUR", chroms=[1], seed=7, miss_rate=miss, large_every=3)
+    prob = synth.make_problem(p)
+    monkeypatch.setenv("DBSLMM_GRAM_BIG_MIN", "1")
+    big = DBSLMMFIT(0).est(prob)
+    monkeypatch.setenv("DBSLMM_GRAM_BIG_MIN", str(10 ** 9))
+    small = DBSLMMFIT(0).est(prob)
+    for x, y in zip(big, small):
+        np.testing.assert_array_equal(x, y)
+    ref, _ = _oracle(prob)
+    assert normwise(np.concatenate(big[:2]), ref) < 1e-10
