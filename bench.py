@@ -72,7 +72,9 @@ def kernel_roofline(name, ms, wl):
         a = wl["gram_ops_alg"] / s / 1e12
         return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_I8_TOPS, unit="TFLOP/s",
                     frac=a / PEAK_I8_TOPS, algorithmic=wl["gram_ops_alg"], ms=ms,
-                    note="int8 ops (2/MAC), algorithmic sum_b n_ref*m_b*(m_b+1)")
+                    executed_tops=wl["gram_ops_exec"] / s / 1e12,
+                    note="int8 ops (2/MAC), algorithmic sum_b n_ref*m_b*(m_b+1); executed = "
+                         "padded tiles x padded individuals")
     fl = {"dbslmm_chol_large": wl["chol_flops_large"], "dbslmm_chol_small": wl["chol_flops_small"],
           "dbslmm_tchol": wl["chol_flops_tiled"]}[name]
     a = fl / s / 1e12 if s > 0 else 0.0

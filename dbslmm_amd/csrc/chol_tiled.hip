@@ -5,9 +5,9 @@
 //
 //   tchol_diag0          step 0 only: factor + invert diagonal tile (0, 0)
 //   tchol_panel(k)       L_ik = A_ik X_kk^T for every tile row i > k     (one workgroup per tile)
-//   tchol_trailing(k)    C_ij -= L_ik L_jk^T, k < j <= i, except (k+1, k+1) (one workgroup/tile)
-//   tchol_diag(k)        lookahead, concurrently on a 4th stream: update tile (k+1, k+1) and
-//                        factor + invert it (its 256 VGPRs stay out of the trailing kernel)
+//   tchol_trailing(k)    C_ij -= L_ik L_jk^T, k < j <= i                 (one workgroup per tile)
+//                        -- the first workgroups take tile (k+1, k+1): update, then factor +
+//                           invert it (lookahead), overlapping the rest of the update
 //   tchol_backward(J)    x_J = X_JJ^T v_J, v_{<J} -= L_{J,<J}^T x_J        (one workgroup per
 //                        256 columns; x_J recomputed per workgroup, v_J is read-only in a launch)
 //
@@ -194,23 +194,32 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);
 }
 
-// trailing update of step k: C_ij -= L_ik L_jk^T for every pair except the diagonal tile
-// (k+1, k+1), which dbslmm_tchol_diag updates and factors concurrently on another stream.
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_trailing(
+// trailing update of step k: C_ij -= L_ik L_jk^T for every pair (k < j <= i).  Items [0, n) are
+// the diagonal tiles (k+1, k+1) of the n active blocks: those workgroups update their tile and
+// then factor + invert it (lookahead) -- dispatched first, they overlap the bulk of the update.
+// Items n.. are the other pairs.  Register budget capped for 2 workgroups per CU (LDS-bound).
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_trailing(
     chol::TiledArgs a, int32_t k, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
     int32_t n) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int item = blockIdx.x;
-    if (item >= pfx[n]) return;
-    const int s = find_item(pfx, n, item);
-    const int b = act[s];
-    const int m = a.blk_m[b], ld = a.blk_ld[b];
-    const int T = (m + kBT - 1) / kBT, Tz = m / kBT;
-    const int nJ = T - 1 - k, tri_n = nJ * (nJ + 1) / 2;
-    int I, J;
-    decode_pair(item - pfx[s] + 1, tri_n, k, Tz, I, J);   // pair 0 is the diagonal tile
+    if (item >= n + pfx[n]) return;
+    const bool diag = item < n;
+    int b, I, J;
+    if (diag) {
+        b = act[item];
+        I = J = k + 1;
+    } else {
+        const int s = find_item(pfx, n, item - n);
+        b = act[s];
+        const int m_ = a.blk_m[b];
+        const int T = (m_ + kBT - 1) / kBT, Tz = m_ / kBT;
+        const int nJ = T - 1 - k, tri_n = nJ * (nJ + 1) / 2;
+        decode_pair(item - n - pfx[s] + 1, tri_n, k, Tz, I, J);   // pair 0 is the diagonal tile
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = a.blk_m[b], ld = a.blk_ld[b];
     double* A = a.M + a.blk_matoff[b];
     const int c0 = kBT * k;
     double* LI = lds;
@@ -220,39 +229,18 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_t
     else LJ = LI;
     __syncthreads();
     const int qi = wave >> 1, qj = wave & 1;
-    if (I == J && qj > qi) return;
-    v4d acc[2][2];
-    const int r0 = kBT * I + kT * qi, cc0 = kBT * J + kT * qj;
-    load_acc(acc, A, ld, r0, cc0, lane);
-    mfma_tile(acc, LI + (2 * qi) * kSub, LJ + (2 * qj) * kSub, -1.0, lane);
-    mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJ + (2 * qj + 1) * kSub, -1.0, lane);
-    store_acc(acc, A, ld, r0, cc0, lane);
-}
-
-// lookahead of step k: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, then factor + invert it
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_diag(
-    chol::TiledArgs a, int32_t k, const int32_t* __restrict__ act, int32_t n) {
-    using namespace chol;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    if (static_cast<int>(blockIdx.x) >= n) return;
-    const int b = act[blockIdx.x];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m = a.blk_m[b], ld = a.blk_ld[b];
-    double* A = a.M + a.blk_matoff[b];
-    const int d0 = kBT * (k + 1);
-    stage64(lds, A, ld, d0, kBT * k, tid);
-    __syncthreads();
-    const int qi = wave >> 1, qj = wave & 1;
-    if (qj <= qi) {
+    if (!(I == J && qj > qi)) {
         v4d acc[2][2];
-        load_acc(acc, A, ld, d0 + kT * qi, d0 + kT * qj, lane);
-        mfma_tile(acc, lds + (2 * qi) * kSub, lds + (2 * qj) * kSub, -1.0, lane);
-        mfma_tile(acc, lds + (2 * qi + 1) * kSub, lds + (2 * qj + 1) * kSub, -1.0, lane);
-        store_acc(acc, A, ld, d0 + kT * qi, d0 + kT * qj, lane);
+        const int r0 = kBT * I + kT * qi, cc0 = kBT * J + kT * qj;
+        load_acc(acc, A, ld, r0, cc0, lane);
+        mfma_tile(acc, LI + (2 * qi) * kSub, LJ + (2 * qj) * kSub, -1.0, lane);
+        mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJ + (2 * qj + 1) * kSub, -1.0, lane);
+        store_acc(acc, A, ld, r0, cc0, lane);
     }
-    __syncthreads();                  // the updated tile is in global memory
+    if (!diag) return;
+    __syncthreads();                  // the updated diagonal tile is in global memory
     if (wave != 0) return;
-    const bool fail = factor_diag64(A, ld, d0, m, a.blk_ms[b], a.dshift, lds, lane);
+    const bool fail = factor_diag64(A, ld, kBT * (k + 1), m, a.blk_ms[b], a.dshift, lds, lane);
     if (fail && lane == 0) atomicMax(a.status + a.blk_id[b], DBSLMM_BLOCK_NOT_PD);
 }
 

@@ -272,9 +272,10 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
 // Kernel 2b: the same Gram for blocks without missing calls, 128 x 128 output tile per
 // 256-thread workgroup (wave w: 64 x 64 quadrant (w >> 1, w & 1) = 2 x 2 MFMA 32x32x32 i8).
 // K runs in stages of 128 individuals through double-buffered LDS (row stride 144 B: the 16 rows
-// of a ds_read_b128 lane group land on 16 distinct 16-B bank groups); the next stage's global
-// loads are in flight while the current stage's 16 MFMAs per wave run.  Diagonal tiles stage
-// one operand and skip the strictly-upper quadrant.  Tiles come in per-XCD queues (entry e runs
+// of a ds_read_b128 lane group land on 16 distinct 16-B bank groups); global loads run ahead of
+// the current stage's 16 MFMAs per wave (see below).  Diagonal tiles stage
+// one operand and skip the strictly-upper quadrant.  Global loads run two stages ahead (two
+// register sets, loop unrolled by two).  Tiles come in per-XCD queues (entry e runs
 // on XCD e % 8) so a block's rows stay in one L2; entries with block < 0 are padding.
 // Blocks with a missing call (flag set by the unpack) take the exact 4-product 32 x 32 path.
 // ------------------------------------------------------------------------------------------
@@ -317,9 +318,11 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     }
     const int8_t* ga = G + static_cast<int64_t>(row0 + kGT * tile.ti) * kpad;
     const int8_t* gb = G + static_cast<int64_t>(row0 + kGT * tile.tj) * kpad;
-    // staging map: 128 rows x 8 chunks of 16 B per operand; thread t moves chunks t + 256 q
-    v4i ra[4], rb[4];
-    auto gload = [&](int64_t k0) {
+    // staging map: 128 rows x 8 chunks of 16 B per operand; thread t moves chunks t + 256 q.
+    // Two register sets: the global loads of stage s + 2 are issued before stage s's MFMAs.
+    v4i ra0[4], rb0[4], ra1[4], rb1[4];
+    auto gload = [&](v4i (&ra)[4], v4i (&rb)[4], int st) {
+        const int64_t k0 = static_cast<int64_t>(st) * kKS;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = q * 256 + tid, r = e >> 3, c = e & 7;
@@ -327,7 +330,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
             if (!diag) rb[q] = *reinterpret_cast<const v4i*>(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](const v4i (&ra)[4], const v4i (&rb)[4], int buf) {
         int8_t* A = glds + buf * 2 * kOpBytes;
         int8_t* B = A + kOpBytes;
 #pragma unroll
@@ -344,34 +347,43 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = v16i{0};
-    const int nst = static_cast<int>(kpad / kKS);
-    gload(0);
-    lstore(0);
-    __syncthreads();
     // operand read offsets: lane l -> row (l & 31) of a 32-row group, k bytes 16 (l >> 5) of a
     // 32-byte k-step
     const int rsub = lane & 31, ksub = 16 * (lane >> 5);
-    for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1;
-        if (st + 1 < nst) gload(static_cast<int64_t>(st + 1) * kKS);
-        if (!idle) {
-            const int8_t* A = glds + buf * 2 * kOpBytes;
-            const int8_t* B = diag ? A : A + kOpBytes;
-            const int8_t* pa = A + (64 * wr + rsub) * kRS + ksub;
-            const int8_t* pb = B + (64 * wc + rsub) * kRS + ksub;
+    auto compute = [&](int buf) {
+        if (idle) return;
+        const int8_t* A = glds + buf * 2 * kOpBytes;
+        const int8_t* B = diag ? A : A + kOpBytes;
+        const int8_t* pa = A + (64 * wr + rsub) * kRS + ksub;
+        const int8_t* pb = B + (64 * wc + rsub) * kRS + ksub;
 #pragma unroll
-            for (int kk = 0; kk < kKS; kk += 32) {
-                const v4i a0 = *reinterpret_cast<const v4i*>(pa + kk);
-                const v4i a1 = *reinterpret_cast<const v4i*>(pa + 32 * kRS + kk);
-                const v4i b0 = *reinterpret_cast<const v4i*>(pb + kk);
-                const v4i b1 = *reinterpret_cast<const v4i*>(pb + 32 * kRS + kk);
-                acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
-            }
+        for (int kk = 0; kk < kKS; kk += 32) {
+            const v4i a0 = *reinterpret_cast<const v4i*>(pa + kk);
+            const v4i a1 = *reinterpret_cast<const v4i*>(pa + 32 * kRS + kk);
+            const v4i b0 = *reinterpret_cast<const v4i*>(pb + kk);
+            const v4i b1 = *reinterpret_cast<const v4i*>(pb + 32 * kRS + kk);
+            acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
         }
-        if (st + 1 < nst) lstore(buf ^ 1);
+    };
+    const int nst = static_cast<int>(kpad / kKS);
+    gload(ra0, rb0, 0);
+    lstore(ra0, rb0, 0);
+    if (nst > 1) gload(ra1, rb1, 1);
+    __syncthreads();
+    for (int st = 0; st < nst; st += 2) {
+        // stage st from LDS buffer 0; ra1 holds st + 1, ra0 receives st + 2
+        if (st + 2 < nst) gload(ra0, rb0, st + 2);
+        compute(0);
+        if (st + 1 < nst) lstore(ra1, rb1, 1);
+        __syncthreads();
+        if (st + 1 >= nst) break;
+        // stage st + 1 from LDS buffer 1; ra0 holds st + 2, ra1 receives st + 3
+        if (st + 3 < nst) gload(ra1, rb1, st + 3);
+        compute(1);
+        if (st + 2 < nst) lstore(ra0, rb0, 0);
         __syncthreads();
     }
     if (idle) return;

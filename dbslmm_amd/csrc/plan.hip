@@ -42,7 +42,7 @@ constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
-    int kind;         // 0 diag0, 1 panel, 2 trailing, 3 backward, 4 diag (lookahead, 4th stream)
+    int kind;         // 0 diag0, 1 panel, 2 trailing (+ lookahead diagonal), 3 backward
     int step;
     int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
     int32_t n;
@@ -56,8 +56,7 @@ struct dbslmm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // main stream (unpack, gram, large-block Cholesky)
     hipStream_t stream2 = nullptr;   // tiled (multi-workgroup) Cholesky sequence, forked/joined
-    hipStream_t stream3 = nullptr;   // its lookahead diagonal factorisations
-    hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr, ev_panel = nullptr, ev_diag = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
     std::string err;
 };
 
@@ -143,9 +142,6 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_panel, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_diag, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
@@ -162,9 +158,6 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                             static_cast<int>(kTiledLds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTiledLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_diag),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kTiledLds)) != hipSuccess) {
         dbslmm_ctx_destroy(c);
         return DBSLMM_E_HIP;
@@ -178,9 +171,6 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
-    if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
-    if (ctx->ev_diag) (void)hipEventDestroy(ctx->ev_diag);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->join3) (void)hipEventDestroy(ctx->join3);
@@ -346,7 +336,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         };
         if (!tb.empty()) add(0, 0, tb, std::vector<int32_t>(tb.size(), 1), 0);
         for (int k = 0; k < Kmax; ++k) {
-            std::vector<int32_t> pa, pc, ta, tc, dc;
+            std::vector<int32_t> pa, pc, ta, tc;
             for (int32_t b : tb) {
                 const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
                 if (Tz > k) { pa.push_back(b); pc.push_back(Tz - k); }
@@ -354,13 +344,11 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                 if (nJ > 0) {
                     const int npairs = nJ * (nJ + 1) / 2 + (Tz == T ? nJ : 0);
                     ta.push_back(b);
-                    dc.push_back(1);
-                    tc.push_back(npairs - 1);     // the diagonal pair goes to tchol_diag
+                    tc.push_back(npairs - 1);
                 }
             }
             add(1, k, pa, pc, 0);
-            add(4, k, ta, dc, 0);
-            add(2, k, ta, tc, 0);
+            add(2, k, ta, tc, static_cast<int>(ta.size()));   // + one diagonal item per block
         }
         for (int J = Kmax - 1; J >= 0; --J) {
             std::vector<int32_t> ba, bc;
@@ -465,20 +453,15 @@ static int collect_timing(dbslmm_plan* p) {
     return DBSLMM_OK;
 }
 
-// Enqueue the tiled sequence on stream2 (lookahead factorisations on stream3, joined back).
+// Enqueue the tiled sequence on stream2.
 static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
     dbslmm_ctx* ctx = p->ctx;
     const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
                              p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn,
                              p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
-    hipStream_t st = ctx->stream2, sd = ctx->stream3;
-    bool diag_pending = false;
+    hipStream_t st = ctx->stream2;
     for (const TLaunch& L : p->tl) {
         if (L.items == 0) continue;
-        if ((L.kind == 1 || L.kind == 3) && diag_pending) {   // needs the lookahead factor
-            HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->ev_diag, 0));
-            diag_pending = false;
-        }
         const int32_t* act = p->d_tlist + L.off;
         const int32_t* pfx = act + L.n;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
@@ -486,17 +469,9 @@ static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
         case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, st, ta, act, L.n); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
         case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
-        case 4:
-            HIP_TRY(ctx, hipEventRecord(ctx->ev_panel, st));
-            HIP_TRY(ctx, hipStreamWaitEvent(sd, ctx->ev_panel, 0));
-            hipLaunchKernelGGL(dbslmm_tchol_diag, g, blk, kTiledLds, sd, ta, L.step, act, L.n);
-            HIP_TRY(ctx, hipEventRecord(ctx->ev_diag, sd));
-            diag_pending = true;
-            break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }
     }
-    if (diag_pending) HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->ev_diag, 0));
     HIP_TRY(ctx, hipGetLastError());
     return DBSLMM_OK;
 }
@@ -550,9 +525,8 @@ int dbslmm_plan_run(dbslmm_plan* p) {
     if (p->n_nonempty > 0) {
         const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
-        // fork: the tiled sequence runs on stream2 (its lookahead factorisations on stream3)
-        // while the single-workgroup and single-wave kernels run on the main stream.  A process
-        // gets 4 hardware queues (null stream + these 3), so each of them has its own.
+        // fork: the tiled sequence runs on stream2 (high priority: the critical path) while the
+        // single-workgroup and single-wave kernels run on the main stream.
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
         if (p->n_large > 0) {
