@@ -194,48 +194,79 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);
 }
 
-// trailing update of step k: C_ij -= L_ik L_jk^T for every pair (k < j <= i).  Items [0, n) are
-// the diagonal tiles (k+1, k+1) of the n active blocks: those workgroups update their tile and
-// then factor + invert it (lookahead) -- dispatched first, they overlap the bulk of the update.
-// Items n.. are the other pairs.  Register budget capped for 2 workgroups per CU (LDS-bound).
+// trailing update of step k: C_ij -= L_ik L_jk^T for every pair (k < j <= i).  The launch's
+// list holds one packed item per workgroup, (block << 16) | (I << 8) | J0, or -1 (padding): the
+// workgroup updates tiles (I, J0 .. J0 + kJRun - 1) (clipped to the lower triangle), with L_I
+// staged once and the next tile's L_J and C prefetched into registers during the current MFMAs.
+// The list starts with the diagonal tiles (k+1, k+1) of the active blocks -- those workgroups
+// update their tile and then factor + invert it (lookahead), overlapping the bulk -- followed by
+// per-XCD queues (item e runs on XCD e % 8; the runs of one tile row I of a block share an XCD,
+// so L_I is served by that XCD's L2).  Register budget capped for 2 workgroups per CU.
+namespace chol {
+constexpr int kJRun = 4;
+// this thread's 16 elements of a 64x64 tile (coalesced rows), and their LDS sub-tile slots
+__device__ __forceinline__ void tile_regs_load(double (&v)[16], const double* A, int ld, int r0, int c0, int tid) {
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int e = it * kLargeThreads + tid;
+        v[it] = A[static_cast<int64_t>(r0 + (e >> 6)) * ld + c0 + (e & 63)];
+    }
+}
+__device__ __forceinline__ void tile_regs_store(const double (&v)[16], double* S, int tid) {
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int e = it * kLargeThreads + tid;
+        const int r = e >> 6, c = e & 63;
+        S[(2 * (r >> 5) + (c >> 5)) * kSub + (r & 31) * kTS + (c & 31)] = v[it];
+    }
+}
+}  // namespace chol
+
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_trailing(
-    chol::TiledArgs a, int32_t k, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
-    int32_t n) {
+    chol::TiledArgs a, int32_t k, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int item = blockIdx.x;
-    if (item >= n + pfx[n]) return;
-    const bool diag = item < n;
-    int b, I, J;
-    if (diag) {
-        b = act[item];
-        I = J = k + 1;
-    } else {
-        const int s = find_item(pfx, n, item - n);
-        b = act[s];
-        const int m_ = a.blk_m[b];
-        const int T = (m_ + kBT - 1) / kBT, Tz = m_ / kBT;
-        const int nJ = T - 1 - k, tri_n = nJ * (nJ + 1) / 2;
-        decode_pair(item - n - pfx[s] + 1, tri_n, k, Tz, I, J);   // pair 0 is the diagonal tile
-    }
+    if (static_cast<int>(blockIdx.x) >= n_items) return;
+    const int32_t it = items[blockIdx.x];
+    if (it < 0) return;
+    const int b = it >> 16, I = (it >> 8) & 255, J0 = it & 255;
+    const bool diag = I == k + 1 && J0 == k + 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m = a.blk_m[b], ld = a.blk_ld[b];
+    const int T = (m + kBT - 1) / kBT;
+    const int J1 = min(J0 + kJRun - 1, min(I, T - 1));
     double* A = a.M + a.blk_matoff[b];
     const int c0 = kBT * k;
     double* LI = lds;
     double* LJ = lds + 4 * kSub;
-    stage64(LI, A, ld, kBT * I, c0, tid);
-    if (I != J) stage64(LJ, A, ld, kBT * J, c0, tid);
-    else LJ = LI;
-    __syncthreads();
     const int qi = wave >> 1, qj = wave & 1;
-    if (!(I == J && qj > qi)) {
-        v4d acc[2][2];
-        const int r0 = kBT * I + kT * qi, cc0 = kBT * J + kT * qj;
-        load_acc(acc, A, ld, r0, cc0, lane);
-        mfma_tile(acc, LI + (2 * qi) * kSub, LJ + (2 * qj) * kSub, -1.0, lane);
-        mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJ + (2 * qj + 1) * kSub, -1.0, lane);
-        store_acc(acc, A, ld, r0, cc0, lane);
+    double lj[16];
+    v4d acc[2][2], nxt[2][2];
+    stage64(LI, A, ld, kBT * I, c0, tid);
+    tile_regs_load(lj, A, ld, kBT * J0, c0, tid);
+    load_acc(acc, A, ld, kBT * I + kT * qi, kBT * J0 + kT * qj, lane);
+    tile_regs_store(lj, LJ, tid);
+    __syncthreads();
+    for (int J = J0; J <= J1; ++J) {
+        const bool more = J < J1;
+        if (more) {
+            tile_regs_load(lj, A, ld, kBT * (J + 1), c0, tid);
+            load_acc(nxt, A, ld, kBT * I + kT * qi, kBT * (J + 1) + kT * qj, lane);
+        }
+        if (!(I == J && qj > qi)) {
+            mfma_tile(acc, LI + (2 * qi) * kSub, LJ + (2 * qj) * kSub, -1.0, lane);
+            mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJ + (2 * qj + 1) * kSub, -1.0, lane);
+            store_acc(acc, A, ld, kBT * I + kT * qi, kBT * J + kT * qj, lane);
+        }
+        if (more) {
+            __syncthreads();                      // every wave is done with LJ
+            tile_regs_store(lj, LJ, tid);
+#pragma unroll
+            for (int si = 0; si < 2; ++si)
+#pragma unroll
+                for (int sj = 0; sj < 2; ++sj) acc[si][sj] = nxt[si][sj];
+            __syncthreads();
+        }
     }
     if (!diag) return;
     __syncthreads();                  // the updated diagonal tile is in global memory

@@ -241,6 +241,11 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         if (m == 0) { p->h_empty.push_back(b); continue; }
         const int nb = static_cast<int>(row0.size());
         const bool tiled = m >= tiled_min;
+        if (tiled && (m / chol::kBT > 254 || nb >= 32767)) {   // packed (block, I, J) trailing items
+            ctx->err = "LD block too large for the tiled path (m must be < 16320 SNPs)";
+            dbslmm_plan_destroy(p);
+            return DBSLMM_E_ARG;
+        }
         is_tiled.push_back(tiled);
         // + the z row of the bordered matrix; the tiled path works on 64 x 64 tiles
         const int64_t ld = round_up(m + 1, tiled ? chol::kBT : kTile);
@@ -336,19 +341,38 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         };
         if (!tb.empty()) add(0, 0, tb, std::vector<int32_t>(tb.size(), 1), 0);
         for (int k = 0; k < Kmax; ++k) {
-            std::vector<int32_t> pa, pc, ta, tc;
+            std::vector<int32_t> pa, pc, ta;
             for (int32_t b : tb) {
                 const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
                 if (Tz > k) { pa.push_back(b); pc.push_back(Tz - k); }
                 const int nJ = T - 1 - k;
-                if (nJ > 0) {
-                    const int npairs = nJ * (nJ + 1) / 2 + (Tz == T ? nJ : 0);
-                    ta.push_back(b);
-                    tc.push_back(npairs - 1);
-                }
+                if (nJ > 0) ta.push_back(b);
             }
             add(1, k, pa, pc, 0);
-            add(2, k, ta, tc, static_cast<int>(ta.size()));   // + one diagonal item per block
+            if (!ta.empty()) {   // trailing: packed items, diagonal tiles first, then per-XCD queues
+                TLaunch L{2, k, static_cast<int32_t>(tlist.size()), 0, 0};
+                for (int32_t b : ta) tlist.push_back((b << 16) | ((k + 1) << 8) | (k + 1));
+                std::vector<std::vector<int32_t>> q(kXcd);
+                std::vector<int64_t> load(kXcd, 0);
+                for (int32_t b : ta) {
+                    const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
+                    for (int I = k + 1; I <= Tz; ++I) {
+                        const int jmax = std::min(I, T - 1);
+                        const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+                        for (int J = k + 1; J <= jmax; J += chol::kJRun)
+                            if (!(I == k + 1 && J == k + 1)) q[x].push_back((b << 16) | (I << 8) | J);
+                        load[x] += jmax - k;
+                    }
+                }
+                size_t qmax = 0;
+                for (const auto& v : q) qmax = std::max(qmax, v.size());
+                // align the queue part so that item e of it runs on XCD e % 8
+                while ((tlist.size() - L.off) % kXcd) tlist.push_back(-1);
+                for (size_t i = 0; i < qmax; ++i)
+                    for (int x = 0; x < kXcd; ++x) tlist.push_back(i < q[x].size() ? q[x][i] : -1);
+                L.items = static_cast<int32_t>(tlist.size() - L.off);
+                p->tl.push_back(L);
+            }
         }
         for (int J = Kmax - 1; J >= 0; --J) {
             std::vector<int32_t> ba, bc;
@@ -468,7 +492,7 @@ static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
         switch (L.kind) {
         case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, st, ta, act, L.n); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
-        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
+        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }
     }
