@@ -247,8 +247,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             return DBSLMM_E_ARG;
         }
         is_tiled.push_back(tiled);
-        // + the z row of the bordered matrix; the tiled path works on 64 x 64 tiles
-        const int64_t ld = round_up(m + 1, tiled ? chol::kBT : kTile);
+        // + the z row of the bordered matrix; the tiled path works on 128 x 128 regions
+        const int64_t ld = round_up(m + 1, tiled ? 2 * chol::kBT : kTile);
         row0.push_back(static_cast<int32_t>(slot_pos.size()));
         mv.push_back(static_cast<int32_t>(m));
         msv.push_back(static_cast<int32_t>(ms));
@@ -317,7 +317,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     order.erase(std::remove_if(order.begin(), order.end(), [&](int b) { return is_tiled[b] != 0; }),
                 order.end());
     for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
-    // tiled sequence: diag0, then per step k panel(k) + trailing(k), then backward(J) descending
+    // tiled sequence: diag0, then per 128-column step s panel(s) + trailing(s), then backward(J)
+    // descending (64-row tiles)
     std::vector<int32_t> tlist;
     {
         std::vector<int32_t> tb;
@@ -339,40 +340,51 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             L.items = acc + extra;
             p->tl.push_back(L);
         };
-        if (!tb.empty()) add(0, 0, tb, std::vector<int32_t>(tb.size(), 1), 0);
-        for (int k = 0; k < Kmax; ++k) {
-            std::vector<int32_t> pa, pc, ta;
+        if (!tb.empty()) {
+            TLaunch L{0, 0, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(tb.size()),
+                      static_cast<int32_t>(tb.size())};
+            tlist.insert(tlist.end(), tb.begin(), tb.end());
+            p->tl.push_back(L);
+        }
+        // outer steps of 128 columns: s covers tile columns k0 = 2s, k1 = 2s + 1
+        auto add_items = [&](int kind, int step, const std::vector<int32_t>& head,
+                             std::vector<std::vector<int32_t>>& q) {
+            TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), 0, 0};
+            tlist.insert(tlist.end(), head.begin(), head.end());
+            size_t qmax = 0;
+            for (const auto& v : q) qmax = std::max(qmax, v.size());
+            // align the queue part so that item e of it runs on XCD e % 8
+            while ((tlist.size() - L.off) % kXcd) tlist.push_back(-1);
+            for (size_t i = 0; i < qmax; ++i)
+                for (int x = 0; x < kXcd; ++x) tlist.push_back(i < q[x].size() ? q[x][i] : -1);
+            L.items = static_cast<int32_t>(tlist.size() - L.off);
+            if (L.items > 0) p->tl.push_back(L);
+        };
+        const int Smax = (Kmax + 1) / 2;
+        for (int st = 0; st < Smax; ++st) {
+            const int k1 = 2 * st + 1;
+            std::vector<int32_t> panel, head;
+            std::vector<std::vector<int32_t>> q(kXcd), none(kXcd);
+            std::vector<int64_t> load(kXcd, 0);
             for (int32_t b : tb) {
                 const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
-                if (Tz > k) { pa.push_back(b); pc.push_back(Tz - k); }
-                const int nJ = T - 1 - k;
-                if (nJ > 0) ta.push_back(b);
-            }
-            add(1, k, pa, pc, 0);
-            if (!ta.empty()) {   // trailing: packed items, diagonal tiles first, then per-XCD queues
-                TLaunch L{2, k, static_cast<int32_t>(tlist.size()), 0, 0};
-                for (int32_t b : ta) tlist.push_back((b << 16) | ((k + 1) << 8) | (k + 1));
-                std::vector<std::vector<int32_t>> q(kXcd);
-                std::vector<int64_t> load(kXcd, 0);
-                for (int32_t b : ta) {
-                    const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
-                    for (int I = k + 1; I <= Tz; ++I) {
-                        const int jmax = std::min(I, T - 1);
-                        const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                        for (int J = k + 1; J <= jmax; J += chol::kJRun)
-                            if (!(I == k + 1 && J == k + 1)) q[x].push_back((b << 16) | (I << 8) | J);
-                        load[x] += jmax - k;
-                    }
+                for (int i = k1 + 1; i <= Tz; ++i)
+                    for (int h = 0; h < 2 && k1 - 1 + h <= T - 1; ++h) panel.push_back((b << 16) | (i << 8) | h);
+                if (k1 + 1 > T - 1) continue;          // no columns beyond this step's region
+                head.push_back((b << 16) | ((k1 + 1) << 8) | (k1 + 1));   // region s+1 (lookahead)
+                for (int I = k1 + 3; I <= Tz; ++I) {
+                    const int jmax = std::min(I, T - 1);
+                    const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+                    for (int J = k1 + 1; J <= jmax; J += chol::kJRun) q[x].push_back((b << 16) | (I << 8) | J);
+                    load[x] += jmax - k1;
                 }
-                size_t qmax = 0;
-                for (const auto& v : q) qmax = std::max(qmax, v.size());
-                // align the queue part so that item e of it runs on XCD e % 8
-                while ((tlist.size() - L.off) % kXcd) tlist.push_back(-1);
-                for (size_t i = 0; i < qmax; ++i)
-                    for (int x = 0; x < kXcd; ++x) tlist.push_back(i < q[x].size() ? q[x][i] : -1);
-                L.items = static_cast<int32_t>(tlist.size() - L.off);
+            }
+            if (!panel.empty()) {
+                TLaunch L{1, st, static_cast<int32_t>(tlist.size()), 0, static_cast<int32_t>(panel.size())};
+                tlist.insert(tlist.end(), panel.begin(), panel.end());
                 p->tl.push_back(L);
             }
+            if (!head.empty()) add_items(2, st, head, q);
         }
         for (int J = Kmax - 1; J >= 0; --J) {
             std::vector<int32_t> ba, bc;
@@ -491,7 +503,7 @@ static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
         switch (L.kind) {
         case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, st, ta, act, L.n); break;
-        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, pfx, L.n); break;
+        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
         case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }
