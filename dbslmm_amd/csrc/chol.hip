@@ -245,18 +245,21 @@ __device__ __forceinline__ void acc_to_lds(const v4d (&acc)[2][2], double* W, in
                 W[(16 * si + (lane >> 4) + 4 * q) * kTS + 16 * sj + (lane & 15)] = acc[si][sj][q];
 }
 
-// Wave 0: factor the diagonal tile (c0, c0) and invert it.
-//   Coalesced load into Lb (LDS); lane r < 32 keeps row r in registers and factors
-//   right-looking.  Per column j: pivot from lane j (readlane), 1/sqrt by rsq + Newton, the
-//   scaled column is written to LDS once and read back by every lane as 16 broadcast
-//   ds_read_b128 (no per-element round trips).  X = L^{-1} is formed column-per-lane from
-//   broadcast row reads, published to Xl (LDS), and written back: lower = L, diagonal + upper
-//   (r, c >= r) = X[c][r].  Returns true when a pivot was not positive.
+// Wave 0: factor the diagonal tile (c0, c0) and invert it, in one pass.
+//   Coalesced load into Lb (LDS).  Lane r < 32 keeps ROW r of the tile in v[] and factors it
+//   right-looking; lane 32 + c keeps COLUMN c of X = L^{-1} (initially e_c) and runs the
+//   column-oriented forward substitution of L X = I alongside.  Both halves apply the same
+//   instructions per column j: pivot p = L_jj^2 from lane j (readlane), rs = 1/sqrt(p) (rsq +
+//   Newton), v[j] *= rs, then v[i] -= v[j] * L[i][j] for i > j with column j of L broadcast
+//   from LDS (written once by the row lanes, read back as ds_read_b128 broadcasts).  So the
+//   inverse costs no extra passes.  X is published to Xl (LDS) and the tile is written back:
+//   lower = L, diagonal + upper (r, c >= r) = X[c][r].  Returns true on a non-positive pivot.
 __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, int ms, double dshift,
                                             double* Xl, double* Lb, double* colb, int lane,
                                             bool from_lds) {
     FSTAMP_DECL
     const int r = lane & 31;
+    const bool xlane = lane >= kT;       // lanes 32..63: columns of X
     const int jmax = min(kT, m - c0);
     // tile -> Lb: from global (coalesced), or already in Lb (lookahead: the updating wave put it
     // there); keep the lower triangle of rows <= m, add 1/(sigma_s n) on the small diagonal
@@ -271,22 +274,22 @@ __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, in
         Lb[rr * kTS + cc] = v;
     }
     wave_sync();
-    double d[kT];
+    double v[kT];
 #pragma unroll
-    for (int c = 0; c < kT; ++c) d[c] = Lb[r * kTS + c];
+    for (int c = 0; c < kT; ++c) v[c] = xlane ? (c == r ? 1.0 : 0.0) : Lb[r * kTS + c];
     FSTAMP(4);
     bool fail = false;
     double* rdl = colb + kT;           // reciprocal pivots (LDS, 32)
 #pragma unroll
     for (int j = 0; j < kT; ++j) {
         if (j < jmax) {
-            const double p = readlane_f64(d[j], j);
+            const double p = readlane_f64(v[j], j);
             fail |= !(p > 0.0);
             const double rs = rsqrt_f64(p);
-            d[j] = (r == j) ? p * rs : ((r > j) ? d[j] * rs : 0.0);
-            if (lane < kT) {
-                colb[r] = d[j];
-                Lb[r * kTS + j] = d[j];
+            v[j] = (!xlane && r < j) ? 0.0 : v[j] * rs;    // row lanes: L[r][j]; X lanes: x[j]
+            if (!xlane) {
+                colb[r] = v[j];
+                Lb[r * kTS + j] = v[j];
             }
             if (lane == 0) rdl[j] = rs;
             wave_sync();
@@ -301,39 +304,19 @@ __device__ __forceinline__ bool factor_diag(double* A, int ld, int c0, int m, in
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    if (k0 + k > j) d[k0 + k] -= d[j] * col[k];
+                    if (k0 + k > j) v[k0 + k] -= v[j] * col[k];
             }
             wave_sync();
         }
     }
     FSTAMP(5);
-    // X = L^{-1}, lane c owns column c: x[q] = (delta_qc - sum_{k<q} L[q][k] x[k]) / L[q][q]
-    double x[kT];
+    // X columns beyond jmax are identity rows / columns (never used beyond the tile's SNPs)
+    if (xlane) {
 #pragma unroll
-    for (int q = 0; q < kT; ++q) {
-        double s0 = (q == r) ? 1.0 : 0.0, s1 = 0.0;
-#pragma unroll
-        for (int k0 = 0; k0 < q; k0 += 8) {      // broadcast row reads, 8 at a time
-            double row[8];
-#pragma unroll
-            for (int k = 0; k < 8; k += 2) {
-                const v2d t = *reinterpret_cast<const v2d*>(Lb + q * kTS + k0 + k);
-                row[k] = t[0];
-                row[k + 1] = t[1];
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (k0 + k < q) {
-                    if (k & 1) s1 -= row[k] * x[k0 + k];
-                    else s0 -= row[k] * x[k0 + k];
-                }
-            }
+        for (int q = 0; q < kT; ++q) {
+            if (q >= jmax) v[q] = (q == r) ? 1.0 : 0.0;
+            Xl[q * kTS + r] = v[q];
         }
-        x[q] = (q < jmax) ? (s0 + s1) * rdl[q] : ((q == r) ? 1.0 : 0.0);
-    }
-    if (lane < kT) {
-#pragma unroll
-        for (int q = 0; q < kT; ++q) Xl[q * kTS + r] = x[q];
     }
     wave_sync();
     FSTAMP(6);
