@@ -466,40 +466,71 @@ __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* 
     double* v = panel;   // v / x vector
     if (m > kPanelMax * kTileD) v = y + row0;
     if (!fail) {
-        // backward substitution L^T x = y, right-looking over tile rows J = Tm-1 .. 0
+        // backward substitution L^T x = y, right-looking over tile rows J = Tm-1 .. 0.
+        // Per step: the strip L[c1.., 0..c1) is loaded into registers up front (overlapping the
+        // x_J reduction), the next diagonal tile is prefetched, x_J = X_JJ^T v_J comes from an
+        // LDS copy of the stored inverse.
+        constexpr int NG = NT / kT;                        // thread groups of 32
+        double* D = Lb;                                    // diagonal tile (stride kTS)
         for (int c = tid; c < m; c += NT) v[c] = A[static_cast<int64_t>(m) * ld + c];
-        __syncthreads();
+        double dg[kT * kT / NT];
+        auto load_diag = [&](int J) {
+            const int c1 = kT * J, jm = min(kT, m - c1);
+#pragma unroll
+            for (int it = 0; it < kT * kT / NT; ++it) {
+                const int e = it * NT + tid, rr = e >> 5, cc = e & 31;
+                dg[it] = (cc >= rr && cc < jm) ? A[static_cast<int64_t>(c1 + rr) * ld + c1 + cc] : 0.0;
+            }
+        };
+        load_diag(Tm - 1);
         for (int J = Tm - 1; J >= 0; --J) {
             const int c1 = kT * J;
             const int jmax = min(kT, m - c1);
-            constexpr int NG = NT / kT;                        // thread groups of 32
-            {   // x_J = X_JJ^T v_J with X^T stored in the tile's diagonal + upper triangle
+            // strip loads for this step (2 columns per thread at most: m < 16 * kTileD)
+            double l0[kT], l1[kT];
+            const int col0 = tid, col1 = tid + NT;
+#pragma unroll
+            for (int r = 0; r < kT; ++r) {
+                l0[r] = (col0 < c1 && r < jmax) ? A[static_cast<int64_t>(c1 + r) * ld + col0] : 0.0;
+                l1[r] = (col1 < c1 && r < jmax) ? A[static_cast<int64_t>(c1 + r) * ld + col1] : 0.0;
+            }
+#pragma unroll
+            for (int it = 0; it < kT * kT / NT; ++it) {
+                const int e = it * NT + tid;
+                D[(e >> 5) * kTS + (e & 31)] = dg[it];
+            }
+            __syncthreads();
+            if (J > 0) load_diag(J - 1);
+            {   // x_J = X_JJ^T v_J: stored (c, k >= c) = X[k][c]
                 const int c = tid & 31, g = tid >> 5;
-                double s = 0.0;
-                if (c < jmax)
-                    for (int k = c + g; k < jmax; k += NG)
-                        s += A[static_cast<int64_t>(c1 + c) * ld + c1 + k] * v[c1 + k];
-                red[g * kT + c] = s;
+                double sx = 0.0;
+                for (int k = c + g; k < jmax; k += NG) sx += D[c * kTS + k] * v[c1 + k];
+                red[g * kT + c] = sx;
             }
             __syncthreads();
             if (tid < jmax) {
-                double s = 0.0;
+                double sx = 0.0;
 #pragma unroll
-                for (int q = 0; q < NG; ++q) s += red[q * kT + tid];
-                v[c1 + tid] = s;
+                for (int q = 0; q < NG; ++q) sx += red[q * kT + tid];
+                v[c1 + tid] = sx;
             }
             __syncthreads();
-            // v[col] -= sum_r L[c1 + r][col] x[c1 + r] for col < c1 (row strip of tile row J)
-            for (int col = tid; col < c1; col += NT) {
-                double s0 = 0.0, s1 = 0.0;
+            // v[col] -= sum_r L[c1 + r][col] x[r] for col < c1
+            double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
 #pragma unroll
-                for (int rr = 0; rr < kT; rr += 2) {
-                    const double l0 = A[static_cast<int64_t>(c1 + rr) * ld + col];
-                    const double l1 = A[static_cast<int64_t>(c1 + rr + 1) * ld + col];
-                    if (rr < jmax) s0 += l0 * v[c1 + rr];
-                    if (rr + 1 < jmax) s1 += l1 * v[c1 + rr + 1];
-                }
-                v[col] -= s0 + s1;
+            for (int r = 0; r < kT; r += 2) {
+                const double x0 = r < jmax ? v[c1 + r] : 0.0, x1 = r + 1 < jmax ? v[c1 + r + 1] : 0.0;
+                s0 += l0[r] * x0;
+                s1 += l0[r + 1] * x1;
+                t0 += l1[r] * x0;
+                t1 += l1[r + 1] * x1;
+            }
+            if (col0 < c1) v[col0] -= s0 + s1;
+            if (col1 < c1) v[col1] -= t0 + t1;
+            for (int col = tid + 2 * NT; col < c1; col += NT) {      // m > 512: generic tail
+                double sg = 0.0;
+                for (int r = 0; r < jmax; ++r) sg += A[static_cast<int64_t>(c1 + r) * ld + col] * v[c1 + r];
+                v[col] -= sg;
             }
             __syncthreads();
         }
