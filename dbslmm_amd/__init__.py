@@ -126,6 +126,18 @@ class Plan:
     def set_sigma(self, sigma_s: float):
         self.ctx.check(self.ctx.lib.dbslmm_plan_set_sigma(self.h, float(sigma_s)), "plan_set_sigma")
 
+    def run_multi(self, sigmas):
+        """h2f tuning: one unpack + Gram, one solve per sigma_s -> [(beta_s, beta_l, status)]."""
+        p = self.prob
+        sig = np.ascontiguousarray(sigmas, dtype=np.float64)
+        n = len(sig)
+        bs = np.zeros((n, p.n_s))
+        bl = np.zeros((n, p.n_l))
+        st = np.zeros((n, p.num_block), dtype=np.int32)
+        self.ctx.check(self.ctx.lib.dbslmm_plan_run_multi(self.h, _ptr(sig), n, _ptr(bs), _ptr(bl),
+                                                          _ptr(st)), "plan_run_multi")
+        return [(bs[i], bl[i], st[i]) for i in range(n)]
+
     def enable_timing(self, on: bool = True):
         self.ctx.check(self.ctx.lib.dbslmm_plan_enable_timing(self.h, int(on)), "plan_enable_timing")
 

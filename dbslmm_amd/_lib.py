@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libdbslmm_hip.so")
 EXPORTS = (
     "dbslmm_abi_version", "dbslmm_ctx_create", "dbslmm_ctx_destroy", "dbslmm_last_error",
     "dbslmm_est", "dbslmm_plan_create", "dbslmm_plan_run", "dbslmm_plan_sync",
-    "dbslmm_plan_download", "dbslmm_plan_set_sigma", "dbslmm_plan_destroy",
+    "dbslmm_plan_download", "dbslmm_plan_set_sigma", "dbslmm_plan_destroy", "dbslmm_plan_run_multi",
     "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
     "dbslmm_bed_maf", "dbslmm_read_snp_std",
 )
@@ -67,6 +67,7 @@ def load(path: str | None = None):
     L.dbslmm_plan_sync.argtypes = [V]
     L.dbslmm_plan_download.argtypes = [V, V, V, V]
     L.dbslmm_plan_set_sigma.argtypes = [V, C.c_double]
+    L.dbslmm_plan_run_multi.argtypes = [V, V, C.c_int32, V, V, V]
     L.dbslmm_plan_destroy.argtypes = [V]
     L.dbslmm_plan_destroy.restype = None
     L.dbslmm_plan_enable_timing.argtypes = [V, C.c_int]

@@ -549,8 +549,9 @@ extern "C" __global__ __launch_bounds__(chol::kSmallWaves * chol::kWave) void db
     const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
     const int64_t* __restrict__ blk_matoff, const int32_t* __restrict__ blk_id,
     const double* __restrict__ z_slot, const int32_t* __restrict__ slot_out,
-    const double* __restrict__ rsd, double dshift, double inv_sqrt_n,
+    const double* __restrict__ rsd, const double* __restrict__ dshift_p, double inv_sqrt_n,
     double* __restrict__ beta_s, double* __restrict__ beta_l, int32_t* __restrict__ status) {
+    const double dshift = *dshift_p;   // 1/(sigma_s n): a device scalar so one launch list serves every sigma
     __shared__ __attribute__((aligned(16))) double lds[chol::kSmallWaves * chol::kSmallDoublesPerWave];
     const chol::BlockArgs a{blk_row0, blk_m, blk_ms, blk_ld, blk_matoff, blk_id, z_slot, slot_out,
                             rsd, dshift, inv_sqrt_n, beta_s, beta_l, status};
@@ -568,8 +569,10 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_la
     const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
     const int64_t* __restrict__ blk_matoff, const int32_t* __restrict__ blk_id,
     const double* __restrict__ z_slot, const int32_t* __restrict__ slot_out,
-    const double* __restrict__ rsd, double dshift, double inv_sqrt_n, double* __restrict__ y,
-    double* __restrict__ beta_s, double* __restrict__ beta_l, int32_t* __restrict__ status) {
+    const double* __restrict__ rsd, const double* __restrict__ dshift_p, double inv_sqrt_n,
+    double* __restrict__ y, double* __restrict__ beta_s, double* __restrict__ beta_l,
+    int32_t* __restrict__ status) {
+    const double dshift = *dshift_p;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const chol::BlockArgs a{blk_row0, blk_m, blk_ms, blk_ld, blk_matoff, blk_id, z_slot, slot_out,
                             rsd, dshift, inv_sqrt_n, beta_s, beta_l, status};

@@ -36,7 +36,7 @@ struct TiledArgs {
     const double* z_slot;
     const int32_t* slot_out;
     const double* rsd;
-    double dshift;
+    const double* dshift;   // device scalar 1/(sigma_s n)
     double inv_sqrt_n;
     double* y;
     double* beta_s;
@@ -318,9 +318,9 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_d
     for (int c = tid; c < m; c += chol::kLargeThreads)
         A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];   // z row of the bordered matrix
     chol::BlockArgs ba{a.blk_row0, a.blk_m, a.blk_ms, a.blk_ld, a.blk_matoff, a.blk_id, a.z_slot,
-                       a.slot_out, a.rsd, a.dshift, a.inv_sqrt_n, a.beta_s, a.beta_l, a.status};
+                       a.slot_out, a.rsd, *a.dshift, a.inv_sqrt_n, a.beta_s, a.beta_l, a.status};
     __syncthreads();
-    const bool fail = chol::diag128(A, ld, 0, m, a.blk_ms[b], a.dshift, lds, tid);
+    const bool fail = chol::diag128(A, ld, 0, m, a.blk_ms[b], *a.dshift, lds, tid);
     chol::report_status(ba, b, row0, m, tid, chol::kLargeThreads, fail && tid == 0);
 }
 
@@ -378,7 +378,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tcho
     if (I == k0n && J0 == k0n) {          // region s+1: its tiles, then factor it
         update_run(A, ld, k0n, k0n, k0n, c0, lds, tid);
         if (k0n + 1 <= Tz) update_run(A, ld, k0n + 1, k0n, min(k0n + 1, T - 1), c0, lds, tid);
-        const bool fail = diag128(A, ld, kBT * k0n, m, a.blk_ms[b], a.dshift, lds, tid);
+        const bool fail = diag128(A, ld, kBT * k0n, m, a.blk_ms[b], *a.dshift, lds, tid);
         if (fail && tid == 0) atomicMax(a.status + a.blk_id[b], DBSLMM_BLOCK_NOT_PD);
         return;
     }

@@ -44,6 +44,7 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     int gpu = 0;
     double tau = 0.8;
     bool precise = false, dry_run = false;
+    string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
 };
 
 struct Allele { int64_t pos; string a1, a2; double maf; };                 // ALLELE
@@ -79,7 +80,9 @@ void print_help() {
               << " -eff      [filename]   specify output the estimate effect SNPs.\n"
               << " --gpu     [num]        HIP device (extension)\n"
               << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
-              << " --precise-out          17 significant digits in <eff>.txt (extension)\n";
+              << " --precise-out          17 significant digits in <eff>.txt (extension)\n"
+              << " -h2f      [list]       h2 factors, e.g. 0.8,1,1.2: one Gram, one solve per factor,\n"
+              << "                        <eff>_h2f<f>.txt each (software/DBSLMM.R tuning, extension)\n";
 }
 
 // DBSLMM::Assign (scr/dbslmm.cpp:67-172): a flag's value is skipped when it starts with '-'.
@@ -107,6 +110,7 @@ void assign(int argc, char** argv, Param& p) {
         else if (!strcmp(a, "--gpu")) { if ((v = take(i))) p.gpu = atoi(v); }
         else if (!strcmp(a, "--tau")) { if ((v = take(i))) p.tau = atof(v); }
         else if (!strcmp(a, "--precise-out")) p.precise = true;
+        else if (is("--h2f", "-h2f")) { if ((v = take(i))) p.h2f = v; }
         else if (!strcmp(a, "--dry-run")) p.dry_run = true;
     }
 }
@@ -387,31 +391,63 @@ int main(int argc, char** argv) {
         prob.l_pos = l_pos.data();
         prob.z_l = z_l.data();
     }
-    vector<double> beta_s(info_s.size()), beta_l(info_l.size());
-    vector<int32_t> status(std::max(nb, 1));
+    // h2 factors (software/DBSLMM.R:204-219 runs dbslmm with -h h2 * hh for each hh); without
+    // -h2f a single run with factor 1 and the plain <eff>.txt name
+    vector<double> factors;
+    if (!p.h2f.empty()) {
+        for (const string& t : split(p.h2f, ',')) factors.push_back(atof(t.c_str()));
+        for (double f : factors)
+            if (!(f > 0) || p.h * f > 1) return fail("-h2f: h * factor must be in (0, 1]");
+    } else {
+        factors.push_back(1.0);
+    }
+    const int nf = static_cast<int>(factors.size());
+    vector<double> sigmas(nf);
+    for (int i = 0; i < nf; ++i) sigmas[i] = p.h * factors[i] / static_cast<double>(p.nsnp);
+    vector<double> beta_s(static_cast<size_t>(nf) * info_s.size()), beta_l(static_cast<size_t>(nf) * info_l.size());
+    vector<int32_t> status(static_cast<size_t>(nf) * std::max(nb, 1));
     std::cout << "Fitting model...\n";
     const double t0 = walltime();
-    const int rc = dbslmm_est(ctx, &prob, beta_s.data(), beta_l.data(), status.data());
-    if (rc != DBSLMM_OK) return fail(string("dbslmm_est: ") + dbslmm_last_error(ctx));
+    dbslmm_plan* plan = nullptr;
+    int rc = dbslmm_plan_create(ctx, &prob, &plan);
+    if (rc == DBSLMM_OK) rc = dbslmm_plan_run_multi(plan, sigmas.data(), nf, beta_s.data(), beta_l.data(), status.data());
+    dbslmm_plan_destroy(plan);
+    if (rc != DBSLMM_OK) return fail(string("dbslmm_plan_run_multi: ") + dbslmm_last_error(ctx));
     std::cout << "Fitting time: " << walltime() - t0 << " seconds.\n";
-    int n_bad = 0;
-    for (int b = 0; b < nb; ++b)
-        if (status[b] == DBSLMM_BLOCK_NOT_PD || status[b] == DBSLMM_BLOCK_MONOMORPHIC) ++n_bad;
-    if (n_bad) std::cerr << "ERROR: Matrix is Singular! (" << n_bad << " LD blocks, beta = nan)\n";
 
-    // output writer (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small rows
-    std::ofstream out(p.eff + ".txt");
-    if (p.precise) out.precision(17);
-    auto emit = [&](const vector<Info>& info, const vector<double>& beta, int flag) {
-        for (size_t i = 0; i < info.size(); ++i) {
-            const double noscl = beta[i] / std::sqrt(2 * info[i].maf * (1 - info[i].maf));
-            if (std::isinf(noscl)) continue;
-            out << info[i].snp << " " << info[i].a1 << " " << beta[i] << " " << noscl << " " << flag << "\n";
+    for (int f = 0; f < nf; ++f) {
+        int n_bad = 0;
+        for (int b = 0; b < nb; ++b) {
+            const int32_t st = status[static_cast<size_t>(f) * nb + b];
+            if (st == DBSLMM_BLOCK_NOT_PD || st == DBSLMM_BLOCK_MONOMORPHIC) ++n_bad;
         }
-    };
-    emit(info_l, beta_l, 1);
-    emit(info_s, beta_s, 0);
-    out.close();
+        if (n_bad) std::cerr << "ERROR: Matrix is Singular! (" << n_bad << " LD blocks, beta = nan)\n";
+        // output name: <eff>.txt, or with -h2f the driver's <prefix>_h2f<hh>.dbslmm.txt
+        string name = p.eff;
+        if (!p.h2f.empty()) {
+            char hh[32];
+            snprintf(hh, sizeof(hh), "%.15g", factors[f]);
+            const string ext = ".dbslmm";
+            if (name.size() > ext.size() && name.compare(name.size() - ext.size(), ext.size(), ext) == 0)
+                name = name.substr(0, name.size() - ext.size()) + "_h2f" + hh + ext;
+            else
+                name += string("_h2f") + hh;
+        }
+        // output writer (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small rows
+        std::ofstream out(name + ".txt");
+        if (p.precise) out.precision(17);
+        const double* bs = beta_s.data() + static_cast<size_t>(f) * info_s.size();
+        const double* bl = beta_l.data() + static_cast<size_t>(f) * info_l.size();
+        auto emit = [&](const vector<Info>& info, const double* beta, int flag) {
+            for (size_t i = 0; i < info.size(); ++i) {
+                const double noscl = beta[i] / std::sqrt(2 * info[i].maf * (1 - info[i].maf));
+                if (std::isinf(noscl)) continue;
+                out << info[i].snp << " " << info[i].a1 << " " << beta[i] << " " << noscl << " " << flag << "\n";
+            }
+        };
+        emit(info_l, bl, 1);
+        emit(info_s, bs, 0);
+    }
     dbslmm_ctx_destroy(ctx);
     return 0;
 }

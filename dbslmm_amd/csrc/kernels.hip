@@ -410,6 +410,9 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     }
 }
 
+// one device scalar, in stream order (the solve kernels read sigma's shift from it)
+extern "C" __global__ void dbslmm_set_scalar(double* __restrict__ dst, double v) { *dst = v; }
+
 // ------------------------------------------------------------------------------------------
 // readSNPIm + nomalizeVec for a list of rows in ORIGINAL individual order (diagnostics and
 // parity): out[j * n_ref + i] = (g_ij - mu_j) * rsd_j with missing calls at the mean (0).

@@ -78,7 +78,6 @@ struct dbslmm_plan {
     int32_t* d_tlist = nullptr;         // work lists of the tiled sequence
     std::vector<TLaunch> tl;
     hipGraphExec_t graph_exec = nullptr;   // captured tiled sequence
-    double graph_dshift = 0.0;
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
     GramTile* d_tiles = nullptr;       // 32 x 32 tiles of the small blocks (dbslmm_gram_i8)
@@ -86,6 +85,8 @@ struct dbslmm_plan {
     int32_t n_btiles = 0;
     double* d_M = nullptr;
     double *d_beta_s = nullptr, *d_beta_l = nullptr;
+    double* d_dshift = nullptr;        // 1/(sigma_s n), read by the solve kernels
+    double* d_Mkeep = nullptr;         // pristine Gram for multi-sigma runs (allocated on demand)
     std::vector<int32_t> h_ld;  // per non-empty block
     std::vector<int32_t> h_empty;  // original ids of empty blocks
     // workload figures
@@ -185,7 +186,8 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
-                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles};
+                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_dshift,
+                    p->d_Mkeep};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -454,6 +456,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = hipMemset(p->d_M, 0, std::max<int64_t>(1, p->M_elems) * sizeof(double))) != hipSuccess) return fail("hipMemset M");
     if ((e = hipMalloc(&p->d_beta_s, std::max<int64_t>(1, p->n_s) * sizeof(double))) != hipSuccess) return fail("hipMalloc beta");
     if ((e = hipMalloc(&p->d_beta_l, std::max<int64_t>(1, p->n_l) * sizeof(double))) != hipSuccess) return fail("hipMalloc beta");
+    if ((e = hipMalloc(&p->d_dshift, sizeof(double))) != hipSuccess) return fail("hipMalloc dshift");
     *out = p;
     return DBSLMM_OK;
 }
@@ -490,10 +493,10 @@ static int collect_timing(dbslmm_plan* p) {
 }
 
 // Enqueue the tiled sequence on stream2.
-static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
+static int enqueue_tiled(dbslmm_plan* p, double isn) {
     dbslmm_ctx* ctx = p->ctx;
     const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
-                             p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, dshift, isn,
+                             p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, p->d_dshift, isn,
                              p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
     hipStream_t st = ctx->stream2;
     for (const TLaunch& L : p->tl) {
@@ -512,8 +515,9 @@ static int enqueue_tiled(dbslmm_plan* p, double dshift, double isn) {
     return DBSLMM_OK;
 }
 
-int dbslmm_plan_run(dbslmm_plan* p) {
-    if (!p) return DBSLMM_E_ARG;
+// One run.  front: unpack + Gram (else the Gram of the previous front run is reused);
+// keep: 1 = save the Gram to d_Mkeep after the front, 2 = restore M from it before the solve.
+static int run_impl(dbslmm_plan* p, bool front, int keep) {
     dbslmm_ctx* ctx = p->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -529,10 +533,10 @@ int dbslmm_plan_run(dbslmm_plan* p) {
         p->runs_pending++;
     }
     const size_t nbk = std::max<int32_t>(1, std::max(p->n_nonempty, p->num_block));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
+    if (front) HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
     HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, nbk * sizeof(int32_t), s));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], s));
-    if (p->n_slots > 0) {
+    if (front && p->n_slots > 0) {
         const int wpb = 4;
         dim3 grid((p->n_slots + wpb - 1) / wpb);
         hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, s, p->d_bed, p->n_ref,
@@ -541,7 +545,7 @@ int dbslmm_plan_run(dbslmm_plan* p) {
         HIP_TRY(ctx, hipGetLastError());
     }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], s));
-    if (p->n_tiles > 0) {
+    if (front && p->n_tiles > 0) {
         dim3 grid((p->n_tiles + 3) / 4);
         hipLaunchKernelGGL(dbslmm_gram_i8, grid, dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
@@ -549,7 +553,7 @@ int dbslmm_plan_run(dbslmm_plan* p) {
                            static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M);
         HIP_TRY(ctx, hipGetLastError());
     }
-    if (p->n_btiles > 0) {
+    if (front && p->n_btiles > 0) {
         hipLaunchKernelGGL(dbslmm_gram_big, dim3(p->n_btiles), dim3(256), gram::kLdsBytes, s, p->d_G,
                            p->kpad, p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
@@ -557,9 +561,15 @@ int dbslmm_plan_run(dbslmm_plan* p) {
                            p->tau, p->d_M);
         HIP_TRY(ctx, hipGetLastError());
     }
+    if (keep && p->M_elems > 0) {
+        const size_t mb = static_cast<size_t>(p->M_elems) * sizeof(double);
+        if (keep == 1) HIP_TRY(ctx, hipMemcpyAsync(p->d_Mkeep, p->d_M, mb, hipMemcpyDeviceToDevice, s));
+        else HIP_TRY(ctx, hipMemcpyAsync(p->d_M, p->d_Mkeep, mb, hipMemcpyDeviceToDevice, s));
+    }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
     if (p->n_nonempty > 0) {
         const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
+        hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift, dshift);
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
         // fork: the tiled sequence runs on stream2 (high priority: the critical path) while the
         // single-workgroup and single-wave kernels run on the main stream.
@@ -569,7 +579,7 @@ int dbslmm_plan_run(dbslmm_plan* p) {
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M, p->d_order, p->n_large, p->d_row0, p->d_m,
                                p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z, p->d_slot_out,
-                               p->d_rsd, dshift, isn, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status);
+                               p->d_rsd, p->d_dshift, isn, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status);
             HIP_TRY(ctx, hipGetLastError());
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
@@ -582,7 +592,7 @@ int dbslmm_plan_run(dbslmm_plan* p) {
             hipLaunchKernelGGL(dbslmm_chol_small, dim3(g), dim3(chol::kSmallWaves * chol::kWave), 0,
                                ss, p->d_M, p->d_order + p->n_large, p->n_small, p->d_row0,
                                p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
-                               p->d_slot_out, p->d_rsd, dshift, isn, p->d_beta_s, p->d_beta_l,
+                               p->d_slot_out, p->d_rsd, p->d_dshift, isn, p->d_beta_s, p->d_beta_l,
                                p->d_status);
             HIP_TRY(ctx, hipGetLastError());
         }
@@ -590,16 +600,12 @@ int dbslmm_plan_run(dbslmm_plan* p) {
         if (ss != s) HIP_TRY(ctx, hipEventRecord(ctx->join, ss));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
         if (!p->tl.empty()) {
-            // the tiled sequence (~3 launches per 64-column step) is replayed from a graph
-            // captured on first use; re-captured when sigma (a kernel argument) changes
-            if (p->graph_exec && p->graph_dshift != dshift) {
-                (void)hipGraphExecDestroy(p->graph_exec);
-                p->graph_exec = nullptr;
-            }
+            // the tiled sequence (~2 launches per 128-column step) is replayed from a graph
+            // captured on first use (sigma is read from a device scalar, so it stays valid)
             if (!p->graph_exec) {
                 hipGraph_t gr = nullptr;
                 HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-                const int rc = enqueue_tiled(p, dshift, isn);
+                const int rc = enqueue_tiled(p, isn);
                 hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
                 if (rc != DBSLMM_OK) {
                     if (gr) (void)hipGraphDestroy(gr);
@@ -609,7 +615,6 @@ int dbslmm_plan_run(dbslmm_plan* p) {
                 hipError_t ie = hipGraphInstantiate(&p->graph_exec, gr, nullptr, nullptr, 0);
                 (void)hipGraphDestroy(gr);
                 HIP_TRY(ctx, ie);
-                p->graph_dshift = dshift;
             }
             HIP_TRY(ctx, hipGraphLaunch(p->graph_exec, ctx->stream2));
         }
@@ -626,6 +631,40 @@ int dbslmm_plan_run(dbslmm_plan* p) {
         HIP_TRY(ctx, hipEventRecord(ev[7], s));
     }
     p->ran = true;
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_run(dbslmm_plan* p) {
+    if (!p) return DBSLMM_E_ARG;
+    return run_impl(p, true, 0);
+}
+
+// h2f tuning (software/DBSLMM.R:204-219 runs dbslmm once per h2 factor): one unpack + Gram,
+// then one factorisation + solve per sigma, the Gram restored from a device copy in between.
+int dbslmm_plan_run_multi(dbslmm_plan* p, const double* sigmas, int32_t n_sigma, double* beta_s,
+                          double* beta_l, int32_t* block_status) {
+    if (!p) return DBSLMM_E_ARG;
+    dbslmm_ctx* ctx = p->ctx;
+    ARG_CHECK(ctx, sigmas && n_sigma > 0, "sigmas / n_sigma");
+    for (int i = 0; i < n_sigma; ++i)
+        ARG_CHECK(ctx, sigmas[i] > 0.0 && std::isfinite(sigmas[i]), "sigma_s must be > 0");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (n_sigma > 1 && !p->d_Mkeep && p->M_elems > 0)
+        HIP_TRY(ctx, hipMalloc(&p->d_Mkeep, static_cast<size_t>(p->M_elems) * sizeof(double)));
+    const double sigma0 = p->sigma_s;
+    for (int i = 0; i < n_sigma; ++i) {
+        p->sigma_s = sigmas[i];
+        int rc = run_impl(p, i == 0, n_sigma > 1 ? (i == 0 ? 1 : 2) : 0);
+        if (!rc) rc = dbslmm_plan_sync(p);
+        if (!rc) rc = dbslmm_plan_download(p, beta_s ? beta_s + static_cast<int64_t>(i) * p->n_s : nullptr,
+                                           beta_l ? beta_l + static_cast<int64_t>(i) * p->n_l : nullptr,
+                                           block_status ? block_status + static_cast<int64_t>(i) * p->num_block : nullptr);
+        if (rc) {
+            p->sigma_s = sigma0;
+            return rc;
+        }
+    }
+    p->sigma_s = sigma0;
     return DBSLMM_OK;
 }
 

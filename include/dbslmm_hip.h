@@ -115,6 +115,13 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* p, dbslmm_plan** o
 int dbslmm_plan_run(dbslmm_plan* plan);
 int dbslmm_plan_sync(dbslmm_plan* plan);
 int dbslmm_plan_download(dbslmm_plan* plan, double* beta_s, double* beta_l, int32_t* block_status);
+/* h2f tuning (replaces the three dbslmm runs of software/DBSLMM.R:204-219, -h = h2 * h2f):
+ * one unpack + Gram, then for each sigma_s[i] one factorisation + solve; outputs are
+ * n_sigma consecutive slices: beta_s[i * n_s ..], beta_l[i * n_l ..], block_status[i * num_block ..]
+ * (NULL skips).  Synchronous.  The plan's own sigma_s is unchanged. */
+int dbslmm_plan_run_multi(dbslmm_plan* plan, const double* sigma_s, int32_t n_sigma,
+                          double* beta_s, double* beta_l, int32_t* block_status);
+
 /* Change sigma_s (h2f tuning, software/DBSLMM.R:205-219) without re-uploading. */
 int dbslmm_plan_set_sigma(dbslmm_plan* plan, double sigma_s);
 void dbslmm_plan_destroy(dbslmm_plan* plan);

@@ -110,3 +110,22 @@ def test_cli_lmm_only_tau08(tmp_path):
     ref = np.array(g["lmm_tau0.8_nsnp996_direct"]["beta_s"])
     assert got.size == ref.size
     assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-10
+
+
+@pytest.mark.gpu
+def test_cli_h2f_tuning_matches_separate_runs(tmp_path):
+    """-h2f 0.8,1,1.2 (one Gram, three solves) writes the R driver's file names
+    (<prefix>_h2f<hh>.dbslmm.txt, software/DBSLMM.R:204-219) with the same rows as three runs
+    with -h 0.5*hh."""
+    s, l = split_summary(tmp_path)
+    base = ["-s", s, "-l", l, "-r", REF, "-b", BLOCKS_EUR1, "-n", "2400", "-nsnp", "996",
+            "-mafMax", "0.2", "--precise-out"]
+    prefix = str(tmp_path / "chr1")
+    r = run(base + ["-h", "0.5", "-h2f", "0.8,1,1.2", "-eff", prefix + ".dbslmm"])
+    assert r.returncode == 0, r.stderr
+    for hh in ("0.8", "1", "1.2"):
+        tuned = open(f"{prefix}_h2f{hh}.dbslmm.txt").read()
+        single = str(tmp_path / f"single{hh}")
+        r = run(base + ["-h", repr(0.5 * float(hh)), "-eff", single])
+        assert r.returncode == 0, r.stderr
+        assert tuned == open(single + ".txt").read()

@@ -202,3 +202,21 @@ def test_bench_config_vs_oracle(fit):
     got = np.concatenate([bs, bl])
     assert np.all(st[st != 1] == 0)
     assert normwise(got, ref_d) < 1e-10
+
+
+def test_run_multi_sigma_matches_separate_solves(fit):
+    """h2f tuning: one Gram, three solves == three fresh plans (bit-identical), any block path."""
+    from dbslmm_amd import Plan, synth
+    p = synth.simulate(20000, 600, seed=3, chroms=[1, 2, 3], miss_rate=0.001)
+    prob = synth.make_problem(p)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    plan = Plan(fit.ctx, prob)
+    multi = plan.run_multi(sig)
+    for f, (bs, bl, st) in zip(sig, multi):
+        q = synth.make_problem(p)
+        q.sigma_s = f
+        rs, rl, rst = fit.est(q)
+        np.testing.assert_array_equal(bs, rs)
+        np.testing.assert_array_equal(bl, rl)
+        np.testing.assert_array_equal(st, rst)
+    assert not np.array_equal(multi[0][0], multi[2][0])
