@@ -33,7 +33,7 @@ PEAK_F64_TFLOPS = 78.6       # fp64 (vector = matrix rate on gfx950)
 CONFIGS = {
     2: dict(snps=50000, n_ref=2000, pop="EUR", lmm_only=False, gen="numpy"),
     3: dict(snps=500000, n_ref=5000, pop="EUR", lmm_only=False, gen="gpu"),
-    4: dict(snps=1000000, n_ref=10000, pop="EUR", lmm_only=False, gen="gpu"),
+    4: dict(snps=1000000, n_ref=10000, pop="EUR", lmm_only=False, gen="gpu", h2f="0.8,1,1.2"),
     5: dict(snps=1000000, n_ref=10000, pop="AFR", lmm_only=True, gen="gpu"),
 }
 
@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--n-ref", type=int, default=None)
     ap.add_argument("--pop", default=None)
     ap.add_argument("--lmm-only", action="store_true", default=None)
+    ap.add_argument("--h2f", default=None,
+                    help="h2 factors, e.g. 0.8,1,1.2: one Gram + one solve per factor per step "
+                         "(DBSLMM tuning, config 4)")
     ap.add_argument("--gen", choices=("numpy", "gpu"), default=None,
                     help="synthetic panel generator (default: numpy for config 2, gpu above)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,10 +61,12 @@ def parse():
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    a.h2f = [float(x) for x in a.h2f.split(",")] if a.h2f else None
     return a
 
 
-def kernel_roofline(name, ms, wl):
+def kernel_roofline(name, ms, wl, n_solve=1):
+    """ms = the kernel's time per step; n_solve = solves per step (h2f factors)."""
     s = ms * 1e-3
     if name == "dbslmm_unpack_stats":
         b = wl["unpack_read_bytes"] + wl["unpack_write_bytes"]
@@ -75,8 +80,8 @@ def kernel_roofline(name, ms, wl):
                     executed_tops=wl["gram_ops_exec"] / s / 1e12,
                     note="int8 ops (2/MAC), algorithmic sum_b n_ref*m_b*(m_b+1); executed = "
                          "padded tiles x padded individuals")
-    fl = {"dbslmm_chol_large": wl["chol_flops_large"], "dbslmm_chol_small": wl["chol_flops_small"],
-          "dbslmm_tchol": wl["chol_flops_tiled"]}[name]
+    fl = n_solve * {"dbslmm_chol_large": wl["chol_flops_large"], "dbslmm_chol_small": wl["chol_flops_small"],
+                    "dbslmm_tchol": wl["chol_flops_tiled"]}[name]
     a = fl / s / 1e12 if s > 0 else 0.0
     return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
                 frac=a / PEAK_F64_TFLOPS, algorithmic=fl, ms=ms,
@@ -128,8 +133,16 @@ def main():
     plan = Plan(ctx, prob)
     wl = plan.workload()
 
+    sigmas = [prob.sigma_s * f for f in args.h2f] if args.h2f else None
+
+    def step():
+        if sigmas:
+            plan.run_multi(sigmas)      # one Gram, len(sigmas) solves (synchronous)
+        else:
+            plan.run()
+
     for _ in range(args.warmup):
-        plan.run()
+        step()
     plan.sync()
     torch.cuda.synchronize()
     barrier()
@@ -137,14 +150,19 @@ def main():
     plan.enable_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.run()
+        step()
     plan.sync()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kms, nlaunch = plan.kernel_ms()
-    beta_s, beta_l, status = plan.download()
+    kms = kms * nlaunch / args.steps          # per step (a tuning step is len(h2f) runs)
+    if sigmas:   # the bench compares the h2f = 1 (or first) solve with the CPU reference
+        i1 = args.h2f.index(1.0) if 1.0 in args.h2f else 0
+        beta_s, beta_l, status = plan.run_multi([sigmas[i1]])[0]
+    else:
+        beta_s, beta_l, status = plan.download()
 
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     snps = torch.tensor([wl["snps"]], dtype=torch.float64, device="cuda")
@@ -155,7 +173,8 @@ def main():
     total_snps = float(snps.item())
     value = total_snps * args.steps / elapsed
 
-    kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl) for k in range(len(KERNEL_NAMES))]
+    n_solve = len(sigmas) if sigmas else 1
+    kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl, n_solve) for k in range(len(KERNEL_NAMES))]
     dom = max(kernels, key=lambda r: r["ms"])
     traffic, tsrc = pmc_traffic(dom["kernel"], args)
     roof = dict(bound=dom["bound"], achieved=dom["achieved"], peak=dom["peak"], unit=dom["unit"],
@@ -235,6 +254,7 @@ def main():
             "config": {"workload": f"synthetic {args.snps} SNP x {args.n_ref} indiv, 22 chr "
                                    f"{args.pop} LD blocks, {'LMM-only' if args.lmm_only else 'DBSLMM large+small'}, "
                                    f"h2=0.5 (BASELINE configs[{args.config - 1}])", "generator": args.gen,
+                       "h2f": args.h2f,
                        "snps_per_gpu": wl["snps"], "n_ref": args.n_ref, "blocks": wl["blocks"],
                        "gram": "exact int8 dosages on v_mfma_i32_32x32x32_i8, fp64 epilogue",
                        "solve": "fp64 Cholesky of the joint per-block matrix",
