@@ -3,7 +3,7 @@
 // row m, beta = L^{-T} y / sqrt n), but every block with m >= the tiled threshold is spread over
 // many workgroups, batched across blocks, one launch per phase of a 64-wide panel step:
 //
-//   tchol_diag0          step 0 only: factor + invert diagonal tile (0, 0)
+//   tchol_region(r)      factor + invert the 128 x 128 diagonal region r in LDS
 //   tchol_panel(k)       L_ik = A_ik X_kk^T for every tile row i > k     (one workgroup per tile)
 //   tchol_trailing(k)    C_ij -= L_ik L_jk^T, k < j <= i                 (one workgroup per tile)
 //                        -- the first workgroups take tile (k+1, k+1): update, then factor +
@@ -72,57 +72,6 @@ __device__ __forceinline__ void zero_acc(v4d (&acc)[2][2]) {
         for (int sj = 0; sj < 2; ++sj) acc[si][sj] = v4d{0.0, 0.0, 0.0, 0.0};
 }
 
-// Wave-level factorisation + inversion of the 64x64 diagonal tile at (c0, c0) (rows <= m).
-// lds: >= 6 sub-tiles + 2*kT.  Returns true when a pivot was not positive.
-__device__ __forceinline__ bool factor_diag64(double* A, int ld, int c0, int m, int ms, double dshift,
-                              double* lds, int lane) {
-    double* Xl = lds;                 // X00, later X11
-    double* Lb = lds + kSub;
-    double* L10 = lds + 2 * kSub;
-    double* XT = lds + 3 * kSub;      // X00^T
-    double* TT = lds + 4 * kSub;      // (L10 X00)^T
-    double* W = lds + 5 * kSub;
-    double* colb = lds + 6 * kSub;
-    bool fail = factor_diag(A, ld, c0, m, ms, dshift, Xl, Lb, colb, lane, false);
-    if (c0 + kT > m) return fail;     // the tile ends inside its first half
-    // X00^T, A10 -> LDS
-    for (int e = lane; e < kT * kT; e += kWave) {
-        const int q = e >> 5, r = e & 31;
-        XT[r * kTS + q] = Xl[q * kTS + r];
-    }
-    stage_tile(W, A, ld, c0 + kT, c0, lane);
-    wave_sync();
-    v4d acc[2][2];
-    zero_acc(acc);
-    mfma_tile(acc, W, Xl, 1.0, lane);                  // L10 = A10 X00^T
-    store_acc(acc, A, ld, c0 + kT, c0, lane);
-    acc_to_lds(acc, L10, lane);
-    wave_sync();
-    v4d c11[2][2];
-    load_acc(c11, A, ld, c0 + kT, c0 + kT, lane);
-    mfma_tile(c11, L10, L10, -1.0, lane);              // A11 -= L10 L10^T
-    acc_to_lds(c11, Lb, lane);
-    wave_sync();
-    fail |= factor_diag(A, ld, c0 + kT, m, ms, dshift, Xl, Lb, colb, lane, true);   // Xl = X11
-    zero_acc(acc);
-    mfma_tile(acc, L10, XT, 1.0, lane);                // T = L10 X00
-    acc_to_lds_t(acc, TT, lane);
-    wave_sync();
-    zero_acc(acc);
-    mfma_tile(acc, Xl, TT, -1.0, lane);                // X10 = -X11 T
-    // X10^T -> sub-tile (0, 1): element (r, 32 + c) = X10[c][r]
-#pragma unroll
-    for (int si = 0; si < 2; ++si)
-#pragma unroll
-        for (int sj = 0; sj < 2; ++sj)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int R = 16 * si + (lane >> 4) + 4 * q, Cc = 16 * sj + (lane & 15);
-                A[static_cast<int64_t>(c0 + Cc) * ld + c0 + kT + R] = acc[si][sj][q];
-            }
-    return fail;
-}
-
 // 64x64 tile (r0, c0) -> 4 LDS sub-tiles: S[2a + b] = rows 32a.., cols 32b..
 __device__ __forceinline__ void stage64(double* S, const double* A, int ld, int r0, int c0, int tid) {
     constexpr int NT = kLargeThreads;
@@ -144,12 +93,13 @@ __device__ __forceinline__ void stage64(double* S, const double* A, int ld, int 
 
 // ---------------------------------------------------------------- 128-column outer steps
 // Outer step s covers tile columns k0 = 2s, k1 = 2s + 1 (columns c0 = 128 s ..).  Its 128 x 128
-// diagonal region R is factored by diag128 (two factor_diag64 + MFMA glue) and holds, after it:
-// strict lower = L_RR, diagonal + upper (r, c >= r) = X[c][r], X = L_RR^{-1} (so each 64 x 64
-// diagonal tile keeps its own inverse for the backward solve, and tile (k0, k1) holds X10^T).
-// panel128(s):    L_i = A_i X^T for 64-row tiles i below R; workgroup = (i, column half h)
-// trailing128(s): C_IJ -= L_{I,s} L_{J,s}^T with K = 128 (two 64-deep phases, C in registers)
-//                 for J >= k1 + 1; the first workgroups update region s+1 and run diag128 on it.
+// diagonal region is factored by dbslmm_tchol_region and holds, after it: strict lower = L,
+// each 64 x 64 diagonal tile's diagonal + upper (r, c >= r) = X[c][r] of its own inverse (what the
+// panel and the backward solve read).
+// panel(s):    L_i = A_i L_RR^{-T} for 64-row tiles i below the region (substitution over the
+//              region's two 64-column halves)
+// trailing(s): C_IJ -= L_{I,s} L_{J,s}^T with K = 128 (two 64-deep phases, C in registers)
+//              for the tile rows below region s+1.
 namespace chol {
 
 // X block (64 x 64) in row-major form from the stored upper triangle: X[q][r] = A(rr0 + r,
@@ -162,6 +112,23 @@ __device__ __forceinline__ void stage_x(double* S, const double* A, int ld, int 
         const int e = it * kLargeThreads + tid, r = e >> 6, q = e & 63;
         v[it] = (!diag || q >= r) ? A[static_cast<int64_t>(rr0 + r) * ld + cc0 + q] : 0.0;
     }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int e = it * kLargeThreads + tid, r = e >> 6, q = e & 63;
+        S[(2 * (q >> 5) + (r >> 5)) * kSub + (q & 31) * kTS + (r & 31)] = v[it];
+    }
+}
+
+// stage_x split into its loads (registers) and its LDS stores, so loads can be issued early
+__device__ __forceinline__ void xregs_load(double (&v)[16], const double* A, int ld, int rr0, int cc0,
+                                           bool diag, int tid) {
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int e = it * kLargeThreads + tid, r = e >> 6, q = e & 63;
+        v[it] = (!diag || q >= r) ? A[static_cast<int64_t>(rr0 + r) * ld + cc0 + q] : 0.0;
+    }
+}
+__device__ __forceinline__ void xregs_store(const double (&v)[16], double* S, int tid) {
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int e = it * kLargeThreads + tid, r = e >> 6, q = e & 63;
@@ -201,65 +168,95 @@ __device__ __forceinline__ void tile_regs_store(const double (&v)[16], double* S
     }
 }
 
-// Factor + invert the 128 x 128 diagonal region at (c0, c0), rows <= m (whole workgroup).
-// LDS: 8 sub-tiles + 2 kT + 8 doubles.  Returns true (on every thread) on a non-positive pivot.
-__device__ __forceinline__ bool diag128(double* A, int ld, int c0, int m, int ms, double dshift, double* lds, int tid) {
-    const int lane = tid & 63, wave = tid >> 6, qi = wave >> 1, qj = wave & 1;
-    int* fflag = reinterpret_cast<int*>(lds + 8 * kSub + 2 * kT);
-    if (tid == 0) *fflag = 0;
-    __syncthreads();
-    if (wave == 0) {
-        const bool f = factor_diag64(A, ld, c0, m, ms, dshift, lds, lane);
-        if (f && lane == 0) *fflag = 1;
+// 32 x 32 tile in LDS (stride kTS, lower triangle valid, rows beyond m zero): factor and invert
+// it in one pass (the scheme of factor_diag: row lanes factor, lanes 32..63 carry the columns of
+// X = L^{-1}).  L goes back into T (strict upper zeroed), X row-major into Xo.
+__device__ __forceinline__ bool factor_tile_lds(double* T, double* Xo, double* colb, int c0, int m,
+                                                int ms, double dshift, int lane) {
+    const int r = lane & 31;
+    const bool xlane = lane >= kT;
+    const int jmax = min(kT, m - c0);
+    double v[kT];
+#pragma unroll
+    for (int c = 0; c < kT; ++c) {
+        double t = xlane ? (c == r ? 1.0 : 0.0) : (c <= r ? T[r * kTS + c] : 0.0);
+        if (!xlane && c == r && c0 + r < ms) t += dshift;
+        v[c] = t;
     }
-    __syncthreads();
-    if (c0 + kBT > m) return *fflag != 0;          // no rows in the second half
-    double* XS = lds;
-    double* W = lds + 4 * kSub;
-    stage_x(XS, A, ld, c0, c0, true, tid);          // X00
-    stage64(W, A, ld, c0 + kBT, c0, tid);           // A10
-    __syncthreads();
-    v4d acc[2][2];
-    zero_acc(acc);
-    for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
-    __syncthreads();
-    store_acc(acc, A, ld, c0 + kBT + kT * qi, c0 + kT * qj, lane);   // L10
-    acc_to_lds(acc, W + (2 * qi + qj) * kSub, lane);
-    stage_upper(XS, A, ld, c0, c0, tid);            // X00^T
-    __syncthreads();
-    if (qj <= qi) {                                 // A11 -= L10 L10^T
-        v4d c11[2][2];
-        load_acc(c11, A, ld, c0 + kBT + kT * qi, c0 + kBT + kT * qj, lane);
-        for (int kc = 0; kc < 2; ++kc) mfma_tile(c11, W + (2 * qi + kc) * kSub, W + (2 * qj + kc) * kSub, -1.0, lane);
-        store_acc(c11, A, ld, c0 + kBT + kT * qi, c0 + kBT + kT * qj, lane);
+    wave_sync();
+    bool fail = false;
+#pragma unroll
+    for (int j = 0; j < kT; ++j) {
+        if (j < jmax) {
+            const double p = readlane_f64(v[j], j);
+            fail |= !(p > 0.0);
+            const double rs = rsqrt_f64(p);
+            v[j] = (!xlane && r < j) ? 0.0 : v[j] * rs;
+            if (!xlane) colb[r] = v[j];
+            wave_sync();
+#pragma unroll
+            for (int k0 = (j + 1) & ~7; k0 < kT; k0 += 8) {
+                double col[8];
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    const v2d t = *reinterpret_cast<const v2d*>(colb + k0 + k);
+                    col[k] = t[0];
+                    col[k + 1] = t[1];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k0 + k > j) v[k0 + k] -= v[j] * col[k];
+            }
+            wave_sync();
+        }
     }
-    zero_acc(acc);                                  // T = L10 X00, parked in tile (k0, k1)
-    for (int kc = qj; kc < 2; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
-    store_acc(acc, A, ld, c0 + kT * qi, c0 + kBT + kT * qj, lane);
-    __syncthreads();
-    if (wave == 0) {
-        const bool f = factor_diag64(A, ld, c0 + kBT, m, ms, dshift, lds, lane);
-        if (f && lane == 0) *fflag = 1;
+    if (!xlane) {
+#pragma unroll
+        for (int c = 0; c < kT; ++c) T[r * kTS + c] = c <= r ? v[c] : 0.0;
+    } else {
+#pragma unroll
+        for (int q = 0; q < kT; ++q) Xo[q * kTS + r] = q >= jmax ? (q == r ? 1.0 : 0.0) : v[q];
     }
-    __syncthreads();
-    stage_x(XS, A, ld, c0 + kBT, c0 + kBT, true, tid);   // X11
-    stage_x(W, A, ld, c0, c0 + kBT, false, tid);          // T^T (row-major transpose of T)
-    __syncthreads();
-    zero_acc(acc);                                  // X10 = -X11 T
-    for (int kc = 0; kc <= qi; ++kc) mfma_tile(acc, XS + (2 * qi + kc) * kSub, W + (2 * qj + kc) * kSub, -1.0, lane);
-    // X10^T over T: element (r, 64 + c) = X10[c][r]
+    wave_sync();
+    return fail;
+}
+
+// acc (2 x 2 of 16 x 16) += sign * P Q^T with Q given TRANSPOSED in LDS (Qt[k][ri], stride kTS)
+__device__ __forceinline__ void mfma_tile_qt(v4d (&acc)[2][2], const double* P, const double* Qt,
+                                             double sign, int lane) {
+    const int ri = lane & 15, kq = lane >> 4;
+    double p0[kT / 4], p1[kT / 4], q0[kT / 4], q1[kT / 4];
+#pragma unroll
+    for (int kk = 0; kk < kT / 4; ++kk) {
+        const int k = 4 * kk + kq;
+        p0[kk] = P[ri * kTS + k];
+        p1[kk] = P[(16 + ri) * kTS + k];
+        q0[kk] = Qt[k * kTS + ri];
+        q1[kk] = Qt[k * kTS + 16 + ri];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kT / 4; ++kk) {
+        const double a0 = sign * p0[kk], a1 = sign * p1[kk];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q0[kk], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, q1[kk], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, q0[kk], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, q1[kk], acc[1][1], 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void lds_to_acc(v4d (&acc)[2][2], const double* W, int lane) {
 #pragma unroll
     for (int si = 0; si < 2; ++si)
 #pragma unroll
         for (int sj = 0; sj < 2; ++sj)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int R = kT * qi + 16 * si + (lane >> 4) + 4 * q, Cc = kT * qj + 16 * sj + (lane & 15);
-                A[static_cast<int64_t>(c0 + Cc) * ld + c0 + kBT + R] = acc[si][sj][q];
-            }
-    __syncthreads();
-    return *fflag != 0;
+            for (int q = 0; q < 4; ++q)
+                acc[si][sj][q] = W[(16 * si + (lane >> 4) + 4 * q) * kTS + 16 * sj + (lane & 15)];
 }
+
+// lower sub-tiles (a >= b) of a 128 x 128 region, 4 x 4 of 32
+__device__ __forceinline__ int rsub(int a, int b) { return a * (a + 1) / 2 + b; }
+constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X10 (2) + colb
 
 // C(I, J..) -= L_{I,s} L_{J,s}^T, K = 128 as two 64-deep phases, over a run of tiles J0..J1 of
 // tile row I (skips the strictly-upper quadrant of a diagonal tile).  Next phase's operands and
@@ -306,83 +303,223 @@ __device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int
 }  // namespace chol
 
 // ---------------------------------------------------------------- kernels
-// step 0: z row, factor + invert region 0 of each tiled block; flag monomorphic SNPs
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_diag0(
-    chol::TiledArgs a, const int32_t* __restrict__ blocks, int32_t n) {
+// Factor region r (128 x 128 at c0 = 128 r) of each listed block, entirely in LDS (one workgroup
+// per block, 4 waves): load the region's lower sub-tiles -- applying the pending K = 128 update
+// C -= P P^T from the panel of step r-1 when `update` (P staged one 32-column slice at a time) --
+// then four 32-column steps (wave 0: factor_tile_lds; all waves: MFMA panel and trailing updates
+// inside the region), the 64-level inverse blocks X10 = -X11 L10 X00 of its two 64 x 64
+// diagonal tiles, and one write-back: strict lower = L, each 64 x 64 diagonal tile's diagonal +
+// upper = its X^T (what the panel and the backward solve read).  Region 0 without update also
+// writes the z row and flags monomorphic SNPs.
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_region(
+    chol::TiledArgs a, int32_t reg, int32_t update, const int32_t* __restrict__ blocks, int32_t n) {
+    using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n) return;
     const int b = blocks[blockIdx.x];
-    const int tid = threadIdx.x;
-    const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b], ms = a.blk_ms[b];
     double* A = a.M + a.blk_matoff[b];
-    for (int c = tid; c < m; c += chol::kLargeThreads)
-        A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];   // z row of the bordered matrix
-    chol::BlockArgs ba{a.blk_row0, a.blk_m, a.blk_ms, a.blk_ld, a.blk_matoff, a.blk_id, a.z_slot,
-                       a.slot_out, a.rsd, *a.dshift, a.inv_sqrt_n, a.beta_s, a.beta_l, a.status};
+    const double dshift = *a.dshift;
+    const int c0 = 2 * kBT * reg;
+    double* R = lds;
+    double* X32 = lds + 10 * kSub;
+    double* X10 = lds + 14 * kSub;
+    double* colb = lds + 16 * kSub;
+    int* fflag = reinterpret_cast<int*>(colb + 2 * kT);
+    if (tid == 0) *fflag = 0;
+    if (reg == 0 && !update) {
+        for (int c = tid; c < m; c += kLargeThreads)
+            A[static_cast<int64_t>(m) * ld + c] = a.z_slot[row0 + c];   // z row
+        __syncthreads();
+    }
+    // 1) region -> registers (wave w owns sub-tiles w, w + 4, w + 8), pending update, -> LDS
+    v4d acc[3][2][2];
+    int qa[3], qb[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int q = wave + 4 * u;
+        int aa = 0;
+        while ((aa + 1) * (aa + 2) / 2 <= q) ++aa;
+        qa[u] = aa;
+        qb[u] = q - aa * (aa + 1) / 2;
+        if (q < 10) load_acc(acc[u], A, ld, c0 + kT * qa[u], c0 + kT * qb[u], lane);
+    }
+    if (update) {
+        double* P = X32;   // staging of one 32-column slice of the panel rows (4 sub-tiles)
+        const int cp = c0 - 2 * kBT;
+        for (int k = 0; k < 4; ++k) {
+            __syncthreads();
+            stage_tile(P + wave * kSub, A, ld, c0 + kT * wave, cp + kT * k, lane);
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+                if (wave + 4 * u < 10) mfma_tile(acc[u], P + qa[u] * kSub, P + qb[u] * kSub, -1.0, lane);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+        if (wave + 4 * u < 10) acc_to_lds(acc[u], R + (wave + 4 * u) * kSub, lane);
     __syncthreads();
-    const bool fail = chol::diag128(A, ld, 0, m, a.blk_ms[b], *a.dshift, lds, tid);
-    chol::report_status(ba, b, row0, m, tid, chol::kLargeThreads, fail && tid == 0);
+    // 2) four 32-column steps inside the region
+    for (int t = 0; t < 4; ++t) {
+        if (c0 + kT * t >= m) break;
+        if (wave == 0) {
+            const bool f = factor_tile_lds(R + rsub(t, t) * kSub, X32 + t * kSub, colb, c0 + kT * t,
+                                           m, ms, dshift, lane);
+            if (f && lane == 0) *fflag = 1;
+        }
+        __syncthreads();
+        {   // panel: R[i][t] <- R[i][t] X_t^T
+            const int i = t + 1 + wave;
+            if (i <= 3 && c0 + kT * i <= m) {
+                v4d pc[2][2];
+                zero_acc(pc);
+                mfma_tile(pc, R + rsub(i, t) * kSub, X32 + t * kSub, 1.0, lane);
+                acc_to_lds(pc, R + rsub(i, t) * kSub, lane);
+            }
+        }
+        __syncthreads();
+        {   // trailing: R[i][j] -= R[i][t] R[j][t]^T, t < j <= i <= 3
+            const int nt = 3 - t, np = nt * (nt + 1) / 2;
+            for (int pq = wave; pq < np; pq += 4) {
+                int ii = 0;
+                while ((ii + 1) * (ii + 2) / 2 <= pq) ++ii;
+                const int i = t + 1 + ii, j = t + 1 + (pq - ii * (ii + 1) / 2);
+                if (c0 + kT * i > m) continue;
+                v4d tc[2][2];
+                lds_to_acc(tc, R + rsub(i, j) * kSub, lane);
+                mfma_tile(tc, R + rsub(i, t) * kSub, R + rsub(j, t) * kSub, -1.0, lane);
+                acc_to_lds(tc, R + rsub(i, j) * kSub, lane);
+            }
+        }
+        __syncthreads();
+    }
+    // 3) 64-level inverse blocks: X10_p = -X_{2p+1} (L_{2p+1,2p} X_{2p}), p = wave (0, 1)
+    if (wave < 2 && c0 + kBT * wave + kT <= m) {
+        const int p = wave;
+        {
+            v4d tt[2][2];
+            zero_acc(tt);
+            mfma_tile_qt(tt, R + rsub(2 * p + 1, 2 * p) * kSub, X32 + 2 * p * kSub, 1.0, lane);   // T = L10 X00
+            acc_to_lds(tt, X10 + p * kSub, lane);
+            chol::wave_sync();
+            zero_acc(tt);
+            mfma_tile_qt(tt, X32 + (2 * p + 1) * kSub, X10 + p * kSub, -1.0, lane);          // -X11 T
+            chol::wave_sync();
+            acc_to_lds(tt, X10 + p * kSub, lane);
+        }
+    }
+    __syncthreads();
+    // 4) write-back
+    for (int q = 0; q < 10; ++q) {
+        int aa = 0;
+        while ((aa + 1) * (aa + 2) / 2 <= q) ++aa;
+        const int bb = q - aa * (aa + 1) / 2;
+        const double* S = R + q * kSub;
+        for (int e = tid; e < kT * kT; e += kLargeThreads) {
+            const int rr = e >> 5, cc = e & 31;
+            const int gr = c0 + kT * aa + rr, gc = c0 + kT * bb + cc;
+            if (gr > m || gc >= m) continue;
+            if (aa == bb && cc >= rr) continue;
+            A[static_cast<int64_t>(gr) * ld + gc] = S[rr * kTS + cc];
+        }
+    }
+    for (int t = 0; t < 4; ++t) {      // diagonal + upper of the 32-level diagonal sub-tiles: X^T
+        const int jm = min(kT, m - (c0 + kT * t));
+        if (jm <= 0) break;
+        const double* X = X32 + t * kSub;
+        for (int e = tid; e < kT * kT; e += kLargeThreads) {
+            const int rr = e >> 5, cc = e & 31;
+            if (cc >= rr && rr < jm)
+                A[static_cast<int64_t>(c0 + kT * t + rr) * ld + c0 + kT * t + cc] = X[cc * kTS + rr];
+        }
+    }
+    for (int p = 0; p < 2; ++p) {      // upper-right sub-tile of each 64 x 64 diagonal tile: X10^T
+        if (c0 + kBT * p + kT > m) break;
+        const double* X = X10 + p * kSub;
+        for (int e = tid; e < kT * kT; e += kLargeThreads) {
+            const int rr = e >> 5, cc = e & 31;
+            A[static_cast<int64_t>(c0 + kBT * p + rr) * ld + c0 + kBT * p + kT + cc] = X[cc * kTS + rr];
+        }
+    }
+    const bool fail = *fflag != 0;
+    if (reg == 0 && !update) {
+        chol::BlockArgs ba{a.blk_row0, a.blk_m, a.blk_ms, a.blk_ld, a.blk_matoff, a.blk_id, a.z_slot,
+                           a.slot_out, a.rsd, dshift, a.inv_sqrt_n, a.beta_s, a.beta_l, a.status};
+        chol::report_status(ba, b, row0, m, tid, chol::kLargeThreads, fail && tid == 0);
+    } else if (fail && tid == 0) {
+        atomicMax(a.status + a.blk_id[b], DBSLMM_BLOCK_NOT_PD);
+    }
 }
 
-// panel of outer step s: items (block << 16) | (i << 8) | h -> L(i, column half h)
+// panel of outer step s, one workgroup per 64-row tile i below region s (item (block << 16) |
+// (i << 8)): L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of
+// the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_panel(
     chol::TiledArgs a, int32_t s, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
     const int32_t it = items[blockIdx.x];
-    const int b = it >> 16, i = (it >> 8) & 255, h = it & 255;
+    const int b = it >> 16, i = (it >> 8) & 255;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qi = wave >> 1, qj = wave & 1;
-    const int ld = a.blk_ld[b];
+    const int m = a.blk_m[b], ld = a.blk_ld[b];
+    const int T = (m + kBT - 1) / kBT;
     double* A = a.M + a.blk_matoff[b];
     const int c0 = 2 * kBT * s;
     double* XS = lds;
     double* W = lds + 4 * kSub;
+    const bool two = 2 * s + 1 <= T - 1;            // the region has a second column tile
+    // every global load of the workgroup first (one latency), then the three products
+    double x00[16], ai0[16], l10[16], x11[16];
+    v4d cc[2][2];
+    xregs_load(x00, A, ld, c0, c0, true, tid);
+    tile_regs_load(ai0, A, ld, kBT * i, c0, tid);
+    if (two) {
+        tile_regs_load(l10, A, ld, c0 + kBT, c0, tid);
+        xregs_load(x11, A, ld, c0 + kBT, c0 + kBT, true, tid);
+        load_acc(cc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);   // A_i1
+    }
+    xregs_store(x00, XS, tid);
+    tile_regs_store(ai0, W, tid);
+    __syncthreads();
     v4d acc[2][2];
     zero_acc(acc);
-    // h = 0: A_{i,0} X00^T;  h = 1: A_{i,0} X10^T + A_{i,1} X11^T
-    stage_x(XS, A, ld, c0, c0 + kBT * h, h == 0, tid);
-    stage64(W, A, ld, kBT * i, c0, tid);
+    for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
+    store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);           // L_i0
+    if (!two) return;
     __syncthreads();
-    for (int kc = 0; kc < 2; ++kc)
-        if (h == 1 || kc <= qj) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
-    if (h == 1) {
-        __syncthreads();
-        stage_x(XS, A, ld, c0 + kBT, c0 + kBT, true, tid);
-        stage64(W, A, ld, kBT * i, c0 + kBT, tid);
-        __syncthreads();
-        for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
-    }
-    store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kBT * h + kT * qj, lane);
+    acc_to_lds(acc, W + (2 * qi + qj) * kSub, lane);
+    tile_regs_store(l10, XS, tid);
+    __syncthreads();
+    for (int kc = 0; kc < 2; ++kc) mfma_tile(cc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, -1.0, lane);
+    __syncthreads();
+    acc_to_lds(cc, W + (2 * qi + qj) * kSub, lane);                          // A_i1 - L_i0 L10^T
+    xregs_store(x11, XS, tid);
+    __syncthreads();
+    zero_acc(acc);
+    for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
+    store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);     // L_i1
 }
 
 // trailing update of outer step s.  Items (block << 16) | (I << 8) | J0, -1 = padding: a run of
-// tiles (I, J0 .. J0 + kJRun - 1) (clipped to the lower triangle).  The list starts with one
-// item per active block for region s+1 (I = J0 = 2s + 2): that workgroup updates the region's
-// tiles and factors it (lookahead); then per-XCD queues (item e runs on XCD e % 8; the runs of
-// one tile row I of a block share an XCD, so L_I is served by its L2).
+// tiles (I, J0 .. J0 + run - 1) (clipped to the lower triangle; run = kJRun while the step has
+// plenty of tiles, 1 in the short tail steps), for tile rows below region
+// s+1 (which dbslmm_tchol_region updates and factors itself); per-XCD queues (item e runs on
+// XCD e % 8; the runs of one tile row I of a block share an XCD, so L_I is served by its L2).
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_trailing(
-    chol::TiledArgs a, int32_t s, const int32_t* __restrict__ items, int32_t n_items) {
+    chol::TiledArgs a, int32_t s, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
     const int32_t it = items[blockIdx.x];
     if (it < 0) return;
     const int b = it >> 16, I = (it >> 8) & 255, J0 = it & 255;
-    const int tid = threadIdx.x;
     const int m = a.blk_m[b], ld = a.blk_ld[b];
-    const int T = (m + kBT - 1) / kBT, Tz = m / kBT;
+    const int T = (m + kBT - 1) / kBT;
     double* A = a.M + a.blk_matoff[b];
-    const int c0 = 2 * kBT * s;
-    const int k0n = 2 * s + 2;
-    if (I == k0n && J0 == k0n) {          // region s+1: its tiles, then factor it
-        update_run(A, ld, k0n, k0n, k0n, c0, lds, tid);
-        if (k0n + 1 <= Tz) update_run(A, ld, k0n + 1, k0n, min(k0n + 1, T - 1), c0, lds, tid);
-        const bool fail = diag128(A, ld, kBT * k0n, m, a.blk_ms[b], *a.dshift, lds, tid);
-        if (fail && tid == 0) atomicMax(a.status + a.blk_id[b], DBSLMM_BLOCK_NOT_PD);
-        return;
-    }
-    update_run(A, ld, I, J0, min(J0 + kJRun - 1, min(I, T - 1)), c0, lds, tid);
+    update_run(A, ld, I, J0, min(J0 + run - 1, min(I, T - 1)), 2 * kBT * s, lds, threadIdx.x);
 }
 
 // backward step J (launches J = Kmax-1 .. 0).  v lives in y[row0 ..]; x_J overwrites v_J once

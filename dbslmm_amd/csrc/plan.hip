@@ -36,13 +36,14 @@ namespace {
 constexpr int kEvPerRun = 8;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
+constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
-    int kind;         // 0 diag0, 1 panel, 2 trailing (+ lookahead diagonal), 3 backward
+    int kind;         // 0 region 0, 1 panel, 2 trailing, 3 backward, 4 region `step` with update
     int step;
     int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
     int32_t n;
@@ -151,9 +152,9 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                             static_cast<int>(kCholLargeLds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_big),
                             hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_diag0),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_region),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTiledLds)) != hipSuccess ||
+                            static_cast<int>(kRegionLds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_panel),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kTiledLds)) != hipSuccess ||
@@ -365,19 +366,24 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         const int Smax = (Kmax + 1) / 2;
         for (int st = 0; st < Smax; ++st) {
             const int k1 = 2 * st + 1;
-            std::vector<int32_t> panel, head;
-            std::vector<std::vector<int32_t>> q(kXcd), none(kXcd);
+            std::vector<int32_t> panel, head, regs;
+            std::vector<std::vector<int32_t>> q(kXcd);
             std::vector<int64_t> load(kXcd, 0);
+            int64_t ntiles = 0;          // trailing tiles of this step: runs of kJRun only if plenty
             for (int32_t b : tb) {
                 const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
-                for (int i = k1 + 1; i <= Tz; ++i)
-                    for (int h = 0; h < 2 && k1 - 1 + h <= T - 1; ++h) panel.push_back((b << 16) | (i << 8) | h);
+                for (int I = k1 + 3; I <= Tz; ++I) ntiles += std::min(I, T - 1) - k1;
+            }
+            const int run = ntiles >= 4096 ? chol::kJRun : 1;
+            for (int32_t b : tb) {
+                const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
+                for (int i = k1 + 1; i <= Tz; ++i) panel.push_back((b << 16) | (i << 8));
                 if (k1 + 1 > T - 1) continue;          // no columns beyond this step's region
-                head.push_back((b << 16) | ((k1 + 1) << 8) | (k1 + 1));   // region s+1 (lookahead)
+                regs.push_back(b);                      // region s+1: update + factor in LDS
                 for (int I = k1 + 3; I <= Tz; ++I) {
                     const int jmax = std::min(I, T - 1);
                     const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                    for (int J = k1 + 1; J <= jmax; J += chol::kJRun) q[x].push_back((b << 16) | (I << 8) | J);
+                    for (int J = k1 + 1; J <= jmax; J += run) q[x].push_back((b << 16) | (I << 8) | J);
                     load[x] += jmax - k1;
                 }
             }
@@ -386,7 +392,14 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                 tlist.insert(tlist.end(), panel.begin(), panel.end());
                 p->tl.push_back(L);
             }
-            if (!head.empty()) add_items(2, st, head, q);
+            if (!regs.empty()) {
+                TLaunch L{4, st + 1, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(regs.size()),
+                          static_cast<int32_t>(regs.size())};
+                tlist.insert(tlist.end(), regs.begin(), regs.end());
+                p->tl.push_back(L);
+            }
+            add_items(2, st, head, q);
+            if (!p->tl.empty() && p->tl.back().kind == 2 && p->tl.back().step == st) p->tl.back().n = run;
         }
         for (int J = Kmax - 1; J >= 0; --J) {
             std::vector<int32_t> ba, bc;
@@ -505,9 +518,10 @@ static int enqueue_tiled(dbslmm_plan* p, double isn) {
         const int32_t* pfx = act + L.n;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
         switch (L.kind) {
-        case 0: hipLaunchKernelGGL(dbslmm_tchol_diag0, g, blk, kTiledLds, st, ta, act, L.n); break;
+        case 0: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, 0, 0, act, L.n); break;
+        case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, L.step, 1, act, L.n); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
-        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
+        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, L.n, act, L.items); break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }
     }
