@@ -410,6 +410,141 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Kernel 2c: the Gram of the big blocks (m >= 512), 256 x 256 output tile per 512-thread
+// workgroup: wave w computes rows 64 (w & 3) .., columns 128 (w >> 2) .. (2 x 4 MFMA 32x32x32
+// i8 tiles, 128 accumulator registers).  Twice the operand reuse of the 128-tile kernel: the
+// 64-byte K stages (two operands x 256 rows, 80-B row stride: conflict-free ds_read_b128) cost
+// 32 KB of L2/MALL traffic per 8.4 M ops.  Double-buffered LDS, global loads two stages ahead in
+// registers.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
+// skip the MFMAs.  Missing-call blocks: exact 4-product path per 32 x 32 sub-tile.
+// ------------------------------------------------------------------------------------------
+namespace gram {
+constexpr int kHT = 256;                   // output tile edge
+constexpr int kHK = 64;                    // individuals (bytes) per K stage
+constexpr int kHRS = kHK + 16;             // LDS row stride (bytes)
+constexpr int kHOp = kHT * kHRS;           // one operand stage
+constexpr int kHLdsBytes = 2 * 2 * kHOp;   // 2 stages x (A, B) = 81,920 B
+}  // namespace gram
+
+extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
+    const int8_t* __restrict__ G, int64_t kpad,
+    const GramTile* __restrict__ tiles, int32_t n_tiles,
+    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
+    const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
+    const int32_t* __restrict__ block_flags,
+    const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    using namespace gram;
+    extern __shared__ __attribute__((aligned(16))) int8_t hlds[];
+    if (static_cast<int>(blockIdx.x) >= n_tiles) return;
+    const GramTile tile = tiles[blockIdx.x];
+    const int b = tile.block;
+    if (b < 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row0 = blk_row0[b], m = blk_m[b], ld = blk_ld[b];
+    const int64_t moff = blk_matoff[b];
+    const bool diag = tile.ti == tile.tj;
+    if (block_flags[b] & 1) {   // missing calls: 8 x 8 sub-tiles of 32, 4-product form
+        for (int q = wave; q < 64; q += 8) {
+            const int si = q >> 3, sj = q & 7;
+            if (diag && sj > si) continue;
+            const int r0 = kHT * tile.ti + 32 * si, c0 = kHT * tile.tj + 32 * sj;
+            if (r0 >= m || c0 >= m) continue;
+            gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
+                        tau, M);
+        }
+        return;
+    }
+    const int8_t* ga = G + static_cast<int64_t>(row0 + kHT * tile.ti) * kpad;
+    const int8_t* gb = G + static_cast<int64_t>(row0 + kHT * tile.tj) * kpad;
+    // staging map: 256 rows x 4 chunks of 16 B per operand; thread t moves chunks t, t + 512
+    v4i ra0[2], rb0[2], ra1[2], rb1[2];
+    auto gload = [&](v4i (&ra)[2], v4i (&rb)[2], int st) {
+        const int64_t k0 = static_cast<int64_t>(st) * kHK;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int e = q * 512 + tid, r = e >> 2, c = e & 3;
+            ra[q] = *reinterpret_cast<const v4i*>(ga + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
+            if (!diag) rb[q] = *reinterpret_cast<const v4i*>(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
+        }
+    };
+    auto lstore = [&](const v4i (&ra)[2], const v4i (&rb)[2], int buf) {
+        int8_t* A = hlds + buf * 2 * kHOp;
+        int8_t* B = A + kHOp;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int e = q * 512 + tid, r = e >> 2, c = e & 3;
+            *reinterpret_cast<v4i*>(A + r * kHRS + 16 * c) = ra[q];
+            if (!diag) *reinterpret_cast<v4i*>(B + r * kHRS + 16 * c) = rb[q];
+        }
+    };
+    const int wr = wave & 3, wc = wave >> 2;       // rows 64 wr .., columns 128 wc ..
+    const bool idle = diag && 128 * wc >= 64 * wr + 64;
+    v16i acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0};
+    const int rsub = lane & 31, ksub = 16 * (lane >> 5);
+    auto compute = [&](int buf) {
+        if (idle) return;
+        const int8_t* A = hlds + buf * 2 * kHOp;
+        const int8_t* B = diag ? A : A + kHOp;
+        const int8_t* pa = A + (64 * wr + rsub) * kHRS + ksub;
+        const int8_t* pb = B + (128 * wc + rsub) * kHRS + ksub;
+#pragma unroll
+        for (int kk = 0; kk < kHK; kk += 32) {
+            v4i av[2], bv[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = *reinterpret_cast<const v4i*>(pa + 32 * i * kHRS + kk);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const v4i*>(pb + 32 * j * kHRS + kk);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    const int nst = static_cast<int>(kpad / kHK);
+    gload(ra0, rb0, 0);
+    lstore(ra0, rb0, 0);
+    if (nst > 1) gload(ra1, rb1, 1);
+    __syncthreads();
+    for (int st = 0; st < nst; st += 2) {
+        if (st + 2 < nst) gload(ra0, rb0, st + 2);
+        compute(0);
+        if (st + 1 < nst) lstore(ra1, rb1, 1);
+        __syncthreads();
+        if (st + 1 >= nst) break;
+        if (st + 3 < nst) gload(ra1, rb1, st + 3);
+        compute(1);
+        if (st + 2 < nst) lstore(ra0, rb0, 0);
+        __syncthreads();
+    }
+    if (idle) return;
+    const double scale = tau / n_ref_d;
+#pragma unroll
+    for (int sj = 0; sj < 4; ++sj) {
+        const int lj = kHT * tile.tj + 128 * wc + 32 * sj + (lane & 31);
+        if (lj >= m) continue;
+        const double Sj = S[row0 + lj], rj = rsd[row0 + lj];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int li = kHT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (li >= m) continue;
+                const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
+                double v = scale * (c * rsd[row0 + li] * rj);
+                if (li == lj) v += 1.0 - tau;
+                M[moff + static_cast<int64_t>(li) * ld + lj] = v;
+            }
+        }
+    }
+}
+
 // one device scalar, in stream order (the solve kernels read sigma's shift from it)
 extern "C" __global__ void dbslmm_set_scalar(double* __restrict__ dst, double v) { *dst = v; }
 

@@ -39,6 +39,7 @@ constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
+constexpr int kGramHugeMinDefault = 512; // ... and the 256 x 256 one from here
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
@@ -82,8 +83,10 @@ struct dbslmm_plan {
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
     GramTile* d_tiles = nullptr;       // 32 x 32 tiles of the small blocks (dbslmm_gram_i8)
-    GramTile* d_btiles = nullptr;      // 128 x 128 tiles of the other blocks, per-XCD queues
+    GramTile* d_btiles = nullptr;      // 128 x 128 tiles of the mid blocks, per-XCD queues
     int32_t n_btiles = 0;
+    GramTile* d_htiles = nullptr;      // 256 x 256 tiles of the big blocks, per-XCD queues
+    int32_t n_htiles = 0;
     double* d_M = nullptr;
     double *d_beta_s = nullptr, *d_beta_l = nullptr;
     double* d_dshift = nullptr;        // 1/(sigma_s n), read by the solve kernels
@@ -152,6 +155,8 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                             static_cast<int>(kCholLargeLds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_big),
                             hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_region),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kRegionLds)) != hipSuccess ||
@@ -187,7 +192,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
-                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_dshift,
+                    p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_Mkeep};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -229,8 +234,10 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<GramTile> tiles;
     int64_t gram_big_min = kGramBigMinDefault;
     if (const char* env = getenv("DBSLMM_GRAM_BIG_MIN")) gram_big_min = std::max<int64_t>(1, atoll(env));
-    std::vector<std::vector<GramTile>> xq(kXcd);
-    std::vector<double> xload(kXcd, 0.0);
+    int64_t gram_huge_min = kGramHugeMinDefault;
+    if (const char* env = getenv("DBSLMM_GRAM_HUGE_MIN")) gram_huge_min = std::max<int64_t>(1, atoll(env));
+    std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd);
+    std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0);
     int64_t moff = 0;
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
@@ -281,7 +288,15 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             slot_out.push_back(INT32_MIN);
             z.push_back(0.0);
         }
-        if (m >= gram_big_min) {   // 128 x 128 tiles, the block's queue on the least-loaded XCD
+        if (m >= gram_huge_min) {   // 256 x 256 tiles; each tile row on the least-loaded XCD
+            const int T = static_cast<int>((m + gram::kHT - 1) / gram::kHT);
+            for (int ti = 0; ti < T; ++ti) {
+                const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
+                for (int tj = 0; tj <= ti; ++tj) hq[x].push_back({nb, ti, tj, 0});
+                hload[x] += ti + 1;
+            }
+            ops_exec += 2.0 * p->kpad * gram::kHT * gram::kHT * (T * (T + 1) / 2);
+        } else if (m >= gram_big_min) {   // 128 x 128 tiles, the block's queue on the least-loaded XCD
             const int T = static_cast<int>((m + gram::kGT - 1) / gram::kGT);
             const int x = static_cast<int>(std::min_element(xload.begin(), xload.end()) - xload.begin());
             for (int ti = 0; ti < T; ++ti)
@@ -309,6 +324,15 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         for (int x = 0; x < kXcd; ++x)
             for (size_t i = 0; i < xq[x].size(); ++i) btiles[i * kXcd + x] = xq[x][i];
         p->n_btiles = static_cast<int32_t>(btiles.size());
+    }
+    std::vector<GramTile> htiles;
+    {
+        size_t qmax = 0;
+        for (const auto& q : hq) qmax = std::max(qmax, q.size());
+        htiles.assign(qmax * kXcd, GramTile{-1, 0, 0, 0});
+        for (int x = 0; x < kXcd; ++x)
+            for (size_t i = 0; i < hq[x].size(); ++i) htiles[i * kXcd + x] = hq[x][i];
+        p->n_htiles = static_cast<int32_t>(htiles.size());
     }
     p->M_elems = moff;
     p->h_ld = ldv;
@@ -421,7 +445,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[4] = ops_exec;
     p->wl[5] = chol_flops_large;
     p->wl[6] = p->n_nonempty;
-    p->wl[7] = p->n_tiles + p->n_btiles;
+    p->wl[7] = p->n_tiles + p->n_btiles + p->n_htiles;
     p->wl[8] = chol_flops_small;
     p->wl[9] = p->n_large;
     p->wl[10] = chol_flops_tiled;
@@ -439,8 +463,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
     if ((e = hipMemset(p->d_bed, 0, pr->bed_len + 16)) != hipSuccess) return fail("hipMemset bed");
     if ((e = hipMemcpy(p->d_bed, pr->bed, pr->bed_len, hipMemcpyHostToDevice)) != hipSuccess) return fail("upload bed");
-    // + kGT spare rows: a 128-row Gram tile may read past the last slot (results discarded)
-    const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kGT) * p->kpad;
+    // + kHT spare rows: a 256-row Gram tile may read past the last slot (results discarded)
+    const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kHT) * p->kpad;
     if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
     if ((e = hipMemset(p->d_G, 0, g_bytes)) != hipSuccess) return fail("hipMemset G");
     if ((e = dev_upload(&p->d_slot_pos, slot_pos)) != hipSuccess) return fail("upload slots");
@@ -456,6 +480,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_order, order)) != hipSuccess) return fail("upload order");
     if ((e = dev_upload(&p->d_tiles, tiles)) != hipSuccess) return fail("upload tiles");
     if ((e = dev_upload(&p->d_btiles, btiles)) != hipSuccess) return fail("upload tiles");
+    if ((e = dev_upload(&p->d_htiles, htiles)) != hipSuccess) return fail("upload tiles");
     if ((e = dev_upload(&p->d_tlist, tlist)) != hipSuccess) return fail("upload tiled lists");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -565,6 +590,14 @@ static int run_impl(dbslmm_plan* p, bool front, int keep) {
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
                            static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (front && p->n_htiles > 0) {
+        hipLaunchKernelGGL(dbslmm_gram_huge, dim3(p->n_htiles), dim3(512), gram::kHLdsBytes, s, p->d_G,
+                           p->kpad, p->d_htiles, p->n_htiles, p->d_row0, p->d_m, p->d_ld,
+                           p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
+                           static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
+                           p->tau, p->d_M);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_btiles > 0) {

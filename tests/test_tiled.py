@@ -119,16 +119,19 @@ def test_tiled_plan_rerun_bit_identical(monkeypatch):
 @pytest.mark.parametrize("miss", [0.0, 0.01])
 @pytest.mark.parametrize("n_ref", [200, 333])
 def test_gram_kernels_bit_identical(monkeypatch, miss, n_ref):
-    """128x128 LDS-staged Gram (m >= DBSLMM_GRAM_BIG_MIN) and the per-wave 32x32 Gram compute
-    the same exact integers and the same fp64 epilogue: beta must agree bit for bit."""
+    """The 256x256 (m >= DBSLMM_GRAM_HUGE_MIN), 128x128 (m >= DBSLMM_GRAM_BIG_MIN) and per-wave
+    32x32 Gram kernels compute the same exact integers and the same fp64 epilogue: beta must
+    agree bit for bit whichever kernel handles every block."""
     from dbslmm_amd import DBSLMMFIT, synth
     p = synth.simulate(6000, n_ref, pop="EUR", chroms=[1], seed=7, miss_rate=miss, large_every=3)
     prob = synth.make_problem(p)
-    monkeypatch.setenv("DBSLMM_GRAM_BIG_MIN", "1")
-    big = DBSLMMFIT(0).est(prob)
-    monkeypatch.setenv("DBSLMM_GRAM_BIG_MIN", str(10 ** 9))
-    small = DBSLMMFIT(0).est(prob)
-    for x, y in zip(big, small):
-        np.testing.assert_array_equal(x, y)
+    out = []
+    for big, huge in ((1, 1), (1, 10 ** 9), (10 ** 9, 10 ** 9)):
+        monkeypatch.setenv("DBSLMM_GRAM_BIG_MIN", str(big))
+        monkeypatch.setenv("DBSLMM_GRAM_HUGE_MIN", str(huge))
+        out.append(DBSLMMFIT(0).est(prob))
+    for other in out[1:]:
+        for x, y in zip(out[0], other):
+            np.testing.assert_array_equal(x, y)
     ref, _ = _oracle(prob)
-    assert normwise(np.concatenate(big[:2]), ref) < 1e-10
+    assert normwise(np.concatenate(out[0][:2]), ref) < 1e-10
