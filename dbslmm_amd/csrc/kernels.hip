@@ -411,20 +411,27 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 2c: the Gram of the big blocks (m >= 512), 256 x 256 output tile per 512-thread
+// Kernel 2c: the Gram of the big blocks (m >= 384), 256 x 256 output tile per 512-thread
 // workgroup: wave w computes rows 64 (w & 3) .., columns 128 (w >> 2) .. (2 x 4 MFMA 32x32x32
-// i8 tiles, 128 accumulator registers).  Twice the operand reuse of the 128-tile kernel: the
-// 64-byte K stages (two operands x 256 rows, 80-B row stride: conflict-free ds_read_b128) cost
-// 32 KB of L2/MALL traffic per 8.4 M ops.  Double-buffered LDS, global loads two stages ahead in
-// registers.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
-// skip the MFMAs.  Missing-call blocks: exact 4-product path per 32 x 32 sub-tile.
+// i8 tiles, 128 accumulator registers).  K runs in 64-byte stages through a 3-slot LDS ring
+// filled by LDS-DMA (global_load_lds_dwordx4: no staging registers), two stages in flight:
+// per stage each wave issues its DMA pieces for stage st + 2, waits with a counted vmcnt for
+// stage st, raw s_barrier (a __syncthreads() would drain the DMAs in flight), 16 MFMAs, barrier.
+// The LDS image is lane-linear per DMA piece (1 KiB = 16 rows x 64 B, unpadded), swizzled through
+// the SOURCE address: position p of row r holds K chunk p ^ ((r >> 2) & 3), which puts the 16
+// rows of every ds_read_b128 lane group on 16 distinct bank groups.  Diagonal tiles stage one
+// operand; waves whose 64 x 128 piece is strictly upper skip the MFMAs.  Missing-call blocks:
+// exact 4-product path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
 namespace gram {
 constexpr int kHT = 256;                   // output tile edge
-constexpr int kHK = 64;                    // individuals (bytes) per K stage
-constexpr int kHRS = kHK + 16;             // LDS row stride (bytes)
-constexpr int kHOp = kHT * kHRS;           // one operand stage
-constexpr int kHLdsBytes = 2 * 2 * kHOp;   // 2 stages x (A, B) = 81,920 B
+constexpr int kHK = 64;                    // individuals (bytes) per K stage = one row chunk set
+constexpr int kHOp = kHT * kHK;            // one operand stage (16 KiB)
+constexpr int kHSlots = 3;                 // LDS ring depth
+constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 96 KiB
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+__device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r >> 2) & 3)); }
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
@@ -458,25 +465,20 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     }
     const int8_t* ga = G + static_cast<int64_t>(row0 + kHT * tile.ti) * kpad;
     const int8_t* gb = G + static_cast<int64_t>(row0 + kHT * tile.tj) * kpad;
-    // staging map: 256 rows x 4 chunks of 16 B per operand; thread t moves chunks t, t + 512
-    v4i ra0[2], rb0[2], ra1[2], rb1[2];
-    auto gload = [&](v4i (&ra)[2], v4i (&rb)[2], int st) {
+    // DMA pieces: wave w fills rows 32 w .. 32 w + 31 of each operand (two 16-row pieces)
+    const int prow = lane >> 2, ppos = lane & 3;
+    auto issue = [&](int st) {
+        int8_t* slot = hlds + (st % kHSlots) * 2 * kHOp;
         const int64_t k0 = static_cast<int64_t>(st) * kHK;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int e = q * 512 + tid, r = e >> 2, c = e & 3;
-            ra[q] = *reinterpret_cast<const v4i*>(ga + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
-            if (!diag) rb[q] = *reinterpret_cast<const v4i*>(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
-        }
-    };
-    auto lstore = [&](const v4i (&ra)[2], const v4i (&rb)[2], int buf) {
-        int8_t* A = hlds + buf * 2 * kHOp;
-        int8_t* B = A + kHOp;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int e = q * 512 + tid, r = e >> 2, c = e & 3;
-            *reinterpret_cast<v4i*>(A + r * kHRS + 16 * c) = ra[q];
-            if (!diag) *reinterpret_cast<v4i*>(B + r * kHRS + 16 * c) = rb[q];
+        for (int j = 0; j < 2; ++j) {
+            const int r = 32 * wave + 16 * j + prow;
+            const int c = ppos ^ ((r >> 2) & 3);
+            __builtin_amdgcn_global_load_lds((gptr_t)(ga + static_cast<int64_t>(r) * kpad + k0 + 16 * c),
+                                             (lptr_t)(slot + (32 * wave + 16 * j) * kHK), 16, 0, 0);
+            if (!diag)
+                __builtin_amdgcn_global_load_lds((gptr_t)(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c),
+                                                 (lptr_t)(slot + kHOp + (32 * wave + 16 * j) * kHK), 16, 0, 0);
         }
     };
     const int wr = wave & 3, wc = wave >> 2;       // rows 64 wr .., columns 128 wc ..
@@ -486,20 +488,21 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0};
-    const int rsub = lane & 31, ksub = 16 * (lane >> 5);
-    auto compute = [&](int buf) {
+    const int rsub = lane & 31, csub = lane >> 5;   // row in a 32-row group, 16-B half of a k-step
+    auto compute = [&](int st) {
         if (idle) return;
-        const int8_t* A = hlds + buf * 2 * kHOp;
+        const int8_t* A = hlds + (st % kHSlots) * 2 * kHOp;
         const int8_t* B = diag ? A : A + kHOp;
-        const int8_t* pa = A + (64 * wr + rsub) * kHRS + ksub;
-        const int8_t* pb = B + (128 * wc + rsub) * kHRS + ksub;
 #pragma unroll
-        for (int kk = 0; kk < kHK; kk += 32) {
+        for (int kk = 0; kk < kHK / 32; ++kk) {
+            const int c = 2 * kk + csub;
             v4i av[2], bv[4];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) av[i] = *reinterpret_cast<const v4i*>(pa + 32 * i * kHRS + kk);
+            for (int i = 0; i < 2; ++i)
+                av[i] = *reinterpret_cast<const v4i*>(A + swz(64 * wr + 32 * i + rsub, c));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const v4i*>(pb + 32 * j * kHRS + kk);
+            for (int j = 0; j < 4; ++j)
+                bv[j] = *reinterpret_cast<const v4i*>(B + swz(128 * wc + 32 * j + rsub, c));
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -508,20 +511,24 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         }
     };
     const int nst = static_cast<int>(kpad / kHK);
-    gload(ra0, rb0, 0);
-    lstore(ra0, rb0, 0);
-    if (nst > 1) gload(ra1, rb1, 1);
-    __syncthreads();
-    for (int st = 0; st < nst; st += 2) {
-        if (st + 2 < nst) gload(ra0, rb0, st + 2);
-        compute(0);
-        if (st + 1 < nst) lstore(ra1, rb1, 1);
-        __syncthreads();
-        if (st + 1 >= nst) break;
-        if (st + 3 < nst) gload(ra1, rb1, st + 3);
-        compute(1);
-        if (st + 2 < nst) lstore(ra0, rb0, 0);
-        __syncthreads();
+    issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+        if (st + 2 < nst) {
+            issue(st + 2);
+            // this wave's DMAs for stages st+1 and st+2 may stay in flight
+            if (diag) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if (st + 1 < nst) {
+            if (diag) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();               // stage st is in LDS (every wave waited)
+        compute(st);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();               // slot st % 3 may be refilled
     }
     if (idle) return;
     const double scale = tau / n_ref_d;

@@ -39,7 +39,7 @@ constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
-constexpr int kGramHugeMinDefault = 512; // ... and the 256 x 256 one from here
+constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
