@@ -234,7 +234,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<GramTile> tiles;
     int64_t gram_big_min = kGramBigMinDefault;
     if (const char* env = getenv("DBSLMM_GRAM_BIG_MIN")) gram_big_min = std::max<int64_t>(1, atoll(env));
-    int64_t gram_huge_min = kGramHugeMinDefault;
+    // the 256-tile kernel pays once its K loop outweighs its 512 KB fp64 epilogue per tile
+    int64_t gram_huge_min = p->kpad >= 4096 ? kGramHugeMinDefault : 2 * kGramHugeMinDefault;
     if (const char* env = getenv("DBSLMM_GRAM_HUGE_MIN")) gram_huge_min = std::max<int64_t>(1, atoll(env));
     std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd);
     std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0);
