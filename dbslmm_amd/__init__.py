@@ -22,7 +22,7 @@ from . import _lib
 from ._lib import (WORKLOAD_LEN, BLOCK_EMPTY, BLOCK_MONOMORPHIC, BLOCK_NOT_PD, BLOCK_OK, KERNEL_NAMES,
                    DbslmmError)
 
-__all__ = ["Context", "Plan", "DBSLMMFIT", "BlockProblem", "bed_maf", "read_snp_std",
+__all__ = ["Context", "Plan", "DBSLMMFIT", "BlockProblem", "bed_maf", "read_snp_std", "valid_blocks",
            "DbslmmError", "BLOCK_OK", "BLOCK_EMPTY", "BLOCK_NOT_PD", "BLOCK_MONOMORPHIC",
            "KERNEL_NAMES"]
 
@@ -209,3 +209,19 @@ def read_snp_std(ctx: Context, bed: np.ndarray, n_ref: int, rows) -> tuple[np.nd
     ctx.check(ctx.lib.dbslmm_read_snp_std(ctx.h, _ptr(bed), bed.size, n_ref, _ptr(rows), len(rows),
                                           _ptr(out), _ptr(maf)), "read_snp_std")
     return out.reshape(len(rows), n_ref).T, maf
+
+
+def valid_blocks(ctx: Context, bed: np.ndarray, n_ref: int, ptr, pos, z1, z2):
+    """External-validation terms of the `valid` tool (scr/validate.cpp:221-257) on the GPU:
+    per block nume = z1.z2 and deno = z1^T (X^T X / n_ref) z1."""
+    bed = np.ascontiguousarray(bed, dtype=np.uint8)
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    pos = np.ascontiguousarray(pos, dtype=np.int32)
+    z1 = np.ascontiguousarray(z1, dtype=np.float64)
+    z2 = np.ascontiguousarray(z2, dtype=np.float64)
+    nb = len(ptr) - 1
+    nume = np.zeros(nb)
+    deno = np.zeros(nb)
+    ctx.check(ctx.lib.dbslmm_valid_blocks(ctx.h, _ptr(bed), bed.size, n_ref, nb, _ptr(ptr), _ptr(pos),
+                                          _ptr(z1), _ptr(z2), _ptr(nume), _ptr(deno)), "valid_blocks")
+    return nume, deno

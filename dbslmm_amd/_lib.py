@@ -17,7 +17,7 @@ EXPORTS = (
     "dbslmm_est", "dbslmm_plan_create", "dbslmm_plan_run", "dbslmm_plan_sync",
     "dbslmm_plan_download", "dbslmm_plan_set_sigma", "dbslmm_plan_destroy", "dbslmm_plan_run_multi",
     "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
-    "dbslmm_bed_maf", "dbslmm_read_snp_std",
+    "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks",
 )
 
 ABI_VERSION = 2
@@ -75,6 +75,7 @@ def load(path: str | None = None):
     L.dbslmm_plan_workload.argtypes = [V, V]
     L.dbslmm_bed_maf.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int64, V]
     L.dbslmm_read_snp_std.argtypes = [V, V, C.c_int64, C.c_int32, V, C.c_int32, V, V]
+    L.dbslmm_valid_blocks.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int32, V, V, V, V, V, V]
     if L.dbslmm_abi_version() != ABI_VERSION:
         raise DbslmmError("ABI version mismatch")
     _lib = L

@@ -30,11 +30,13 @@
 #include <vector>
 
 #include "../../../include/dbslmm_hip.h"
+#include "host_io.hpp"
 
 using std::string;
 using std::vector;
 
 namespace {
+using namespace dbslmm_host;
 
 struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised here)
     string s, l, r, b, eff, test_indicator_file, dat_str;
@@ -48,7 +50,6 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
 };
 
 struct Allele { int64_t pos; string a1, a2; double maf; };                 // ALLELE
-struct Block { string chr; long start, end; };                              // BLOCK
 struct Summ { string snp; long ps; string a1, a2; double maf, z; };        // SUMM (P unused)
 struct Info { string snp; long ps; int64_t pos; int block; string a1; double maf, z; };  // INFO
 
@@ -114,58 +115,6 @@ void assign(int argc, char** argv, Param& p) {
         else if (!strcmp(a, "--dry-run")) p.dry_run = true;
     }
 }
-
-vector<string> split(const string& line, char sep) {
-    vector<string> out;
-    string e;
-    std::stringstream ss(line);
-    while (std::getline(ss, e, sep)) out.push_back(e);
-    return out;
-}
-
-// IO::getRow (scr/dtpr.cpp:71-80)
-int get_row(const string& path) {
-    std::ifstream f(path);
-    string line;
-    int n = 0;
-    while (std::getline(f, line)) ++n;
-    return n;
-}
-
-// IO::readBlock (scr/dtpr.cpp:47-68)
-vector<Block> read_block(const string& path) {
-    vector<Block> out;
-    std::ifstream f(path);
-    string line;
-    while (std::getline(f, line)) {
-        auto t = split(line, '\t');
-        if (t.size() < 3) continue;
-        out.push_back({t[0], atol(t[1].c_str()), atol(t[2].c_str())});
-    }
-    return out;
-}
-
-// mmap'd .bed image
-struct Mapped {
-    const uint8_t* p = nullptr;
-    size_t n = 0;
-    int fd = -1;
-    bool open(const string& path) {
-        fd = ::open(path.c_str(), O_RDONLY);
-        if (fd < 0) return false;
-        struct stat st;
-        if (fstat(fd, &st) != 0) return false;
-        n = static_cast<size_t>(st.st_size);
-        void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
-        if (m == MAP_FAILED) return false;
-        p = static_cast<const uint8_t*>(m);
-        return true;
-    }
-    ~Mapped() {
-        if (p) munmap(const_cast<uint8_t*>(p), n);
-        if (fd >= 0) close(fd);
-    }
-};
 
 // IO::readBim (scr/dtpr.cpp:83-123): maf from the GPU MAF pass when constr.
 bool read_bim(const string& ref, const vector<double>& maf, std::unordered_map<string, Allele>& bim,

@@ -552,6 +552,63 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// `valid` (scr/validate.cpp:221-257): deno_b = z1^T (X^T X / n_ref) z1 = |X z1|^2 / n_ref per
+// block, X the nomalizeVec-standardised reference genotypes (missing calls at the mean -> 0).
+// Computed as a weighted row sum straight from the packed .bed (no Gram): thread = one packed
+// dword column (16 individuals), looping over the block's SNPs; y = X z1 in fp64 registers; the
+// workgroup reduces sum(y^2) into partial[b][blockIdx.x]; dbslmm_valid_reduce sums the
+// partials of each block in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void dbslmm_valid_partial(
+    const uint8_t* __restrict__ bed, int32_t n_ref, int64_t bytes_per_snp,
+    const int64_t* __restrict__ ptr, const int32_t* __restrict__ pos,
+    const double* __restrict__ z1, const double* __restrict__ mu, const double* __restrict__ rsd,
+    double* __restrict__ partial, int32_t n_chunks) {
+    __shared__ double red[256 / kWave];
+    const int b = blockIdx.y;
+    const int64_t w = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t n_words = (n_ref + 15) / 16;
+    double y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = 0.0;
+    if (w < n_words) {
+        const int nv = static_cast<int>(min<int64_t>(16, n_ref - 16 * w));
+        for (int64_t j = ptr[b]; j < ptr[b + 1]; ++j) {
+            const uint32_t word = load_u32_any(bed, 3 + static_cast<int64_t>(pos[j]) * bytes_per_snp + 4 * w);
+            const double m0 = mu[j], wt = z1[j] * rsd[j];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t code = (word >> (2 * i)) & 3u;
+                // 00 -> 2, 10 -> 1, 11 -> 0, 01 -> missing (the mean: contributes 0)
+                const double g = code == 0 ? 2.0 : (code == 2 ? 1.0 : (code == 3 ? 0.0 : m0));
+                if (i < nv) y[i] += (g - m0) * wt;
+            }
+        }
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += y[i] * y[i];
+    for (int off = kWave / 2; off > 0; off >>= 1) s += __shfl_down(s, off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int q = 0; q < 256 / kWave; ++q) t += red[q];
+        partial[static_cast<int64_t>(b) * n_chunks + blockIdx.x] = t;
+    }
+}
+
+extern "C" __global__ void dbslmm_valid_reduce(const double* __restrict__ partial, int32_t n_chunks,
+                                               int32_t num_block, double n_ref_d,
+                                               double* __restrict__ deno) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= num_block) return;
+    double t = 0.0;
+    for (int c = 0; c < n_chunks; ++c) t += partial[static_cast<int64_t>(b) * n_chunks + c];
+    deno[b] = t / n_ref_d;
+}
+
 // one device scalar, in stream order (the solve kernels read sigma's shift from it)
 extern "C" __global__ void dbslmm_set_scalar(double* __restrict__ dst, double v) { *dst = v; }
 

@@ -863,6 +863,73 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
     return rc;
 }
 
+// External-validation terms of the `valid` tool (scr/validate.cpp:221-257).
+int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
+                        int32_t num_block, const int64_t* ptr, const int32_t* pos,
+                        const double* z1, const double* z2, double* nume, double* deno) {
+    if (!ctx) return DBSLMM_E_ARG;
+    ARG_CHECK(ctx, bed && ptr && nume && deno && n_ref > 1 && num_block >= 0, "bad arguments");
+    const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
+    const int64_t n_rows = ptr[num_block];
+    ARG_CHECK(ctx, n_rows >= 0 && n_rows < INT32_MAX && (n_rows == 0 || (pos && z1 && z2)), "bad CSR");
+    for (int b = 0; b < num_block; ++b) ARG_CHECK(ctx, ptr[b + 1] >= ptr[b], "CSR offsets not monotone");
+    for (int64_t j = 0; j < n_rows; ++j)
+        ARG_CHECK(ctx, pos[j] >= 0 && 3 + (pos[j] + 1) * bps <= bed_len, "row out of range");
+    // nume = z1 . z2 per block (host: O(m), in the reference's accumulation order)
+    for (int b = 0; b < num_block; ++b) {
+        double t = 0.0;
+        for (int64_t j = ptr[b]; j < ptr[b + 1]; ++j) t += z1[j] * z2[j];
+        nume[b] = t;
+    }
+    if (num_block == 0) return DBSLMM_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const int64_t n_words = (n_ref + 15) / 16;
+    const int32_t n_chunks = static_cast<int32_t>((n_words + 255) / 256);
+    uint8_t* d_bed = nullptr;
+    int32_t* d_pos = nullptr;
+    int64_t* d_ptr = nullptr;
+    double *d_z1 = nullptr, *d_mu = nullptr, *d_rsd = nullptr, *d_part = nullptr, *d_deno = nullptr;
+    std::vector<int32_t> hp(pos, pos + n_rows);
+    std::vector<int64_t> hptr(ptr, ptr + num_block + 1);
+    std::vector<double> hz(z1, z1 + n_rows);
+    const size_t nr = std::max<int64_t>(1, n_rows);
+    int rc = DBSLMM_OK;
+    do {
+        hipError_t e;
+        if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
+            (e = hipMemset(d_bed, 0, bed_len + 16)) != hipSuccess ||
+            (e = hipMemcpy(d_bed, bed, bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = dev_upload(&d_pos, hp)) != hipSuccess || (e = dev_upload(&d_ptr, hptr)) != hipSuccess ||
+            (e = dev_upload(&d_z1, hz)) != hipSuccess ||
+            (e = hipMalloc(&d_mu, nr * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_rsd, nr * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_part, static_cast<size_t>(num_block) * n_chunks * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_deno, num_block * sizeof(double))) != hipSuccess) {
+            ctx->err = std::string("valid alloc/upload: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+            break;
+        }
+        if (n_rows > 0)
+            hipLaunchKernelGGL(dbslmm_unpack_stats, dim3(static_cast<unsigned>((n_rows + 3) / 4)), dim3(256), 0,
+                               ctx->stream, d_bed, n_ref, bps, d_pos, d_pos, static_cast<int32_t>(n_rows),
+                               nullptr, round_up(n_ref, 64), nullptr, d_mu, d_rsd, nullptr, nullptr);
+        hipLaunchKernelGGL(dbslmm_valid_partial, dim3(n_chunks, num_block), dim3(256), 0, ctx->stream,
+                           d_bed, n_ref, bps, d_ptr, d_pos, d_z1, d_mu, d_rsd, d_part, n_chunks);
+        hipLaunchKernelGGL(dbslmm_valid_reduce, dim3((num_block + 255) / 256), dim3(256), 0, ctx->stream,
+                           d_part, n_chunks, num_block, static_cast<double>(n_ref), d_deno);
+        if ((e = hipGetLastError()) != hipSuccess ||
+            (e = hipStreamSynchronize(ctx->stream)) != hipSuccess ||
+            (e = hipMemcpy(deno, d_deno, num_block * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) {
+            ctx->err = std::string("valid run: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+        }
+    } while (0);
+    void* bufs[] = {d_bed, d_pos, d_ptr, d_z1, d_mu, d_rsd, d_part, d_deno};
+    for (void* q : bufs)
+        if (q) (void)hipFree(q);
+    return rc;
+}
+
 #ifdef DBSLMM_STAMPS
 // diagnostic build only (libdbslmm_hip_stamps.so): read + clear the per-phase tick counters
 int dbslmm_debug_stamps(double* out8) {

@@ -150,6 +150,16 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
 int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
                         const int32_t* pos, int32_t n_rows, double* out, double* maf);
 
+/* External-validation R^2 terms: the per-block loop of the `valid` tool (replaces the
+ * Armadillo products of scr/validate.cpp:221-257).  Block b owns .bed rows pos[ptr[b]..ptr[b+1])
+ * with weights z1 (DBSLMM beta) and z2 (external z):
+ *   nume[b] = z1 . z2,   deno[b] = z1^T (X^T X / n_ref) z1 = |X z1|^2 / n_ref
+ * X = the nomalizeVec-standardised reference genotypes (N-1 sd, missing calls at the mean);
+ * a monomorphic SNP gives NaN, as the reference's 0/0 column.  Synchronous; host buffers. */
+int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
+                        int32_t num_block, const int64_t* ptr, const int32_t* pos,
+                        const double* z1, const double* z2, double* nume, double* deno);
+
 #ifdef __cplusplus
 }
 #endif

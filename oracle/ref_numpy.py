@@ -363,3 +363,108 @@ def format_eff(res: EstResult) -> list[str]:
                 continue
             lines.append(f"{e['snp']} {e['a1']} {format_g(b)} {format_g(noscl)} {flag}")
     return lines
+
+
+# ------------------------------------------------------------------------ `valid`
+def read_bim_b(ref: str, n_ref: int, constr: bool):
+    """IO::readBim, ALLELEB overload (dtpr.cpp:125-166): dict snp -> (pos, ps, a1, a2, maf);
+    MAF pass over the .bed when constr; std::map::insert keeps the first of duplicate ids."""
+    n_snp = get_row(ref + ".bim")
+    maf = np.zeros(n_snp)
+    if constr:
+        bed = open(ref + ".bed", "rb").read()
+        idv = np.ones(n_ref, dtype=np.int32)
+        for i in range(n_snp):
+            _, maf[i] = read_snp_im(bed, i, idv)
+    bim = {}
+    with open(ref + ".bim") as f:
+        for count, line in enumerate(f):
+            t = line.rstrip("\n").split("\t")
+            if t[1] not in bim:
+                bim[t[1]] = (count, int(_atof(t[3])), t[4], t[5], maf[count])
+    return bim
+
+
+def read_dbslmm(path: str):
+    """IO::readDBSLMM (dtpr.cpp:223-245): space separated; (snp, a1, z = 3rd column = beta)."""
+    out = []
+    with open(path) as f:
+        for line in f:
+            t = line.rstrip("\n").split(" ")
+            out.append((t[0], t[1], _atof(t[2])))
+    return out
+
+
+def read_ext(path: str):
+    """IO::readExt (dtpr.cpp:248-268): space separated snp a1 maf z; map keyed by snp, first kept."""
+    out = {}
+    with open(path) as f:
+        for line in f:
+            t = line.rstrip("\n").split(" ")
+            if t[0] not in out:
+                out[t[0]] = (t[0], t[1], _atof(t[2]), _atof(t[3]))
+    return out
+
+
+def match_summ(dbslmm, ext):
+    """SNPPROC::matchSumm (dtpr.cpp:411-433): DBSLMM rows in order that the external file has;
+    z2 sign-flipped when the A1 alleles differ.  -> [(snp, a1, maf_ext, z1, z2)]"""
+    out = []
+    for snp, a1, z in dbslmm:
+        if snp in ext:
+            e = ext[snp]
+            out.append((e[0], a1, e[2], z, e[3] if e[1] == a1 else -e[3]))
+    return out
+
+
+def match_all(summc, bim, maf_max):
+    """SNPPROC::matchAll (dtpr.cpp:436-455): A1 equal to the bim A1 and |maf_ref - maf_ext| <
+    mafMax; sorted by bp (std::sort).  -> [(snp, z1, z2, pos, ps)]"""
+    out = []
+    for snp, a1, maf, z1, z2 in summc:
+        if snp in bim:
+            pos, ps, ba1, _, bmaf = bim[snp]
+            if ba1 == a1 and abs(bmaf - maf) < maf_max:
+                out.append((snp, z1, z2, pos, ps))
+    out.sort(key=lambda x: x[4])
+    return out
+
+
+def valid_blocks(bed, n_ref: int, summp, blocks):
+    """VALID::BatchRun per-block loop (validate.cpp:221-257): sequential block scan (stalls like
+    addBlock), standardised reference genotypes, SIGMA = X^T X / n_ref, nume = z1.z2,
+    deno = z1^T SIGMA z1.  -> (nume[num_block], deno[num_block], per-block row lists)"""
+    nb = len(blocks)
+    nume, deno = np.zeros(nb), np.zeros(nb)
+    rows = []
+    count = 0
+    for b, (_, start, end) in enumerate(blocks):
+        idx = []
+        for j in range(count, len(summp)):
+            if start <= summp[j][4] < end:
+                idx.append(j)
+                count += 1
+            else:
+                break
+        rows.append(idx)
+        if not idx:
+            continue
+        z1 = np.array([summp[j][1] for j in idx])
+        z2 = np.array([summp[j][2] for j in idx])
+        X = read_block_matrix(bed, [summp[j][3] for j in idx], n_ref)
+        sigma = X.T @ X / n_ref
+        nume[b] = z1 @ z2
+        deno[b] = z1 @ sigma @ z1
+    return nume, deno, rows
+
+
+def valid(d_path, s_path, ref, maf_max, block_path):
+    """The `valid` tool end to end (validate.cpp:130-262) -> lines of <r2>.txt."""
+    n_ref = get_row(ref + ".fam")
+    summc = match_summ(read_dbslmm(d_path), read_ext(s_path))
+    bim = read_bim_b(ref, n_ref, abs(maf_max - 1.0) >= 1e-10)
+    summp = match_all(summc, bim, maf_max)
+    blocks = read_block(block_path)
+    bed = open(ref + ".bed", "rb").read()
+    nume, deno, _ = valid_blocks(bed, n_ref, summp, blocks)
+    return [f"{format_g(a)} {format_g(b)}" for a, b in zip(nume, deno)], nume, deno
