@@ -164,6 +164,24 @@ class Plan:
                        "plan_download")
         return bs, bl, st
 
+    def variance(self, test_bed: np.ndarray, indicator, s_pos, l_pos=None) -> np.ndarray:
+        """Test-set variance diags (the variance.txt matrix of DBSLMMFIT::est,
+        scr/dbslmmfit.cpp:116,242) of the last run: n_test x num_block.  s_pos / l_pos = each
+        small / large SNP's row in the test .bed (calcBlock's test_info_*_block[i].pos)."""
+        tb = np.ascontiguousarray(test_bed, dtype=np.uint8)
+        ind = np.ascontiguousarray(indicator, dtype=np.int32)
+        sp = np.ascontiguousarray(s_pos, dtype=np.int32)
+        lp = None if l_pos is None else np.ascontiguousarray(l_pos, dtype=np.int32)
+        if sp.size != self.prob.n_s or (self.prob.n_l and (lp is None or lp.size != self.prob.n_l)):
+            raise ValueError("test s_pos / l_pos must align with the plan's small / large SNPs")
+        n_test = int((ind != 0).sum())
+        out = np.zeros(n_test * self.prob.num_block)
+        nt = np.zeros(1, dtype=np.int32)
+        tp = _lib.TestPanel(_ptr(tb), tb.size, ind.size, _ptr(ind), _ptr(sp), _ptr(lp))
+        self.ctx.check(self.ctx.lib.dbslmm_plan_variance(self.h, C.byref(tp), _ptr(out), _ptr(nt)),
+                       "plan_variance")
+        return out.reshape(self.prob.num_block, n_test).T
+
     def close(self):
         if self.h:
             self.ctx.lib.dbslmm_plan_destroy(self.h)

@@ -17,10 +17,10 @@ EXPORTS = (
     "dbslmm_est", "dbslmm_plan_create", "dbslmm_plan_run", "dbslmm_plan_sync",
     "dbslmm_plan_download", "dbslmm_plan_set_sigma", "dbslmm_plan_destroy", "dbslmm_plan_run_multi",
     "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
-    "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks",
+    "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
 )
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol")
@@ -34,6 +34,13 @@ class Problem(C.Structure):
         ("sigma_s", C.c_double), ("tau", C.c_double), ("num_block", C.c_int32),
         ("s_ptr", C.c_void_p), ("s_pos", C.c_void_p), ("z_s", C.c_void_p),
         ("l_ptr", C.c_void_p), ("l_pos", C.c_void_p), ("z_l", C.c_void_p),
+    ]
+
+
+class TestPanel(C.Structure):
+    _fields_ = [
+        ("bed", C.c_void_p), ("bed_len", C.c_int64), ("n_total", C.c_int32),
+        ("indicator", C.c_void_p), ("s_pos", C.c_void_p), ("l_pos", C.c_void_p),
     ]
 
 
@@ -76,6 +83,7 @@ def load(path: str | None = None):
     L.dbslmm_bed_maf.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int64, V]
     L.dbslmm_read_snp_std.argtypes = [V, V, C.c_int64, C.c_int32, V, C.c_int32, V, V]
     L.dbslmm_valid_blocks.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int32, V, V, V, V, V, V]
+    L.dbslmm_plan_variance.argtypes = [V, P(TestPanel), V, V]
     if L.dbslmm_abi_version() != ABI_VERSION:
         raise DbslmmError("ABI version mismatch")
     _lib = L

@@ -119,10 +119,10 @@ __device__ __forceinline__ void report_status(const BlockArgs& a, int b, int row
 // Packed bordered lower triangle: element (r, k <= r) at r(r+1)/2 + k, rows 0..m (row m = z).
 __device__ __forceinline__ int tri(int r) { return r * (r + 1) / 2; }
 
-__device__ void small_block(const BlockArgs& a, const double* __restrict__ M, int b, double* L,
+__device__ void small_block(const BlockArgs& a, double* __restrict__ M, int b, double* L,
                             double* rdg, int lane) {
     const int row0 = a.blk_row0[b], m = a.blk_m[b], ms = a.blk_ms[b], ld = a.blk_ld[b];
-    const double* A = M + a.blk_matoff[b];
+    double* A = M + a.blk_matoff[b];
     for (int r = 0; r < m; ++r) {
         if (lane <= r) {
             double v = A[static_cast<int64_t>(r) * ld + lane];
@@ -161,6 +161,10 @@ __device__ void small_block(const BlockArgs& a, const double* __restrict__ M, in
         if (lane == j) { L[my + j] = p * rs; rdg[j] = rs; }
         wave_sync();
     }
+    // L back to global (strict lower = L, diagonal = 1/L_jj, the convention of the other solve
+    // paths; read by dbslmm_variance)
+    for (int r = 0; r < m; ++r)
+        if (lane <= r) A[static_cast<int64_t>(r) * ld + lane] = lane == r ? rdg[r] : L[tri(r) + lane];
     // backward substitution L^T x = y, y = row m
     double v = lane < m ? L[tri(m) + lane] : 0.0;
     for (int j = m - 1; j >= 0; --j) {
@@ -544,7 +548,7 @@ __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* 
 
 // Blocks with ld <= 64: one wave each, kSmallWaves per workgroup.
 extern "C" __global__ __launch_bounds__(chol::kSmallWaves * chol::kWave) void dbslmm_chol_small(
-    const double* __restrict__ M, const int32_t* __restrict__ order, int32_t n_blocks,
+    double* __restrict__ M, const int32_t* __restrict__ order, int32_t n_blocks,
     const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
     const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
     const int64_t* __restrict__ blk_matoff, const int32_t* __restrict__ blk_id,

@@ -8,8 +8,10 @@
 //
 // Extensions (not in the reference): --gpu N (HIP device), --tau T (default 0.8 as hard-coded at
 // scr/dbslmmfit.cpp:697,751), --precise-out (17 significant digits), --dry-run (stop after
-// matching; prints counts, no GPU).  -dat_str / -test_indicator_file are accepted; the test-set
-// variance file (variance.txt, scr/calc_asymptotic_variance.cpp) is not produced yet.
+// matching; prints counts, no GPU).  With -dat_str and -test_indicator_file the test-set variance
+// matrix is written to ./variance.txt (arma_ascii, scr/dbslmmfit.cpp:242), evaluated on the GPU
+// from the solve's factorisation (dbslmm_plan_variance); with -h2f it belongs to the last factor,
+// as the reference's file after the driver's last run.
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/time.h>
@@ -221,6 +223,85 @@ void to_csr(const vector<Info>& info, int nb, vector<int64_t>& ptr, vector<int32
     }
 }
 
+// readTestBim (scr/calc_asymptotic_variance.cpp:142-153): the bp (4th tab field) of each line
+vector<long> read_test_bim(const string& path) {
+    vector<long> out;
+    std::ifstream f(path);
+    string line;
+    while (std::getline(f, line)) {
+        auto t = split(line, '\t');
+        out.push_back(t.size() > 3 ? atol(t[3].c_str()) : 0);
+    }
+    return out;
+}
+
+// makePosObjectForTestBim (scr/calc_asymptotic_variance.cpp:160-180): pos = the FIRST test .bim
+// line with the SNP's bp; SNPs without one are dropped
+vector<Pos> make_pos_for_test_bim(const vector<long>& base, const vector<Pos>& inter) {
+    std::unordered_map<long, int64_t> first;
+    for (size_t i = 0; i < base.size(); ++i) first.emplace(base[i], static_cast<int64_t>(i));
+    vector<Pos> out;
+    for (const Pos& e : inter) {
+        auto it = first.find(e.ps);
+        if (it == first.end()) continue;
+        Pos q = e;
+        q.pos = it->second;
+        out.push_back(q);
+    }
+    return out;
+}
+
+// read_indices_file (scr/subset_to_test_and_training.cpp:132-150): first space field per line
+vector<int32_t> read_indicator(const string& path) {
+    vector<int32_t> out;
+    std::ifstream f(path);
+    string line;
+    while (std::getline(f, line)) out.push_back(static_cast<int32_t>(atol(split(line, ' ').empty() ? "0" : split(line, ' ')[0].c_str())));
+    return out;
+}
+
+// calcBlock pairs the i-th SNP of a block with the i-th test SNP of the same block
+// (test_info_s_block[i].pos, scr/dbslmmfit.cpp:394-396); a block with fewer test SNPs is an
+// out-of-range read in the reference and an error here.
+bool align_test_pos(const vector<Info>& info, const vector<Info>& t_info, int nb, vector<int32_t>& out,
+                    string& err) {
+    vector<vector<int64_t>> per(nb);
+    for (const auto& e : t_info) per[e.block].push_back(e.pos);
+    vector<size_t> used(nb, 0);
+    out.resize(info.size());
+    for (size_t i = 0; i < info.size(); ++i) {
+        const int b = info[i].block;
+        if (used[b] >= per[b].size()) {
+            err = "block " + std::to_string(b) + ": SNP " + info[i].snp + " has no counterpart in the test .bim";
+            return false;
+        }
+        out[i] = static_cast<int32_t>(per[b][used[b]++]);
+    }
+    return true;
+}
+
+// arma::Mat::save(..., arma_ascii) for a double matrix: header, dims, then each row with every
+// element preceded by a space in scientific notation (precision 14, width 22)
+bool save_arma_ascii(const string& path, const vector<double>& colmajor, int64_t rows, int64_t cols) {
+    std::ofstream f(path);
+    if (!f) return false;
+    f << "ARMA_MAT_TXT_FN008\n" << rows << ' ' << cols << '\n';
+    f.setf(std::ios::scientific);
+    f.precision(14);
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int64_t c = 0; c < cols; ++c) {
+            const double v = colmajor[static_cast<size_t>(c) * rows + r];
+            f.put(' ');
+            f.width(22);
+            if (std::isnan(v)) f << "nan";
+            else if (std::isinf(v)) f << (v > 0 ? "inf" : "-inf");
+            else f << v;
+        }
+        f.put('\n');
+    }
+    return static_cast<bool>(f);
+}
+
 int fail(const string& msg) {
     std::cerr << "ERROR: " << msg << std::endl;
     return 1;
@@ -292,12 +373,13 @@ int main(int argc, char** argv) {
         if (!good_s[i]) bad << summ_s[i].snp << " " << 0 << "\n";
 
     vector<Info> info_l;
+    vector<Pos> inter_l;
     bool has_l = false;
     if (lf) {
         std::cout << "Reading summary data of large effect SNPs from [" << p.l << "]\n";
         const vector<Summ> summ_l = read_summ(p.l);
         vector<char> good_l;
-        const vector<Pos> inter_l = match_ref(summ_l, bim, p.mafMax, good_l);
+        inter_l = match_ref(summ_l, bim, p.mafMax, good_l);
         if (!inter_l.empty()) {
             info_l = add_block(inter_l, blocks);
             std::cout << "After filtering, " << inter_l.size() << " large effect SNPs are selected.\n";
@@ -309,8 +391,22 @@ int main(int argc, char** argv) {
             if (!good_l[i]) bad << summ_l[i].snp << " " << 1 << "\n";
     }
     bad.close();
-    if (!p.dat_str.empty() || !p.test_indicator_file.empty())
-        std::cout << "[NOTE] -dat_str / -test_indicator_file accepted; variance.txt is not produced by this build.\n";
+    // test panel of the variance output (scr/dbslmm.cpp:264-320)
+    const bool want_var = !p.dat_str.empty() && !p.test_indicator_file.empty();
+    if (!want_var && (!p.dat_str.empty() || !p.test_indicator_file.empty()))
+        std::cout << "[NOTE] variance.txt needs both -dat_str and -test_indicator_file; skipped.\n";
+    vector<int32_t> ts_pos, tl_pos, indicator;
+    if (want_var) {
+        const vector<long> base = read_test_bim(p.dat_str + ".bim");
+        string err;
+        if (!align_test_pos(info_s, add_block(make_pos_for_test_bim(base, inter_s), blocks),
+                            static_cast<int>(blocks.size()), ts_pos, err) ||
+            (has_l && !align_test_pos(info_l, add_block(make_pos_for_test_bim(base, inter_l), blocks),
+                                      static_cast<int>(blocks.size()), tl_pos, err)))
+            return fail("test panel " + p.dat_str + ": " + err);
+        indicator = read_indicator(p.test_indicator_file);
+        if (indicator.empty()) return fail(p.test_indicator_file + " is empty or missing");
+    }
 
     const int nb = static_cast<int>(blocks.size());
     vector<int64_t> s_ptr, l_ptr;
@@ -360,8 +456,32 @@ int main(int argc, char** argv) {
     dbslmm_plan* plan = nullptr;
     int rc = dbslmm_plan_create(ctx, &prob, &plan);
     if (rc == DBSLMM_OK) rc = dbslmm_plan_run_multi(plan, sigmas.data(), nf, beta_s.data(), beta_l.data(), status.data());
+    if (rc != DBSLMM_OK) {
+        dbslmm_plan_destroy(plan);
+        return fail(string("dbslmm_plan_run_multi: ") + dbslmm_last_error(ctx));
+    }
+    if (want_var) {
+        Mapped tbed;
+        if (!tbed.open(p.dat_str + ".bed")) {
+            dbslmm_plan_destroy(plan);
+            return fail(p.dat_str + ".bed cannot be opened");
+        }
+        int64_t n_test = 0;
+        for (int32_t v : indicator) n_test += v != 0;
+        vector<double> diags(static_cast<size_t>(n_test) * nb);
+        dbslmm_test_panel tp{tbed.p, static_cast<int64_t>(tbed.n), static_cast<int32_t>(indicator.size()),
+                             indicator.data(), ts_pos.data(), has_l ? tl_pos.data() : nullptr};
+        rc = dbslmm_plan_variance(plan, &tp, diags.data(), nullptr);
+        if (rc != DBSLMM_OK) {
+            dbslmm_plan_destroy(plan);
+            return fail(string("dbslmm_plan_variance: ") + dbslmm_last_error(ctx));
+        }
+        if (!save_arma_ascii("variance.txt", diags, n_test, nb)) {
+            dbslmm_plan_destroy(plan);
+            return fail("variance.txt cannot be written");
+        }
+    }
     dbslmm_plan_destroy(plan);
-    if (rc != DBSLMM_OK) return fail(string("dbslmm_plan_run_multi: ") + dbslmm_last_error(ctx));
     std::cout << "Fitting time: " << walltime() - t0 << " seconds.\n";
 
     for (int f = 0; f < nf; ++f) {

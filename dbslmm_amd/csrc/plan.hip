@@ -29,6 +29,7 @@
 #include "kernels.hip"
 #include "chol.hip"
 #include "chol_tiled.hip"
+#include "variance.hip"
 
 namespace {
 // events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large,
@@ -93,6 +94,8 @@ struct dbslmm_plan {
     double* d_Mkeep = nullptr;         // pristine Gram for multi-sigma runs (allocated on demand)
     std::vector<int32_t> h_ld;  // per non-empty block
     std::vector<int32_t> h_empty;  // original ids of empty blocks
+    std::vector<int32_t> h_slot_out;  // slot -> small index s, large -1-l, padding INT32_MIN
+    double sigma_run = 0.0;        // sigma_s of the factorisation held in d_M
     // workload figures
     double wl[DBSLMM_WORKLOAD_LEN] = {0};
     // timing
@@ -316,6 +319,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     }
     p->n_nonempty = static_cast<int32_t>(row0.size());
     p->n_slots = static_cast<int32_t>(slot_pos.size());
+    p->h_slot_out = slot_out;
     p->n_tiles = static_cast<int32_t>(tiles.size());
     std::vector<GramTile> btiles;
     {
@@ -679,6 +683,7 @@ static int run_impl(dbslmm_plan* p, bool front, int keep) {
         HIP_TRY(ctx, hipEventRecord(ev[7], s));
     }
     p->ran = true;
+    p->sigma_run = p->sigma_s;
     return DBSLMM_OK;
 }
 
@@ -765,6 +770,89 @@ int dbslmm_est(dbslmm_ctx* ctx, const dbslmm_problem* pr, double* beta_s, double
     if (!rc) rc = dbslmm_plan_sync(p);
     if (!rc) rc = dbslmm_plan_download(p, beta_s, beta_l, block_status);
     dbslmm_plan_destroy(p);
+    return rc;
+}
+
+// Test-set variance: compact the test panel to the plan's slots and the
+// indicator-1 individuals, standardise (readSNPIm + nomalizeVec over n_test), then one
+// forward-substitution pass per block against the factor the solve left in d_M.
+int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diags,
+                         int32_t* n_test_out) {
+    if (!p) return DBSLMM_E_ARG;
+    dbslmm_ctx* ctx = p->ctx;
+    if (!p->ran) { ctx->err = "plan_variance before plan_run"; return DBSLMM_E_STATE; }
+    ARG_CHECK(ctx, tp && tp->bed && tp->indicator && tp->n_total > 0, "bad test panel");
+    ARG_CHECK(ctx, p->n_s == 0 || tp->s_pos, "test panel s_pos missing");
+    ARG_CHECK(ctx, p->n_l == 0 || tp->l_pos, "test panel l_pos missing");
+    std::vector<int32_t> sel;
+    for (int32_t i = 0; i < tp->n_total; ++i)
+        if (tp->indicator[i] != 0) sel.push_back(i);   // readSNPIm skips only 0 entries
+    const int32_t n_test = static_cast<int32_t>(sel.size());
+    if (n_test_out) *n_test_out = n_test;
+    if (n_test == 0 || p->num_block == 0) return DBSLMM_OK;
+    ARG_CHECK(ctx, diags, "null diags");
+    const int64_t tbps = (tp->n_total + 3) / 4;
+    const int64_t n_rows = (tp->bed_len - 3) / tbps;
+    ARG_CHECK(ctx, tp->bed_len >= 3 + tbps, "test bed image shorter than one SNP row");
+    std::vector<int32_t> tpos(p->n_slots);
+    for (int32_t s = 0; s < p->n_slots; ++s) {
+        const int32_t o = p->h_slot_out[s];
+        int32_t r = -1;
+        if (o >= 0) r = tp->s_pos[o];
+        else if (o != INT32_MIN) r = tp->l_pos[-1 - o];
+        ARG_CHECK(ctx, o == INT32_MIN || (r >= 0 && r < n_rows), "test SNP bed row out of range");
+        tpos[s] = r;
+    }
+    const int64_t cbps = (n_test + 3) / 4;
+    const int64_t nt_pad = round_up(n_test, 64);
+    const int64_t cbytes = 3 + static_cast<int64_t>(p->n_slots) * cbps + 64;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    uint8_t *d_tbed = nullptr, *d_cbed = nullptr;
+    int32_t *d_tpos = nullptr, *d_sel = nullptr, *d_cpos = nullptr;
+    double *d_mu = nullptr, *d_rsd = nullptr, *d_Y = nullptr, *d_diags = nullptr;
+    std::vector<int32_t> cpos(p->n_slots);
+    for (int32_t s = 0; s < p->n_slots; ++s) cpos[s] = tpos[s] >= 0 ? s : -1;
+    const size_t ndiag = static_cast<size_t>(n_test) * p->num_block;
+    int rc = DBSLMM_OK;
+    do {
+        hipError_t e;
+        if ((e = hipMalloc(&d_tbed, tp->bed_len + 16)) != hipSuccess ||
+            (e = hipMemset(d_tbed, 0, tp->bed_len + 16)) != hipSuccess ||
+            (e = hipMemcpy(d_tbed, tp->bed, tp->bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = dev_upload(&d_tpos, tpos)) != hipSuccess || (e = dev_upload(&d_sel, sel)) != hipSuccess ||
+            (e = dev_upload(&d_cpos, cpos)) != hipSuccess ||
+            (e = hipMalloc(&d_cbed, cbytes)) != hipSuccess ||
+            (e = hipMemset(d_cbed, 0, cbytes)) != hipSuccess ||
+            (e = hipMalloc(&d_mu, std::max<int32_t>(1, p->n_slots) * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_rsd, std::max<int32_t>(1, p->n_slots) * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_Y, std::max<int64_t>(1, p->n_slots) * nt_pad * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&d_diags, ndiag * sizeof(double))) != hipSuccess ||
+            (e = hipMemsetAsync(d_diags, 0, ndiag * sizeof(double), st)) != hipSuccess) {
+            ctx->err = std::string("variance alloc/upload: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+            break;
+        }
+        if (p->n_slots > 0 && p->n_nonempty > 0) {
+            hipLaunchKernelGGL(dbslmm_test_compact, dim3(static_cast<unsigned>((cbps + 255) / 256), p->n_slots),
+                               dim3(256), 0, st, d_tbed, tbps, d_tpos, p->n_slots, d_sel, n_test, cbps, d_cbed);
+            hipLaunchKernelGGL(dbslmm_unpack_stats, dim3(static_cast<unsigned>((p->n_slots + 3) / 4)), dim3(256), 0,
+                               st, d_cbed, n_test, cbps, d_cpos, d_cpos, p->n_slots, nullptr,
+                               nt_pad, nullptr, d_mu, d_rsd, nullptr, nullptr);
+            hipLaunchKernelGGL(dbslmm_variance, dim3(static_cast<unsigned>(nt_pad / 64), p->n_nonempty),
+                               dim3(256), 0, st, p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld,
+                               p->d_matoff, p->d_blk_id, p->d_status, d_cbed, cbps, d_mu, d_rsd, n_test,
+                               p->sigma_run, static_cast<double>(p->n_obs), d_Y, nt_pad, d_diags);
+        }
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess ||
+            (e = hipMemcpy(diags, d_diags, ndiag * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) {
+            ctx->err = std::string("variance run: ") + hipGetErrorString(e);
+            rc = DBSLMM_E_HIP;
+        }
+    } while (0);
+    void* bufs[] = {d_tbed, d_cbed, d_tpos, d_sel, d_cpos, d_mu, d_rsd, d_Y, d_diags};
+    for (void* q : bufs)
+        if (q) (void)hipFree(q);
     return rc;
 }
 

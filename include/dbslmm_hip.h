@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 2
+#define DBSLMM_ABI_VERSION 3
 
 enum {
     DBSLMM_OK = 0,
@@ -140,6 +140,31 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * the tiled blocks, [11] tiled blocks, [12] launches of the tiled sequence per run. */
 #define DBSLMM_WORKLOAD_LEN 13
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
+
+/* Test-set variance (the `diags` matrix DBSLMMFIT::est saves to variance.txt,
+ * scr/dbslmmfit.cpp:116,191-214,242; calcBlock :366-626 with calc_nt_by_nt_matrix,
+ * scr/calc_asymptotic_variance.cpp:22-137).  The test panel is a PLINK .bed image of n_total
+ * individuals; indicator[0..n_total) selects the test individuals (nonzero; readSNPIm,
+ * dtpr.cpp:285-364); s_pos / l_pos give each small / large SNP of the plan (same order and
+ * length as the problem's s_pos / l_pos, l_pos NULL when the plan has no large SNPs) its row
+ * in the test .bed (calcBlock's positional test_info_s_block[i].pos).
+ */
+typedef struct dbslmm_test_panel {
+    const uint8_t* bed;
+    int64_t bed_len;
+    int32_t n_total;
+    const int32_t* indicator;
+    const int32_t* s_pos;
+    const int32_t* l_pos;
+} dbslmm_test_panel;
+
+/* After plan_run / plan_run_multi (uses the factorisation of the most recent sigma_s):
+ * diags is n_test x num_block column-major, n_test = number of indicator entries equal to 1;
+ * column b = diag(X_l var_bl X_l^T + X_s var_bs X_s^T) of block b, zeros for a block without
+ * SNPs, NaN for a block whose status is NOT_PD / MONOMORPHIC.  Synchronous; host buffers.
+ * n_test_out (optional) receives n_test. */
+int dbslmm_plan_variance(dbslmm_plan* plan, const dbslmm_test_panel* test, double* diags,
+                         int32_t* n_test_out);
 
 /* MAF pass: maf[r] for every bed row r < n_snp (readSNPIm with an all-ones indicator). */
 int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,

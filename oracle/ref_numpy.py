@@ -468,3 +468,100 @@ def valid(d_path, s_path, ref, maf_max, block_path):
     bed = open(ref + ".bed", "rb").read()
     nume, deno, _ = valid_blocks(bed, n_ref, summp, blocks)
     return [f"{format_g(a)} {format_g(b)}" for a, b in zip(nume, deno)], nume, deno
+
+
+# ------------------------------------------------------------ test-set variance
+def read_test_bim(path: str):
+    """readTestBim (calc_asymptotic_variance.cpp:143-153): the 4th tab field (bp) of each line."""
+    with open(path) as f:
+        return [line.rstrip("\n").split("\t")[3] for line in f]
+
+
+def make_pos_for_test_bim(base_nums, inter):
+    """makePosObjectForTestBim (calc_asymptotic_variance.cpp:160-180): each SNP's row in the test
+    .bim = the FIRST line with the same bp (O(M^2) scan in the reference; same result)."""
+    first = {}
+    for i, s in enumerate(base_nums):
+        first.setdefault(int(s), i)
+    out = []
+    for p in inter:
+        if p["ps"] in first:
+            e = dict(p)
+            e["pos"] = first[p["ps"]]
+            out.append(e)
+    return out
+
+
+def read_indicator(path: str) -> np.ndarray:
+    """read_indices_file (subset_to_test_and_training.cpp:132-150): first space field per line."""
+    with open(path) as f:
+        return np.array([int(line.rstrip("\n").split(" ")[0]) for line in f], dtype=np.int32)
+
+
+def read_test_block_matrix(bed, rows, indicator: np.ndarray) -> np.ndarray:
+    """calcBlock's test columns (dbslmmfit.cpp:427-429): readSNPIm over the indicator-1
+    individuals of the test panel, nomalizeVec -> n_test x m."""
+    n_test = int(indicator.sum())
+    X = np.zeros((n_test, len(rows)))
+    for c, p in enumerate(rows):
+        g, _ = read_snp_im(bed, int(p), indicator)
+        X[:, c] = normalize(g)
+    return X
+
+
+def nt_diag_ls(sigma_ll, sigma_sl, sigma_ss, sigma2_s, n, Xl_test, Xs_test):
+    """calc_nt_by_nt_matrix, large+small (calc_asymptotic_variance.cpp:22-43, with calc_A_inverse
+    :66-74, calc_var_betal :86-96, calc_var_betas :109-123) -> diag of the n_test x n_test matrix."""
+    ms = sigma_ss.shape[0]
+    ainv = np.linalg.inv(np.eye(ms) / (n * sigma2_s) + sigma_ss)
+    big = sigma_ll - sigma_sl.T @ ainv @ sigma_sl
+    var_bl = np.linalg.inv(big) / n
+    mat1 = sigma_ss - sigma_ss @ ainv @ sigma_ss
+    mat2 = sigma_sl - sigma_ss @ ainv @ sigma_sl
+    var_bs = n * sigma2_s * sigma2_s * (mat1 + mat2 * n @ var_bl @ mat2.T)
+    res = Xl_test @ var_bl @ Xl_test.T + Xs_test @ var_bs @ Xs_test.T
+    return np.diag(res).copy()
+
+
+def nt_diag_s(sigma_ss, sigma2_s, n, Xs_test):
+    """calc_nt_by_nt_matrix, small only (calc_asymptotic_variance.cpp:47-57, :127-137)."""
+    ms = sigma_ss.shape[0]
+    ainv = np.linalg.inv(np.eye(ms) / (n * sigma2_s) + sigma_ss)
+    var_bs = n * sigma2_s * sigma2_s * (sigma_ss - sigma_ss @ ainv @ sigma_ss)
+    return np.diag(Xs_test @ var_bs @ Xs_test.T).copy()
+
+
+def block_sigmas(Xs, Xl, n_ref, tau=0.8):
+    """Sigma_ss, Sigma_sl, Sigma_ll of estBlock (dbslmmfit.cpp:698-709), diagonal restored."""
+    ss = tau * Xs.T @ Xs / n_ref + (1 - tau) * np.eye(Xs.shape[1])
+    if Xl is None or Xl.shape[1] == 0:
+        return ss, None, None
+    sl = tau * Xs.T @ Xl / n_ref
+    ll = tau * Xl.T @ Xl / n_ref + (1 - tau) * np.eye(Xl.shape[1])
+    return ss, sl, ll
+
+
+def variance_diags(bed, n_ref, n_obs, sigma_s, num_block, info_s, info_l, test_bed, indicator,
+                   test_info_s, test_info_l, tau=0.8):
+    """The diags matrix of DBSLMMFIT::est (dbslmmfit.cpp:116, 191-214, 242): n_test x num_block,
+    column b = calcBlock's variance diag (zeros for a block without SNPs)."""
+    n_test = int(indicator.sum())
+    diags = np.zeros((n_test, num_block))
+    for b in range(num_block):
+        rs = [x["pos"] for x in info_s if x["block"] == b]
+        rl = [x["pos"] for x in (info_l or []) if x["block"] == b]
+        ts = [x["pos"] for x in test_info_s if x["block"] == b]
+        tl = [x["pos"] for x in (test_info_l or []) if x["block"] == b]
+        if not rs:
+            continue
+        Xs = read_block_matrix(bed, rs, n_ref)
+        Xs_t = read_test_block_matrix(test_bed, ts[:len(rs)], indicator)
+        if rl:
+            Xl = read_block_matrix(bed, rl, n_ref)
+            Xl_t = read_test_block_matrix(test_bed, tl[:len(rl)], indicator)
+            ss, sl, ll = block_sigmas(Xs, Xl, n_ref, tau)
+            diags[:, b] = nt_diag_ls(ll, sl, ss, sigma_s, n_obs, Xl_t, Xs_t)
+        else:
+            ss, _, _ = block_sigmas(Xs, None, n_ref, tau)
+            diags[:, b] = nt_diag_s(ss, sigma_s, n_obs, Xs_t)
+    return diags

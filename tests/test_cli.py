@@ -18,10 +18,10 @@ def run(args, cwd=None):
     return subprocess.run([CLI] + args, capture_output=True, text=True, cwd=cwd, timeout=300)
 
 
-def split_summary(tmp):
+def split_summary(tmp, summ=SUMM):
     L = set(l_snps())
     s_path, l_path = os.path.join(tmp, "s.txt"), os.path.join(tmp, "l.txt")
-    with open(SUMM) as f, open(s_path, "w") as fs, open(l_path, "w") as fl:
+    with open(summ) as f, open(s_path, "w") as fs, open(l_path, "w") as fl:
         for line in f:
             (fl if line.split("\t")[1] in L else fs).write(line)
     return s_path, l_path
