@@ -3,8 +3,10 @@
 
 One "step" = one full solve of the workload with the packed genotypes already resident in HBM:
 2-bit unpack + per-SNP stats -> joint i8-MFMA Gram per LD block -> fp64 Cholesky + solves ->
-beta in HBM.  Default workload = BASELINE.json configs[1]: synthetic 50k SNPs x 2k individuals
-over the 22-chromosome EUR LD blocks, DBSLMM (large + small effects), h2 = 0.5.
+beta in HBM.  Default workload = the configuration BASELINE.json's metric is quoted on
+("1M SNP x 10k indiv"), configs[3]: synthetic 1M SNPs x 10k individuals over the 22-chromosome
+EUR LD blocks, DBSLMM (large + small effects), h2 = 0.5 tuned over h2f in {0.8, 1.0, 1.2} (one
+Gram + three factorisations and solves per step).  --config 2 is the small configs[1] case.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
@@ -43,8 +45,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
-                    help="BASELINE.json configs[i-1] preset (2 = default single-GPU workload)")
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i-1] preset (4 = the metric's 1M x 10k workload)")
     ap.add_argument("--snps", type=int, default=None)
     ap.add_argument("--n-ref", type=int, default=None)
     ap.add_argument("--pop", default=None)
@@ -90,19 +92,23 @@ def kernel_roofline(name, ms, wl, n_solve=1):
                         if name == "dbslmm_tchol" else "; latency-bound (sequential column chain)"))
 
 
-def pmc_traffic(kernel, args):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
-    WRITE_SIZE, tools/pmc_traffic.py) of this same default workload, or None."""
+def pmc_traffic(kernel, args, n_solve):
+    """HBM bytes per step of `kernel` from the latest committed rocprofv3 PMC passes (FETCH_SIZE x2
+    + WRITE_SIZE, tools/pmc_traffic.py) of this same preset workload (profiles/r*/
+    pmc_traffic_c<N>.json), or None.  The tiled sequence is counted per solve x n_solve."""
     import glob
-    default = (args.snps, args.n_ref, args.pop, args.lmm_only, args.gen) == (50000, 2000, "EUR", False, "numpy")
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
-    if not default or not files:
+    preset = CONFIGS[args.config]
+    same = all(getattr(args, k) == (v if k != "h2f" else [float(x) for x in v.split(",")])
+               for k, v in preset.items()) and (args.h2f is None) == ("h2f" not in preset)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_c{args.config}.json")))
+    if not same or not files:
         return None, None
     d = json.load(open(files[-1]))
     k = d.get("kernels", {}).get(kernel)
     if not k:
         return None, None
-    return k["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    per = k["hbm_bytes"] * (n_solve if kernel.startswith("dbslmm_chol") or kernel == "dbslmm_tchol" else 1)
+    return per, os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -176,7 +182,7 @@ def main():
     n_solve = len(sigmas) if sigmas else 1
     kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl, n_solve) for k in range(len(KERNEL_NAMES))]
     dom = max(kernels, key=lambda r: r["ms"])
-    traffic, tsrc = pmc_traffic(dom["kernel"], args)
+    traffic, tsrc = pmc_traffic(dom["kernel"], args, n_solve)
     roof = dict(bound=dom["bound"], achieved=dom["achieved"], peak=dom["peak"], unit=dom["unit"],
                 frac=dom["frac"], traffic=traffic, kernel=dom["kernel"], traffic_source=tsrc)
 

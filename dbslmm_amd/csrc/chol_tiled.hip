@@ -42,6 +42,23 @@ struct TiledArgs {
     double* beta_s;
     double* beta_l;
     int32_t* status;
+    // replicated factorisations (h2f tuning): item block id bq = b + c * nb is copy c, whose
+    // matrices, sigma scalar, scratch, betas and status sit at these strides
+    int32_t nb;
+    int64_t m_stride, y_stride, bs_stride, bl_stride, st_stride;
+
+    __device__ __forceinline__ TiledArgs view(int bq, int& b) const {
+        const int c = bq / nb;
+        b = bq - c * nb;
+        TiledArgs v = *this;
+        v.M += c * m_stride;
+        v.dshift += c;
+        v.y += c * y_stride;
+        v.beta_s += c * bs_stride;
+        v.beta_l += c * bl_stride;
+        v.status += c * st_stride;
+        return v;
+    }
 };
 
 // work list of one launch: act[0..n) = plan block indices, pfx[0..n] = prefix of item counts
@@ -258,27 +275,29 @@ __device__ __forceinline__ void lds_to_acc(v4d (&acc)[2][2], const double* W, in
 __device__ __forceinline__ int rsub(int a, int b) { return a * (a + 1) / 2 + b; }
 constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X10 (2) + colb
 
-// C(I, J..) -= L_{I,s} L_{J,s}^T, K = 128 as two 64-deep phases, over a run of tiles J0..J1 of
-// tile row I (skips the strictly-upper quadrant of a diagonal tile).  Next phase's operands and
-// the next tile's C are prefetched into registers while the current phase's MFMAs run.
-__device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int J1, int c0,
+// C(I, J..) -= L_{I,.} L_{J,.}^T over columns c0 .. c0 + 128 nk, K = 128 nk as 2 nk 64-deep
+// phases, over a run of tiles J0..J1 of tile row I (skips the strictly-upper quadrant of a
+// diagonal tile).  Next phase's operands and the next tile's C are prefetched into registers
+// while the current phase's MFMAs run.
+__device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int J1, int c0, int nk,
                                            double* lds, int tid) {
     const int lane = tid & 63, wave = tid >> 6, qi = wave >> 1, qj = wave & 1;
     double* LI = lds;
     double* LJ = lds + 4 * kSub;
     double li[16], lj[16];
     v4d acc[2][2], nxt[2][2];
-    const int nph = 2 * (J1 - J0 + 1);
+    const int P = 2 * nk;                       // phases per tile
+    const int nph = P * (J1 - J0 + 1);
     tile_regs_load(li, A, ld, kBT * I, c0, tid);
     if (I != J0) tile_regs_load(lj, A, ld, kBT * J0, c0, tid);
     load_acc(acc, A, ld, kBT * I + kT * qi, kBT * J0 + kT * qj, lane);
     for (int p = 0; p < nph; ++p) {
-        const int J = J0 + (p >> 1);
+        const int J = J0 + p / P;
         tile_regs_store(li, LI, tid);
         if (I != J) tile_regs_store(lj, LJ, tid);
         __syncthreads();
         if (p + 1 < nph) {
-            const int Jn = J0 + ((p + 1) >> 1), kcn = (p + 1) & 1;
+            const int Jn = J0 + (p + 1) / P, kcn = (p + 1) % P;
             tile_regs_load(li, A, ld, kBT * I, c0 + kBT * kcn, tid);
             if (I != Jn) tile_regs_load(lj, A, ld, kBT * Jn, c0 + kBT * kcn, tid);
             if (kcn == 0) load_acc(nxt, A, ld, kBT * I + kT * qi, kBT * Jn + kT * qj, lane);
@@ -289,7 +308,7 @@ __device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int
             mfma_tile(acc, LI + (2 * qi) * kSub, LJp + (2 * qj) * kSub, -1.0, lane);
             mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJp + (2 * qj + 1) * kSub, -1.0, lane);
         }
-        if (p & 1) {
+        if (p % P == P - 1) {
             if (!skip) store_acc(acc, A, ld, kBT * I + kT * qi, kBT * J + kT * qj, lane);
 #pragma unroll
             for (int si = 0; si < 2; ++si)
@@ -305,18 +324,20 @@ __device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int
 // ---------------------------------------------------------------- kernels
 // Factor region r (128 x 128 at c0 = 128 r) of each listed block, entirely in LDS (one workgroup
 // per block, 4 waves): load the region's lower sub-tiles -- applying the pending K = 128 update
-// C -= P P^T from the panel of step r-1 when `update` (P staged one 32-column slice at a time) --
+// C -= P P^T from the panels of regions r-update .. r-1 (update = 0, 1, 2; P staged one 32-column
+// slice at a time) --
 // then four 32-column steps (wave 0: factor_tile_lds; all waves: MFMA panel and trailing updates
 // inside the region), the 64-level inverse blocks X10 = -X11 L10 X00 of its two 64 x 64
 // diagonal tiles, and one write-back: strict lower = L, each 64 x 64 diagonal tile's diagonal +
 // upper = its X^T (what the panel and the backward solve read).  Region 0 without update also
 // writes the z row and flags monomorphic SNPs.
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_region(
-    chol::TiledArgs a, int32_t reg, int32_t update, const int32_t* __restrict__ blocks, int32_t n) {
+    chol::TiledArgs a0, int32_t reg, int32_t update, const int32_t* __restrict__ blocks, int32_t n) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n) return;
-    const int b = blocks[blockIdx.x];
+    int b;
+    const TiledArgs a = a0.view(blocks[blockIdx.x], b);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b], ms = a.blk_ms[b];
     double* A = a.M + a.blk_matoff[b];
@@ -347,8 +368,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     }
     if (update) {
         double* P = X32;   // staging of one 32-column slice of the panel rows (4 sub-tiles)
-        const int cp = c0 - 2 * kBT;
-        for (int k = 0; k < 4; ++k) {
+        const int cp = c0 - 2 * kBT * update;
+        for (int k = 0; k < 4 * update; ++k) {
             __syncthreads();
             stage_tile(P + wave * kSub, A, ld, c0 + kT * wave, cp + kT * k, lane);
             __syncthreads();
@@ -457,12 +478,14 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
 // (i << 8)): L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of
 // the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_panel(
-    chol::TiledArgs a, int32_t s, const int32_t* __restrict__ items, int32_t n_items) {
+    chol::TiledArgs a0, int32_t s, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
     const int32_t it = items[blockIdx.x];
-    const int b = it >> 16, i = (it >> 8) & 255;
+    const int i = (it >> 8) & 255;
+    int b;
+    const TiledArgs a = a0.view(it >> 16, b);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qi = wave >> 1, qj = wave & 1;
     const int m = a.blk_m[b], ld = a.blk_ld[b];
     const int T = (m + kBT - 1) / kBT;
@@ -503,23 +526,27 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);     // L_i1
 }
 
-// trailing update of outer step s.  Items (block << 16) | (I << 8) | J0, -1 = padding: a run of
+// trailing update with the panels of regions s .. s+nk-1 (K = 128 nk).  Items (block << 16) |
+// (I << 8) | J0, -1 = padding: a run of
 // tiles (I, J0 .. J0 + run - 1) (clipped to the lower triangle; run = kJRun while the step has
 // plenty of tiles, 1 in the short tail steps), for tile rows below region
 // s+1 (which dbslmm_tchol_region updates and factors itself); per-XCD queues (item e runs on
 // XCD e % 8; the runs of one tile row I of a block share an XCD, so L_I is served by its L2).
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_trailing(
-    chol::TiledArgs a, int32_t s, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
+    chol::TiledArgs a0, int32_t s, int32_t run, int32_t nk, const int32_t* __restrict__ items,
+    int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
     const int32_t it = items[blockIdx.x];
     if (it < 0) return;
-    const int b = it >> 16, I = (it >> 8) & 255, J0 = it & 255;
+    const int I = (it >> 8) & 255, J0 = it & 255;
+    int b;
+    const TiledArgs a = a0.view(it >> 16, b);
     const int m = a.blk_m[b], ld = a.blk_ld[b];
     const int T = (m + kBT - 1) / kBT;
     double* A = a.M + a.blk_matoff[b];
-    update_run(A, ld, I, J0, min(J0 + run - 1, min(I, T - 1)), 2 * kBT * s, lds, threadIdx.x);
+    update_run(A, ld, I, J0, min(J0 + run - 1, min(I, T - 1)), 2 * kBT * s, nk, lds, threadIdx.x);
 }
 
 // backward step J (launches J = Kmax-1 .. 0).  v lives in y[row0 ..]; x_J overwrites v_J once
@@ -550,7 +577,7 @@ __device__ __forceinline__ void tile_x(const double* A, int ld, int c1, int jmax
 }  // namespace chol
 
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_backward(
-    chol::TiledArgs a, int32_t J, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
+    chol::TiledArgs a0, int32_t J, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
     int32_t n) {
     using namespace chol;
     __shared__ double D[kBT * (kBT + 1)];
@@ -560,7 +587,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_b
     const int item = blockIdx.x;
     if (item >= pfx[n]) return;
     const int s = find_item(pfx, n, item);
-    const int b = act[s];
+    int b;
+    const TiledArgs a = a0.view(act[s], b);
     const int chunk = item - pfx[s];
     const int tid = threadIdx.x;
     const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b];

@@ -50,6 +50,7 @@ struct TLaunch {
     int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
     int32_t n;
     int32_t items;    // workgroups
+    int32_t nk = 1;   // trailing: K = 128 nk (regions step .. step+nk-1); region: pending panels
 };
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -91,8 +92,19 @@ struct dbslmm_plan {
     double* d_M = nullptr;
     double *d_beta_s = nullptr, *d_beta_l = nullptr;
     double* d_dshift = nullptr;        // 1/(sigma_s n), read by the solve kernels
-    double* d_Mkeep = nullptr;         // pristine Gram for multi-sigma runs (allocated on demand)
+    // h2f tuning: n_copies independent factorisations of the same Gram, copy c at
+    // d_M + c M_elems (and the per-copy sigma scalar, scratch, betas, status); one merged tiled
+    // sequence factors all copies (tl_multi, built for multi_n copies)
+    int32_t n_copies = 1;
+    int64_t nbk = 1;                   // status entries per copy
+    std::vector<TLaunch> tl_multi;
+    int32_t* d_tlist_multi = nullptr;
+    int32_t multi_n = 0;
+    hipGraphExec_t graph_multi = nullptr;
+    int32_t var_copy = 0;              // copy holding the latest factorisation (variance)
     std::vector<int32_t> h_ld;  // per non-empty block
+    std::vector<int32_t> h_m;   // per non-empty block
+    std::vector<int32_t> h_tb;  // blocks on the tiled path
     std::vector<int32_t> h_empty;  // original ids of empty blocks
     std::vector<int32_t> h_slot_out;  // slot -> small index s, large -1-l, padding INT32_MIN
     double sigma_run = 0.0;        // sigma_s of the factorisation held in d_M
@@ -131,6 +143,125 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
     if (e != hipSuccess) return e;
     if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
     return e;
+}
+
+// Launch list of the tiled sequence: region 0, then super steps of 256 columns, then the backward
+// steps, for the blocks `tb` (plan block indices), each replicated over `copies` independent
+// factorisations (h2f tuning: item block id bq = b + c * nb addresses copy c of the matrices).
+//   super step (regions r0 = 2S, r1 = 2S + 1; 64-tile columns 4S .. 4S+3):
+//   panel(r0) -> region(r1) [+ pending K = 128 update from panel r0] ->
+//   trailing K = 128 of region r1's columns (from panel r0) -> panel(r1) ->
+//   trailing K = 256 of everything right of region r1 (from panels r0, r1) ->
+//   region(r0 + 2) [+ pending K = 256 update].  Each C tile below is read and written once per
+//   256 columns.
+static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
+                        int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
+    std::vector<std::pair<int32_t, int32_t>> tb;   // (plan block, item block id)
+    for (int c = 0; c < copies; ++c)
+        for (int32_t b : tb0) tb.push_back({b, b + c * nb});
+    int Kmax = 0;
+    for (const auto& e : tb) Kmax = std::max<int>(Kmax, (mv[e.first] + chol::kBT - 1) / chol::kBT);
+    auto add = [&](int kind, int step, const std::vector<int32_t>& act, const std::vector<int32_t>& cnt,
+                   int extra) {
+        if (act.empty()) return;
+        TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(act.size()), 0};
+        tlist.insert(tlist.end(), act.begin(), act.end());
+        int32_t acc = 0;
+        tlist.push_back(0);
+        for (int32_t c : cnt) tlist.push_back(acc += c);
+        L.items = acc + extra;
+        tl.push_back(L);
+    };
+    if (!tb.empty()) {
+        TLaunch L{0, 0, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(tb.size()),
+                  static_cast<int32_t>(tb.size())};
+        for (const auto& e : tb) tlist.push_back(e.second);
+        tl.push_back(L);
+    }
+    auto add_items = [&](int kind, int step, std::vector<std::vector<int32_t>>& q) {
+        TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), 0, 0};
+        size_t qmax = 0;
+        for (const auto& v : q) qmax = std::max(qmax, v.size());
+        // item e runs on XCD e % 8 (L.off is kept a multiple of 8 by the padding below)
+        while ((tlist.size() - L.off) % kXcd) tlist.push_back(-1);
+        for (size_t i = 0; i < qmax; ++i)
+            for (int x = 0; x < kXcd; ++x) tlist.push_back(i < q[x].size() ? q[x][i] : -1);
+        L.items = static_cast<int32_t>(tlist.size() - L.off);
+        if (L.items > 0) tl.push_back(L);
+        return L.items > 0;
+    };
+    const int Smax = (Kmax + 1) / 2;             // 128-column regions
+    auto trailing = [&](int r, int nk, int Jlo, int Jhi_rel, int Ilo) {
+        // tiles (I >= Ilo, Jlo <= J <= min(I, T-1, Jlo + Jhi_rel)), K = 128 nk from region r
+        std::vector<std::vector<int32_t>> q(kXcd);
+        std::vector<int64_t> load(kXcd, 0);
+        int64_t ntiles = 0;
+        for (const auto& e : tb) {
+            const int T = (mv[e.first] + chol::kBT - 1) / chol::kBT, Tz = mv[e.first] / chol::kBT;
+            for (int I = Ilo; I <= Tz; ++I) ntiles += std::max(0, std::min({I, T - 1, Jlo + Jhi_rel}) - Jlo + 1);
+        }
+        // a run never crosses Jlo + Jhi_rel (the kernel clips runs only at min(I, T-1))
+        const int run = std::min(ntiles >= 4096 ? chol::kJRun : 1, Jhi_rel + 1);
+        for (const auto& e : tb) {
+            const int T = (mv[e.first] + chol::kBT - 1) / chol::kBT, Tz = mv[e.first] / chol::kBT;
+            for (int I = Ilo; I <= Tz; ++I) {
+                const int jmax = std::min({I, T - 1, Jlo + Jhi_rel});
+                if (jmax < Jlo) continue;
+                const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+                for (int J = Jlo; J <= jmax; J += run) q[x].push_back((e.second << 16) | (I << 8) | J);
+                load[x] += jmax - Jlo + 1;
+            }
+        }
+        if (add_items(2, r, q)) {
+            tl.back().n = run;
+            tl.back().nk = nk;
+        }
+    };
+    auto panel = [&](int r) {
+        std::vector<int32_t> items;
+        for (const auto& e : tb) {
+            const int Tz = mv[e.first] / chol::kBT;
+            for (int i = 2 * r + 2; i <= Tz; ++i) items.push_back((e.second << 16) | (i << 8));
+        }
+        if (items.empty()) return;
+        TLaunch L{1, r, static_cast<int32_t>(tlist.size()), 0, static_cast<int32_t>(items.size())};
+        tlist.insert(tlist.end(), items.begin(), items.end());
+        tl.push_back(L);
+    };
+    auto region = [&](int r, int nk) {   // region r of every block that has it, nk pending panels
+        std::vector<int32_t> regs;
+        for (const auto& e : tb)
+            if (2 * r <= (mv[e.first] + chol::kBT - 1) / chol::kBT - 1) regs.push_back(e.second);
+        if (regs.empty()) return;
+        TLaunch L{4, r, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(regs.size()),
+                  static_cast<int32_t>(regs.size())};
+        L.nk = nk;
+        tlist.insert(tlist.end(), regs.begin(), regs.end());
+        tl.push_back(L);
+    };
+    constexpr int kBig = 1 << 20;
+    for (int r0 = 0; r0 < Smax; r0 += 2) {
+        const int r1 = r0 + 1;
+        panel(r0);
+        if (r1 < Smax) {
+            region(r1, 1);
+            trailing(r0, 1, 2 * r1, 1, 2 * r1 + 2);           // region r1's two tile columns
+            panel(r1);
+            trailing(r0, 2, 2 * r1 + 2, kBig, 2 * r1 + 4);    // right of region r1, K = 256
+            if (r1 + 1 < Smax) region(r1 + 1, 2);
+        }
+    }
+    for (int J = Kmax - 1; J >= 0; --J) {
+        std::vector<int32_t> ba, bc;
+        for (const auto& e : tb) {
+            const int T = (mv[e.first] + chol::kBT - 1) / chol::kBT;
+            if (T > J) {
+                ba.push_back(e.second);
+                bc.push_back(std::max(1, (chol::kBT * J + chol::kLargeThreads - 1) / chol::kLargeThreads));
+            }
+        }
+        add(3, J, ba, bc, 0);
+    }
 }
 
 extern "C" {
@@ -196,11 +327,12 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
-                    p->d_Mkeep};
+                    p->d_tlist_multi};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
+    if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
     delete p;
 }
 
@@ -349,98 +481,15 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     order.erase(std::remove_if(order.begin(), order.end(), [&](int b) { return is_tiled[b] != 0; }),
                 order.end());
     for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
-    // tiled sequence: diag0, then per 128-column step s panel(s) + trailing(s), then backward(J)
-    // descending (64-row tiles)
     std::vector<int32_t> tlist;
     {
         std::vector<int32_t> tb;
-        int Kmax = 0;
         for (int b = 0; b < p->n_nonempty; ++b)
-            if (is_tiled[b]) {
-                tb.push_back(b);
-                Kmax = std::max<int>(Kmax, (mv[b] + chol::kBT - 1) / chol::kBT);
-            }
+            if (is_tiled[b]) tb.push_back(b);
         p->n_tiled = static_cast<int32_t>(tb.size());
-        auto add = [&](int kind, int step, const std::vector<int32_t>& act,
-                       const std::vector<int32_t>& cnt, int extra) {
-            if (act.empty()) return;
-            TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(act.size()), 0};
-            tlist.insert(tlist.end(), act.begin(), act.end());
-            int32_t acc = 0;
-            tlist.push_back(0);
-            for (int32_t c : cnt) tlist.push_back(acc += c);
-            L.items = acc + extra;
-            p->tl.push_back(L);
-        };
-        if (!tb.empty()) {
-            TLaunch L{0, 0, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(tb.size()),
-                      static_cast<int32_t>(tb.size())};
-            tlist.insert(tlist.end(), tb.begin(), tb.end());
-            p->tl.push_back(L);
-        }
-        // outer steps of 128 columns: s covers tile columns k0 = 2s, k1 = 2s + 1
-        auto add_items = [&](int kind, int step, const std::vector<int32_t>& head,
-                             std::vector<std::vector<int32_t>>& q) {
-            TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), 0, 0};
-            tlist.insert(tlist.end(), head.begin(), head.end());
-            size_t qmax = 0;
-            for (const auto& v : q) qmax = std::max(qmax, v.size());
-            // align the queue part so that item e of it runs on XCD e % 8
-            while ((tlist.size() - L.off) % kXcd) tlist.push_back(-1);
-            for (size_t i = 0; i < qmax; ++i)
-                for (int x = 0; x < kXcd; ++x) tlist.push_back(i < q[x].size() ? q[x][i] : -1);
-            L.items = static_cast<int32_t>(tlist.size() - L.off);
-            if (L.items > 0) p->tl.push_back(L);
-        };
-        const int Smax = (Kmax + 1) / 2;
-        for (int st = 0; st < Smax; ++st) {
-            const int k1 = 2 * st + 1;
-            std::vector<int32_t> panel, head, regs;
-            std::vector<std::vector<int32_t>> q(kXcd);
-            std::vector<int64_t> load(kXcd, 0);
-            int64_t ntiles = 0;          // trailing tiles of this step: runs of kJRun only if plenty
-            for (int32_t b : tb) {
-                const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
-                for (int I = k1 + 3; I <= Tz; ++I) ntiles += std::min(I, T - 1) - k1;
-            }
-            const int run = ntiles >= 4096 ? chol::kJRun : 1;
-            for (int32_t b : tb) {
-                const int T = (mv[b] + chol::kBT - 1) / chol::kBT, Tz = mv[b] / chol::kBT;
-                for (int i = k1 + 1; i <= Tz; ++i) panel.push_back((b << 16) | (i << 8));
-                if (k1 + 1 > T - 1) continue;          // no columns beyond this step's region
-                regs.push_back(b);                      // region s+1: update + factor in LDS
-                for (int I = k1 + 3; I <= Tz; ++I) {
-                    const int jmax = std::min(I, T - 1);
-                    const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                    for (int J = k1 + 1; J <= jmax; J += run) q[x].push_back((b << 16) | (I << 8) | J);
-                    load[x] += jmax - k1;
-                }
-            }
-            if (!panel.empty()) {
-                TLaunch L{1, st, static_cast<int32_t>(tlist.size()), 0, static_cast<int32_t>(panel.size())};
-                tlist.insert(tlist.end(), panel.begin(), panel.end());
-                p->tl.push_back(L);
-            }
-            if (!regs.empty()) {
-                TLaunch L{4, st + 1, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(regs.size()),
-                          static_cast<int32_t>(regs.size())};
-                tlist.insert(tlist.end(), regs.begin(), regs.end());
-                p->tl.push_back(L);
-            }
-            add_items(2, st, head, q);
-            if (!p->tl.empty() && p->tl.back().kind == 2 && p->tl.back().step == st) p->tl.back().n = run;
-        }
-        for (int J = Kmax - 1; J >= 0; --J) {
-            std::vector<int32_t> ba, bc;
-            for (int32_t b : tb) {
-                const int T = (mv[b] + chol::kBT - 1) / chol::kBT;
-                if (T > J) {
-                    ba.push_back(b);
-                    bc.push_back(std::max(1, (chol::kBT * J + chol::kLargeThreads - 1) / chol::kLargeThreads));
-                }
-            }
-            add(3, J, ba, bc, 0);
-        }
+        p->h_m = mv;
+        p->h_tb = tb;
+        build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist);
     }
     const double n_snp = static_cast<double>(p->n_s + p->n_l);
     p->wl[0] = n_snp;
@@ -493,6 +542,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = hipMalloc(&p->d_rsd, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
     if ((e = hipMalloc(&p->d_y, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc y");
     const size_t nbk = std::max<int32_t>(1, std::max(p->n_nonempty, p->num_block));
+    p->nbk = static_cast<int64_t>(nbk);
     if ((e = hipMalloc(&p->d_flags, nbk * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc flags");
     if ((e = hipMalloc(&p->d_status, nbk * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc status");
     if ((e = hipMalloc(&p->d_M, std::max<int64_t>(1, p->M_elems) * sizeof(double))) != hipSuccess) return fail("hipMalloc M");
@@ -535,23 +585,24 @@ static int collect_timing(dbslmm_plan* p) {
     return DBSLMM_OK;
 }
 
-// Enqueue the tiled sequence on stream2.
-static int enqueue_tiled(dbslmm_plan* p, double isn) {
+// Enqueue a tiled launch list on stream2.
+static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist) {
     dbslmm_ctx* ctx = p->ctx;
     const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
                              p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, p->d_dshift, isn,
-                             p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
+                             p->d_y, p->d_beta_s, p->d_beta_l, p->d_status, p->n_nonempty,
+                             p->M_elems, p->n_slots, p->n_s, p->n_l, p->nbk};
     hipStream_t st = ctx->stream2;
-    for (const TLaunch& L : p->tl) {
+    for (const TLaunch& L : tl) {
         if (L.items == 0) continue;
-        const int32_t* act = p->d_tlist + L.off;
+        const int32_t* act = d_tlist + L.off;
         const int32_t* pfx = act + L.n;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
         switch (L.kind) {
         case 0: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, 0, 0, act, L.n); break;
-        case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, L.step, 1, act, L.n); break;
+        case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, L.step, L.nk, act, L.n); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
-        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, L.n, act, L.items); break;
+        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, L.n, L.nk, act, L.items); break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }
     }
@@ -559,11 +610,53 @@ static int enqueue_tiled(dbslmm_plan* p, double isn) {
     return DBSLMM_OK;
 }
 
-// One run.  front: unpack + Gram (else the Gram of the previous front run is reused);
-// keep: 1 = save the Gram to d_Mkeep after the front, 2 = restore M from it before the solve.
-static int run_impl(dbslmm_plan* p, bool front, int keep) {
+// Grow the per-copy buffers to n factorisation copies (contents are rebuilt by the next run).
+static int ensure_copies(dbslmm_plan* p, int n) {
+    dbslmm_ctx* ctx = p->ctx;
+    if (n <= p->n_copies) return DBSLMM_OK;
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    void* old[] = {p->d_M, p->d_dshift, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
+    for (void* q : old)
+        if (q) (void)hipFree(q);
+    p->d_M = p->d_dshift = p->d_y = p->d_beta_s = p->d_beta_l = nullptr;
+    p->d_status = nullptr;
+    const size_t nn = static_cast<size_t>(n);
+    HIP_TRY(ctx, hipMalloc(&p->d_M, std::max<size_t>(1, nn * p->M_elems) * sizeof(double)));
+    HIP_TRY(ctx, hipMemset(p->d_M, 0, std::max<size_t>(1, nn * p->M_elems) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_dshift, nn * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_y, nn * std::max<int64_t>(1, p->n_slots) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_beta_s, nn * std::max<int64_t>(1, p->n_s) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_beta_l, nn * std::max<int64_t>(1, p->n_l) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_status, nn * p->nbk * sizeof(int32_t)));
+    p->n_copies = n;
+    // captured graphs hold the old pointers
+    if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
+    if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
+    p->graph_exec = p->graph_multi = nullptr;
+    return DBSLMM_OK;
+}
+
+// One run: unpack + Gram (front; else the Gram of the previous front run is reused), then n
+// factorisations + solves of it, copy c with sigma_s = sigmas[c] (n > 1: h2f tuning; copies
+// 1.. are device copies of the Gram, all factored by one merged tiled sequence).
+static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     dbslmm_ctx* ctx = p->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (n > 1) {
+        const int rc = ensure_copies(p, n);
+        if (rc) return rc;
+        if (p->multi_n != n) {
+            std::vector<int32_t> tlist;
+            p->tl_multi.clear();
+            build_tiled(p->h_m, p->h_tb, n, p->n_nonempty, p->tl_multi, tlist);
+            if (p->d_tlist_multi) (void)hipFree(p->d_tlist_multi);
+            p->d_tlist_multi = nullptr;
+            HIP_TRY(ctx, dev_upload(&p->d_tlist_multi, tlist));
+            if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
+            p->graph_multi = nullptr;
+            p->multi_n = n;
+        }
+    }
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
     if (p->timing) {
@@ -576,9 +669,9 @@ static int run_impl(dbslmm_plan* p, bool front, int keep) {
         ev = &p->ev[kEvPerRun * p->runs_pending];
         p->runs_pending++;
     }
-    const size_t nbk = std::max<int32_t>(1, std::max(p->n_nonempty, p->num_block));
+    const size_t nbk = static_cast<size_t>(p->nbk);
     if (front) HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, nbk * sizeof(int32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, n * nbk * sizeof(int32_t), s));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], s));
     if (front && p->n_slots > 0) {
         const int wpb = 4;
@@ -613,62 +706,69 @@ static int run_impl(dbslmm_plan* p, bool front, int keep) {
                            p->tau, p->d_M);
         HIP_TRY(ctx, hipGetLastError());
     }
-    if (keep && p->M_elems > 0) {
-        const size_t mb = static_cast<size_t>(p->M_elems) * sizeof(double);
-        if (keep == 1) HIP_TRY(ctx, hipMemcpyAsync(p->d_Mkeep, p->d_M, mb, hipMemcpyDeviceToDevice, s));
-        else HIP_TRY(ctx, hipMemcpyAsync(p->d_M, p->d_Mkeep, mb, hipMemcpyDeviceToDevice, s));
-    }
+    if (!front && n > 1)
+        return (ctx->err = "a multi-copy run needs the Gram front", DBSLMM_E_STATE);
+    // the factorisation overwrites its matrix: copies 1.. of the Gram for the other sigmas
+    for (int c = 1; c < n && p->M_elems > 0; ++c)
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_M + c * p->M_elems, p->d_M, p->M_elems * sizeof(double),
+                                    hipMemcpyDeviceToDevice, s));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
     if (p->n_nonempty > 0) {
-        const double dshift = 1.0 / (p->sigma_s * static_cast<double>(p->n_obs));
-        hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift, dshift);
+        for (int c = 0; c < n; ++c) {
+            const double dshift = 1.0 / (sigmas[c] * static_cast<double>(p->n_obs));
+            hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift + c, dshift);
+        }
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
         // fork: the tiled sequence runs on stream2 (high priority: the critical path) while the
         // single-workgroup and single-wave kernels run on the main stream.
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
-        if (p->n_large > 0) {
+        for (int c = 0; c < n && p->n_large > 0; ++c) {
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
-                               kCholLargeLds, s, p->d_M, p->d_order, p->n_large, p->d_row0, p->d_m,
-                               p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z, p->d_slot_out,
-                               p->d_rsd, p->d_dshift, isn, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status);
+                               kCholLargeLds, s, p->d_M + c * p->M_elems, p->d_order, p->n_large,
+                               p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
+                               p->d_slot_out, p->d_rsd, p->d_dshift + c, isn, p->d_y + c * p->n_slots,
+                               p->d_beta_s + c * p->n_s, p->d_beta_l + c * p->n_l,
+                               p->d_status + c * p->nbk);
             HIP_TRY(ctx, hipGetLastError());
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
         // single-wave blocks: concurrently on stream2 when there is no tiled sequence, else
         // behind the single-workgroup kernel (each stream keeps its own hardware queue)
-        hipStream_t ss = p->tl.empty() ? ctx->stream2 : s;
+        const std::vector<TLaunch>& tl = n > 1 ? p->tl_multi : p->tl;
+        hipStream_t ss = tl.empty() ? ctx->stream2 : s;
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ss));
-        if (p->n_small > 0) {
+        for (int c = 0; c < n && p->n_small > 0; ++c) {
             const unsigned g = static_cast<unsigned>((p->n_small + chol::kSmallWaves - 1) / chol::kSmallWaves);
             hipLaunchKernelGGL(dbslmm_chol_small, dim3(g), dim3(chol::kSmallWaves * chol::kWave), 0,
-                               ss, p->d_M, p->d_order + p->n_large, p->n_small, p->d_row0,
+                               ss, p->d_M + c * p->M_elems, p->d_order + p->n_large, p->n_small, p->d_row0,
                                p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
-                               p->d_slot_out, p->d_rsd, p->d_dshift, isn, p->d_beta_s, p->d_beta_l,
-                               p->d_status);
+                               p->d_slot_out, p->d_rsd, p->d_dshift + c, isn, p->d_beta_s + c * p->n_s,
+                               p->d_beta_l + c * p->n_l, p->d_status + c * p->nbk);
             HIP_TRY(ctx, hipGetLastError());
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[5], ss));
         if (ss != s) HIP_TRY(ctx, hipEventRecord(ctx->join, ss));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
-        if (!p->tl.empty()) {
-            // the tiled sequence (~2 launches per 128-column step) is replayed from a graph
-            // captured on first use (sigma is read from a device scalar, so it stays valid)
-            if (!p->graph_exec) {
+        if (!tl.empty()) {
+            // the tiled sequence (~2.5 launches per 128 columns) is replayed from a graph
+            // captured on first use (sigma is read from device scalars, so it stays valid)
+            hipGraphExec_t& gx = n > 1 ? p->graph_multi : p->graph_exec;
+            if (!gx) {
                 hipGraph_t gr = nullptr;
                 HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-                const int rc = enqueue_tiled(p, isn);
+                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist);
                 hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
                 if (rc != DBSLMM_OK) {
                     if (gr) (void)hipGraphDestroy(gr);
                     return rc;
                 }
                 HIP_TRY(ctx, ce);
-                hipError_t ie = hipGraphInstantiate(&p->graph_exec, gr, nullptr, nullptr, 0);
+                hipError_t ie = hipGraphInstantiate(&gx, gr, nullptr, nullptr, 0);
                 (void)hipGraphDestroy(gr);
                 HIP_TRY(ctx, ie);
             }
-            HIP_TRY(ctx, hipGraphLaunch(p->graph_exec, ctx->stream2));
+            HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));
         HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
@@ -683,42 +783,51 @@ static int run_impl(dbslmm_plan* p, bool front, int keep) {
         HIP_TRY(ctx, hipEventRecord(ev[7], s));
     }
     p->ran = true;
-    p->sigma_run = p->sigma_s;
+    p->sigma_run = sigmas[n - 1];
+    p->var_copy = n - 1;
+    return DBSLMM_OK;
+}
+
+static int download_copy(dbslmm_plan* p, int c, double* beta_s, double* beta_l, int32_t* block_status) {
+    dbslmm_ctx* ctx = p->ctx;
+    if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (beta_s && p->n_s)
+        HIP_TRY(ctx, hipMemcpy(beta_s, p->d_beta_s + c * p->n_s, p->n_s * sizeof(double), hipMemcpyDeviceToHost));
+    if (beta_l && p->n_l)
+        HIP_TRY(ctx, hipMemcpy(beta_l, p->d_beta_l + c * p->n_l, p->n_l * sizeof(double), hipMemcpyDeviceToHost));
+    if (block_status && p->num_block) {
+        HIP_TRY(ctx, hipMemcpy(block_status, p->d_status + c * p->nbk, p->num_block * sizeof(int32_t),
+                               hipMemcpyDeviceToHost));
+        for (int32_t b : p->h_empty) block_status[b] = DBSLMM_BLOCK_EMPTY;
+    }
     return DBSLMM_OK;
 }
 
 int dbslmm_plan_run(dbslmm_plan* p) {
     if (!p) return DBSLMM_E_ARG;
-    return run_impl(p, true, 0);
+    return run_impl(p, true, &p->sigma_s, 1);
 }
 
-// h2f tuning (software/DBSLMM.R:204-219 runs dbslmm once per h2 factor): one unpack + Gram,
-// then one factorisation + solve per sigma, the Gram restored from a device copy in between.
+// h2f tuning (software/DBSLMM.R:204-219 runs dbslmm once per h2 factor): one unpack + Gram, then
+// n_sigma factorisations + solves of device copies of it, all in one merged launch sequence.
 int dbslmm_plan_run_multi(dbslmm_plan* p, const double* sigmas, int32_t n_sigma, double* beta_s,
                           double* beta_l, int32_t* block_status) {
     if (!p) return DBSLMM_E_ARG;
     dbslmm_ctx* ctx = p->ctx;
-    ARG_CHECK(ctx, sigmas && n_sigma > 0, "sigmas / n_sigma");
+    ARG_CHECK(ctx, sigmas && n_sigma > 0 && n_sigma <= 64, "sigmas / n_sigma (1..64)");
     for (int i = 0; i < n_sigma; ++i)
         ARG_CHECK(ctx, sigmas[i] > 0.0 && std::isfinite(sigmas[i]), "sigma_s must be > 0");
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (n_sigma > 1 && !p->d_Mkeep && p->M_elems > 0)
-        HIP_TRY(ctx, hipMalloc(&p->d_Mkeep, static_cast<size_t>(p->M_elems) * sizeof(double)));
-    const double sigma0 = p->sigma_s;
-    for (int i = 0; i < n_sigma; ++i) {
-        p->sigma_s = sigmas[i];
-        int rc = run_impl(p, i == 0, n_sigma > 1 ? (i == 0 ? 1 : 2) : 0);
-        if (!rc) rc = dbslmm_plan_sync(p);
-        if (!rc) rc = dbslmm_plan_download(p, beta_s ? beta_s + static_cast<int64_t>(i) * p->n_s : nullptr,
-                                           beta_l ? beta_l + static_cast<int64_t>(i) * p->n_l : nullptr,
-                                           block_status ? block_status + static_cast<int64_t>(i) * p->num_block : nullptr);
-        if (rc) {
-            p->sigma_s = sigma0;
-            return rc;
-        }
-    }
-    p->sigma_s = sigma0;
-    return DBSLMM_OK;
+    ARG_CHECK(ctx, static_cast<int64_t>(p->n_nonempty) * n_sigma < 32768,
+              "blocks x sigmas must stay below 32768 (packed work items)");
+    int rc = run_impl(p, true, sigmas, n_sigma);
+    if (!rc) rc = dbslmm_plan_sync(p);
+    for (int i = 0; i < n_sigma && !rc; ++i)
+        rc = download_copy(p, i, beta_s ? beta_s + static_cast<int64_t>(i) * p->n_s : nullptr,
+                           beta_l ? beta_l + static_cast<int64_t>(i) * p->n_l : nullptr,
+                           block_status ? block_status + static_cast<int64_t>(i) * p->num_block : nullptr);
+    return rc;
 }
 
 int dbslmm_plan_sync(dbslmm_plan* p) {
@@ -745,19 +854,7 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
 
 int dbslmm_plan_download(dbslmm_plan* p, double* beta_s, double* beta_l, int32_t* block_status) {
     if (!p) return DBSLMM_E_ARG;
-    dbslmm_ctx* ctx = p->ctx;
-    if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (beta_s && p->n_s)
-        HIP_TRY(ctx, hipMemcpy(beta_s, p->d_beta_s, p->n_s * sizeof(double), hipMemcpyDeviceToHost));
-    if (beta_l && p->n_l)
-        HIP_TRY(ctx, hipMemcpy(beta_l, p->d_beta_l, p->n_l * sizeof(double), hipMemcpyDeviceToHost));
-    if (block_status && p->num_block) {
-        HIP_TRY(ctx, hipMemcpy(block_status, p->d_status, p->num_block * sizeof(int32_t), hipMemcpyDeviceToHost));
-        for (int32_t b : p->h_empty) block_status[b] = DBSLMM_BLOCK_EMPTY;
-    }
-    return DBSLMM_OK;
+    return download_copy(p, p->var_copy, beta_s, beta_l, block_status);
 }
 
 int dbslmm_est(dbslmm_ctx* ctx, const dbslmm_problem* pr, double* beta_s, double* beta_l,
@@ -840,8 +937,9 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
                                st, d_cbed, n_test, cbps, d_cpos, d_cpos, p->n_slots, nullptr,
                                nt_pad, nullptr, d_mu, d_rsd, nullptr, nullptr);
             hipLaunchKernelGGL(dbslmm_variance, dim3(static_cast<unsigned>(nt_pad / 64), p->n_nonempty),
-                               dim3(256), 0, st, p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld,
-                               p->d_matoff, p->d_blk_id, p->d_status, d_cbed, cbps, d_mu, d_rsd, n_test,
+                               dim3(256), 0, st, p->d_M + p->var_copy * p->M_elems, p->d_row0, p->d_m,
+                               p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_status + p->var_copy * p->nbk,
+                               d_cbed, cbps, d_mu, d_rsd, n_test,
                                p->sigma_run, static_cast<double>(p->n_obs), d_Y, nt_pad, d_diags);
         }
         if ((e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess ||

@@ -135,3 +135,31 @@ def test_gram_kernels_bit_identical(monkeypatch, miss, n_ref):
             np.testing.assert_array_equal(x, y)
     ref, _ = _oracle(prob)
     assert normwise(np.concatenate(out[0][:2]), ref) < 1e-10
+
+
+@pytest.mark.parametrize("tiled_min", ["64", "512"])
+def test_run_multi_merged_copies_bit_identical(monkeypatch, tiled_min):
+    """h2f tuning factors device copies of the Gram in ONE merged tiled sequence (block ids
+    b + c * nb): each copy must equal a fresh single-sigma plan bit for bit, with the monomorphic
+    block NaN in every copy; a plain run afterwards (copy 0 again) and the variance-holding copy
+    (the last sigma) stay consistent."""
+    from dbslmm_amd import Context, DBSLMMFIT, Plan
+    monkeypatch.setenv("DBSLMM_TILED_MIN", tiled_min)
+    prob = _problem(seed=5, mono_block=3)
+    plan = Plan(Context(0), prob)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    multi = plan.run_multi(sig)
+    fit = DBSLMMFIT(0)
+    for f, (bs, bl, st) in zip(sig, multi):
+        prob.sigma_s = f
+        rs, rl, rst = fit.est(prob)
+        np.testing.assert_array_equal(bs, rs)
+        np.testing.assert_array_equal(bl, rl)
+        np.testing.assert_array_equal(st, rst)
+        assert st[3] == 3
+    prob.sigma_s = sig[2]
+    last = plan.download()
+    np.testing.assert_array_equal(last[0], multi[2][0])
+    plan.set_sigma(sig[0])
+    plan.run()
+    np.testing.assert_array_equal(plan.download()[0], multi[0][0])

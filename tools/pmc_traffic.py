@@ -2,7 +2,11 @@
 
 FETCH_SIZE and WRITE_SIZE are in KB.  On gfx950 FETCH_SIZE reports half of the bytes of a wide
 coalesced streaming read (MI355X_MICROARCH.md, HBM section): the read side is doubled here.
-    python tools/pmc_traffic.py gpurun_out/pmc profiles/r01/pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc profiles/r01/pmc_traffic_c4.json [bench args]
+
+Also records launches per kernel and, for the tiled Cholesky (a sequence of dbslmm_tchol_*
+launches per solve), the summed HBM bytes per solve under "dbslmm_tchol" (solves = launches of
+dbslmm_set_scalar, one per factorisation).
 """
 import collections
 import csv
@@ -12,28 +16,37 @@ import sys
 
 
 def per_kernel(path):
-    agg = collections.defaultdict(list)
+    agg = collections.defaultdict(dict)
     for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+        # one row per (dispatch, counter instance) -> sum the instances of a dispatch
+        d = agg[r["Kernel_Name"]]
+        d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return {k: (sum(v.values()) / len(v), len(v)) for k, v in agg.items()}
 
 
-def main(src, dst):
+def main(src, dst, bench_args=""):
     f = per_kernel(os.path.join(src, "fetch_counter_collection.csv"))
     w = per_kernel(os.path.join(src, "write_counter_collection.csv"))
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over "
-                     "`python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline`",
+                     f"`python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline {bench_args}`".rstrip(),
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
            "kernels": {}}
+    solves = f.get("dbslmm_set_scalar", (0, 0))[1]
+    seq = 0.0
     for k in sorted(set(f) | set(w)):
         if not k.startswith("dbslmm_"):
             continue
-        fk, wk = f.get(k, 0.0), w.get(k, 0.0)
-        out["kernels"][k] = dict(fetch_kb=fk, write_kb=wk, hbm_bytes=(2 * fk + wk) * 1024.0)
+        (fk, n), (wk, _) = f.get(k, (0.0, 0)), w.get(k, (0.0, 0))
+        out["kernels"][k] = dict(fetch_kb=fk, write_kb=wk, hbm_bytes=(2 * fk + wk) * 1024.0, launches=n)
+        if k.startswith("dbslmm_tchol_"):
+            seq += (2 * fk + wk) * 1024.0 * n
+    if solves and seq:
+        out["kernels"]["dbslmm_tchol"] = dict(hbm_bytes=seq / solves, solves=solves,
+                                              note="sum over dbslmm_tchol_* launches per solve")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], " ".join(sys.argv[3:]))
