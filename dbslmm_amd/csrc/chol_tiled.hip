@@ -476,9 +476,10 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
 
 // panel of outer step s, one workgroup per 64-row tile i below region s (item (block << 16) |
 // (i << 8)): L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of
-// the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).
+// the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).  upd: first apply
+// the pending update of A_i from the panel of region s-1.
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_panel(
-    chol::TiledArgs a0, int32_t s, const int32_t* __restrict__ items, int32_t n_items) {
+    chol::TiledArgs a0, int32_t s, int32_t upd, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
@@ -497,15 +498,34 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     // every global load of the workgroup first (one latency), then the three products
     double x00[16], ai0[16], l10[16], x11[16];
     v4d cc[2][2];
+    v4d u0[2][2];
+    if (upd) {
+        // pending K = 128 update from the panel of region s-1 (what a trailing launch of region
+        // s's columns would do): A_i -= L_{i,s-1} L_{R,s-1}^T, R = region s's 128 rows; wave
+        // (qi, qj) updates its quadrant of both 64-column halves, operands staged 32 columns
+        // at a time (sub-tiles 0-1: rows of tile i, 2-5: rows of the region)
+        const int cp = c0 - 2 * kBT;
+        load_acc(u0, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);
+        if (two) load_acc(cc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);
+        for (int kc = 0; kc < 4; ++kc) {
+            for (int q = wave; q < 6; q += 4)
+                stage_tile(lds + q * kSub, A, ld, q < 2 ? kBT * i + kT * q : c0 + kT * (q - 2), cp + kT * kc, lane);
+            __syncthreads();
+            mfma_tile(u0, lds + qi * kSub, lds + (2 + qj) * kSub, -1.0, lane);
+            if (two) mfma_tile(cc, lds + qi * kSub, lds + (4 + qj) * kSub, -1.0, lane);
+            __syncthreads();
+        }
+    }
     xregs_load(x00, A, ld, c0, c0, true, tid);
-    tile_regs_load(ai0, A, ld, kBT * i, c0, tid);
+    if (!upd) tile_regs_load(ai0, A, ld, kBT * i, c0, tid);
     if (two) {
         tile_regs_load(l10, A, ld, c0 + kBT, c0, tid);
         xregs_load(x11, A, ld, c0 + kBT, c0 + kBT, true, tid);
-        load_acc(cc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);   // A_i1
+        if (!upd) load_acc(cc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);   // A_i1
     }
     xregs_store(x00, XS, tid);
-    tile_regs_store(ai0, W, tid);
+    if (upd) acc_to_lds(u0, W + (2 * qi + qj) * kSub, lane);
+    else tile_regs_store(ai0, W, tid);
     __syncthreads();
     v4d acc[2][2];
     zero_acc(acc);
@@ -547,6 +567,261 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tcho
     const int T = (m + kBT - 1) / kBT;
     double* A = a.M + a.blk_matoff[b];
     update_run(A, ld, I, J0, min(J0 + run - 1, min(I, T - 1)), 2 * kBT * s, nk, lds, threadIdx.x);
+}
+
+// ---------------------------------------------------------------- 128 x 128 trailing update
+// C(I, J) -= L_I L_J^T on 128 x 128 tiles (I, J in units of 128 rows), K = 128 nk from column
+// c0, one 512-thread workgroup per run of tiles J0..J1 of tile row I.  A 64 x 64 tile does 8 flops
+// per operand byte loaded, which at the f64 MFMA rate needs ~10 TB/s of L2/HBM operand traffic;
+// a 128 x 128 tile halves that (the bulk of the factorisation is bound by it), and reads its MFMA
+// operands from LDS as conflict-free ds_read_b128 pairs:
+//   * K is staged 32 columns at a time: A = -L_I (128 x 32), B = L_J (128 x 32), row-major in LDS
+//     with a 36-double row stride, double-buffered (one barrier per stage); the next stage is
+//     loaded into registers (16-B global loads) while the current one is multiplied;
+//   * wave w (8 waves) owns rows 64 (w >> 2) .., columns 32 (w & 3) .. of the tile: 4 x 2
+//     accumulators of v_mfma_f64_16x16x4_f64.  The MFMA pair (k, k+1) of lane group q takes
+//     k = 8 j + 2 q (+1): one 16-B read per operand row feeds two MFMAs;
+//   * on a diagonal tile (I == J) the two waves wholly above the diagonal skip their MFMAs and
+//     stores; the next tile's C is prefetched during the last stage of the current one.
+namespace chol {
+constexpr int kT2 = 128;                 // tile edge
+constexpr int kK2 = 32;                  // K per stage
+constexpr int kS2 = 36;                  // LDS row stride (doubles)
+constexpr int kOp2 = kT2 * kS2;          // one operand stage buffer
+constexpr int kTrail2Doubles = 4 * kOp2; // A, B x 2 buffers
+constexpr int kRun2 = 2;                 // tiles per run (when a step has plenty of tiles)
+
+__device__ __forceinline__ void t2_load_stage(v2d (&r)[8], const double* A, int ld, int I, int J, int col, int tid) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int op = it >> 2, e = (it & 3) * 512 + tid;     // 2048 16-B chunks per operand
+        const int row = e >> 4, kc = (e & 15) * 2;
+        const int rb = kT2 * (op ? J : I);
+        r[it] = *reinterpret_cast<const v2d*>(A + static_cast<int64_t>(rb + row) * ld + col + kc);
+    }
+}
+__device__ __forceinline__ void t2_store_stage(const v2d (&r)[8], double* S, int tid) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int op = it >> 2, e = (it & 3) * 512 + tid;
+        const int row = e >> 4, kc = (e & 15) * 2;
+        v2d v = r[it];
+        if (op == 0) v = -v;                                   // A = -L_I: the MFMA subtracts
+        *reinterpret_cast<v2d*>(S + op * kOp2 + row * kS2 + kc) = v;
+    }
+}
+__device__ __forceinline__ void t2_load_c(v4d (&c)[4][2], const double* A, int ld, int r0, int c0, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                c[i][j][q] = A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)];
+}
+__device__ __forceinline__ void t2_store_c(const v4d (&c)[4][2], double* A, int ld, int r0, int c0, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)] = c[i][j][q];
+}
+// acc += A_w B_w^T over one 32-deep stage (A already negated)
+__device__ __forceinline__ void t2_mfma_stage(v4d (&acc)[4][2], const double* S, int wr, int wc, int lane) {
+    const double* SA = S + (64 * wr + (lane & 15)) * kS2 + 2 * (lane >> 4);
+    const double* SB = S + kOp2 + (32 * wc + (lane & 15)) * kS2 + 2 * (lane >> 4);
+#pragma unroll
+    for (int j8 = 0; j8 < kK2 / 8; ++j8) {
+        v2d a[4], b[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v2d*>(SA + 16 * i * kS2 + 8 * j8);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const v2d*>(SB + 16 * j * kS2 + 8 * j8);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][h], b[j][h], acc[i][j], 0, 0, 0);
+    }
+}
+}  // namespace chol
+
+extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing2(
+    chol::TiledArgs a0, int32_t s, int32_t run, int32_t nk, const int32_t* __restrict__ items,
+    int32_t n_items) {
+    using namespace chol;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (static_cast<int>(blockIdx.x) >= n_items) return;
+    const int32_t it = items[blockIdx.x];
+    if (it < 0) return;
+    const int I = (it >> 8) & 255, J0 = it & 255;
+    int b;
+    const TiledArgs a = a0.view(it >> 16, b);
+    const int m = a.blk_m[b], ld = a.blk_ld[b];
+    const int T2 = (m + kT2 - 1) / kT2;
+    const int J1 = min(J0 + run - 1, min(I, T2 - 1));
+    double* A = a.M + a.blk_matoff[b];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
+    const int c0 = 2 * kBT * s;
+    const int nst = 4 * nk;                        // stages per tile
+    const int total = nst * (J1 - J0 + 1);
+    v2d st[8];
+    v4d acc[4][2], nxt[4][2];
+    t2_load_stage(st, A, ld, I, J0, c0, tid);
+    t2_load_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J0 + 32 * wc, lane);
+    for (int g = 0; g < total; ++g) {
+        const int J = J0 + g / nst, t = g % nst;
+        double* S = lds + (g & 1) * 2 * kOp2;
+        t2_store_stage(st, S, tid);
+        __syncthreads();
+        if (g + 1 < total) {
+            const int Jn = J0 + (g + 1) / nst, tn = (g + 1) % nst;
+            t2_load_stage(st, A, ld, I, Jn, c0 + kK2 * tn, tid);
+            if (tn == 0) t2_load_c(nxt, A, ld, kT2 * I + 64 * wr, kT2 * Jn + 32 * wc, lane);
+        }
+        const bool skip = I == J && 32 * wc > 64 * wr + 63;
+        if (!skip) t2_mfma_stage(acc, S, wr, wc, lane);
+        if (t == nst - 1) {
+            if (!skip) t2_store_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J + 32 * wc, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = nxt[i][j];
+        }
+    }
+}
+
+// The same update fed by LDS-DMA (global_load_lds_dwordx4): no staging registers, no LDS store
+// instructions.  Operand rows are unpadded in LDS (32 doubles = 16 chunks of 16 B); the DMA image
+// is lane-linear, so the swizzle goes through the SOURCE address: LDS position p of row r holds
+// K chunk p ^ (r & 15), which puts the 16 rows of every ds_read_b128 lane group on 16 distinct
+// bank groups.  Two slots; per stage: wait for this wave's DMA, barrier, issue the next stage's
+// DMA into the other slot (every wave has left it), multiply.  acc holds -C (negated on load and
+// store), so the MFMAs add L_I L_J^T.
+namespace chol {
+constexpr int kOp3 = kT2 * kK2;                // one operand stage, unpadded (32 KiB)
+constexpr int kTrail3Doubles = 4 * kOp3;       // A, B x 2 slots (128 KiB)
+typedef __attribute__((address_space(1))) const void* gptr_f;
+typedef __attribute__((address_space(3))) void* lptr_f;
+
+__device__ __forceinline__ void t3_load_c(v4d (&c)[4][2], const double* A, int ld, int r0, int c0, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                c[i][j][q] = -A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)];
+}
+__device__ __forceinline__ void t3_store_c(const v4d (&c)[4][2], double* A, int ld, int r0, int c0, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)] = -c[i][j][q];
+}
+// DMA of one stage (rows 16 w .. 16 w + 15 of each operand; 4 rows per instruction)
+__device__ __forceinline__ void t3_issue(double* slot, const double* A, int ld, int I, int J, int col,
+                                         bool diag, int wave, int lane) {
+    const int rr = lane >> 4, p = lane & 15;
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+        if (op == 1 && diag) break;
+        const int rb = kT2 * (op ? J : I);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = 16 * wave + 4 * q + rr;
+            const int c = p ^ (r & 15);
+            __builtin_amdgcn_global_load_lds((gptr_f)(A + static_cast<int64_t>(rb + r) * ld + col + 2 * c),
+                                             (lptr_f)(slot + op * kOp3 + (16 * wave + 4 * q) * kK2), 16, 0, 0);
+        }
+    }
+}
+__device__ __forceinline__ void t3_mfma_stage(v4d (&acc)[4][2], const double* SA, const double* SB,
+                                              int wr, int wc, int lane) {
+    const int ri = lane & 15, kq = lane >> 4;
+    // operand reads one 8-deep group ahead of the MFMAs that consume them
+    v2d a[2][4], b[2][2];
+    auto load = [&](int j8, int u) {
+        const int pc = 2 * ((4 * j8 + kq) ^ ri);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[u][i] = *reinterpret_cast<const v2d*>(SA + (64 * wr + 16 * i + ri) * kK2 + pc);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[u][j] = *reinterpret_cast<const v2d*>(SB + (32 * wc + 16 * j + ri) * kK2 + pc);
+    };
+    load(0, 0);
+#pragma unroll
+    for (int j8 = 0; j8 < kK2 / 8; ++j8) {
+        const int u = j8 & 1;
+        if (j8 + 1 < kK2 / 8) load(j8 + 1, u ^ 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][i][h], b[u][j][h], acc[i][j], 0, 0, 0);
+    }
+}
+}  // namespace chol
+
+extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
+    chol::TiledArgs a0, int32_t s, int32_t run, int32_t nk, const int32_t* __restrict__ items,
+    int32_t n_items) {
+    using namespace chol;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (static_cast<int>(blockIdx.x) >= n_items) return;
+    const int32_t it = items[blockIdx.x];
+    if (it < 0) return;
+    const int I = (it >> 8) & 255, J0 = it & 255;
+    int b;
+    const TiledArgs a = a0.view(it >> 16, b);
+    const int m = a.blk_m[b], ld = a.blk_ld[b];
+    const int T2 = (m + kT2 - 1) / kT2;
+    const int J1 = min(J0 + run - 1, min(I, T2 - 1));
+    double* A = a.M + a.blk_matoff[b];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
+    const int c0 = 2 * kBT * s;
+    const int nst = 4 * nk;
+    const int total = nst * (J1 - J0 + 1);
+    v4d acc[4][2], nxt[4][2];
+    t3_issue(lds, A, ld, I, J0, c0, I == J0, wave, lane);
+    t3_load_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J0 + 32 * wc, lane);
+    // tile j's C store is issued at the start of tile j+1's first stage (after that stage's DMA),
+    // so it drains under that stage's MFMAs instead of in front of the next vmcnt wait
+    for (int g = 0; g < total; ++g) {
+        const int J = J0 + g / nst, t = g % nst;
+        const bool diag = I == J;
+        double* S = lds + (g & 1) * 2 * kOp3;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA (and C traffic)
+        __builtin_amdgcn_s_barrier();                        // stage g is in LDS; slot g+1 free
+        if (g + 1 < total) {
+            const int Jn = J0 + (g + 1) / nst, tn = (g + 1) % nst;
+            t3_issue(lds + ((g + 1) & 1) * 2 * kOp3, A, ld, I, Jn, c0 + kK2 * tn, I == Jn, wave, lane);
+            if (tn == 0) t3_load_c(nxt, A, ld, kT2 * I + 64 * wr, kT2 * Jn + 32 * wc, lane);
+        }
+        if (t == 0 && g > 0) {
+            const int Jp = J - 1;
+            if (!(Jp == I && 32 * wc > 64 * wr + 63)) t3_store_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * Jp + 32 * wc, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = nxt[i][j];
+        }
+        const bool skip = diag && 32 * wc > 64 * wr + 63;
+        if (!skip) t3_mfma_stage(acc, S, diag ? S : S + kOp3, wr, wc, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    {
+        const int J = J1;
+        if (!(J == I && 32 * wc > 64 * wr + 63)) t3_store_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J + 32 * wc, lane);
+    }
 }
 
 // backward step J (launches J = Kmax-1 .. 0).  v lives in y[row0 ..]; x_J overwrites v_J once

@@ -38,6 +38,8 @@ constexpr int kEvPerRun = 8;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
+constexpr size_t kTrail2Lds = sizeof(double) * chol::kTrail2Doubles;
+constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3Doubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
@@ -45,7 +47,8 @@ constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
-    int kind;         // 0 region 0, 1 panel, 2 trailing, 3 backward, 4 region `step` with update
+    int kind;         // 0 region 0, 1 panel, 2 trailing, 3 backward, 4 region `step` with update,
+                      // 5 trailing on 128 x 128 tiles
     int step;
     int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
     int32_t n;
@@ -102,6 +105,7 @@ struct dbslmm_plan {
     int32_t multi_n = 0;
     hipGraphExec_t graph_multi = nullptr;
     int32_t var_copy = 0;              // copy holding the latest factorisation (variance)
+    bool trail_dma = true;             // 128-tile trailing fed by LDS-DMA (env DBSLMM_TRAIL_DMA=0: registers)
     std::vector<int32_t> h_ld;  // per non-empty block
     std::vector<int32_t> h_m;   // per non-empty block
     std::vector<int32_t> h_tb;  // blocks on the tiled path
@@ -150,12 +154,15 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 // factorisations (h2f tuning: item block id bq = b + c * nb addresses copy c of the matrices).
 //   super step (regions r0 = 2S, r1 = 2S + 1; 64-tile columns 4S .. 4S+3):
 //   panel(r0) -> region(r1) [+ pending K = 128 update from panel r0] ->
-//   trailing K = 128 of region r1's columns (from panel r0) -> panel(r1) ->
-//   trailing K = 256 of everything right of region r1 (from panels r0, r1) ->
-//   region(r0 + 2) [+ pending K = 256 update].  Each C tile below is read and written once per
-//   256 columns.
+//   panel(r1) [+ pending K = 128 update of its rows' region-r1 columns from panel r0] ->
+//   trailing K = 256 of everything right of region r1, region r0 + 2 included (panels r0, r1) ->
+//   region(r0 + 2).  Each C tile below is read and written once per 256 columns; the chain of
+//   dependent launches is 5 per 256 columns.
 static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
                         int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
+    // trailing updates on 128 x 128 tiles (dbslmm_tchol_trailing2) unless DBSLMM_TRAIL64=1
+    const char* t64 = getenv("DBSLMM_TRAIL64");
+    const bool t128 = !(t64 && atoi(t64) != 0);
     std::vector<std::pair<int32_t, int32_t>> tb;   // (plan block, item block id)
     for (int c = 0; c < copies; ++c)
         for (int32_t b : tb0) tb.push_back({b, b + c * nb});
@@ -191,8 +198,48 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
         return L.items > 0;
     };
     const int Smax = (Kmax + 1) / 2;             // 128-column regions
+    auto trailing2 = [&](int r, int nk, int Jlo, int Jhi_rel, int Ilo) {
+        // the same tile set in 128 x 128 tiles (Jlo, Ilo, Jhi_rel + 1 even in 64-tile units)
+        std::vector<std::vector<int32_t>> q(kXcd);
+        std::vector<int64_t> load(kXcd, 0);
+        const int jl = Jlo / 2, il = Ilo / 2, jh = (Jhi_rel + 1) / 2 - 1;
+        int64_t ntiles = 0;
+        for (const auto& e : tb) {
+            const int T = (mv[e.first] + 127) / 128, Tz = mv[e.first] / 128;
+            for (int I = il; I <= Tz; ++I) ntiles += std::max(0, std::min({I, T - 1, jl + jh}) - jl + 1);
+        }
+        int run2 = chol::kRun2;
+        if (const char* e = getenv("DBSLMM_RUN2")) run2 = std::max(1, atoi(e));
+        const int run = std::min(ntiles >= 1024 ? run2 : 1, jh + 1);
+        for (const auto& e : tb) {
+            const int T = (mv[e.first] + 127) / 128, Tz = mv[e.first] / 128;
+            for (int I = il; I <= Tz; ++I) {
+                const int jmax = std::min({I, T - 1, jl + jh});
+                if (jmax < jl) continue;
+                const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+                for (int J = jl; J <= jmax; J += run) q[x].push_back((e.second << 16) | (I << 8) | J);
+                load[x] += jmax - jl + 1;
+            }
+        }
+        // within an XCD, walk each block's rows in windows of 8 tile columns: the workgroups in
+        // flight on the XCD then share both their L_I and their L_J strips in its L2
+        if (const char* e = getenv("DBSLMM_TRAIL_ORDER"); !(e && atoi(e) == 0))
+            for (auto& v : q)
+                std::stable_sort(v.begin(), v.end(), [](int32_t u, int32_t w) {
+                    const int bu = u >> 16, bw = w >> 16;
+                    if (bu != bw) return bu < bw;
+                    const int ju = (u & 255) >> 3, jw = (w & 255) >> 3;
+                    if (ju != jw) return ju < jw;
+                    return (u & 0xffff) < (w & 0xffff);
+                });
+        if (add_items(5, r, q)) {
+            tl.back().n = run;
+            tl.back().nk = nk;
+        }
+    };
     auto trailing = [&](int r, int nk, int Jlo, int Jhi_rel, int Ilo) {
         // tiles (I >= Ilo, Jlo <= J <= min(I, T-1, Jlo + Jhi_rel)), K = 128 nk from region r
+        if (t128) return trailing2(r, nk, Jlo, Jhi_rel, Ilo);
         std::vector<std::vector<int32_t>> q(kXcd);
         std::vector<int64_t> load(kXcd, 0);
         int64_t ntiles = 0;
@@ -217,7 +264,7 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             tl.back().nk = nk;
         }
     };
-    auto panel = [&](int r) {
+    auto panel = [&](int r, int upd) {
         std::vector<int32_t> items;
         for (const auto& e : tb) {
             const int Tz = mv[e.first] / chol::kBT;
@@ -225,6 +272,7 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
         }
         if (items.empty()) return;
         TLaunch L{1, r, static_cast<int32_t>(tlist.size()), 0, static_cast<int32_t>(items.size())};
+        L.nk = upd;
         tlist.insert(tlist.end(), items.begin(), items.end());
         tl.push_back(L);
     };
@@ -242,13 +290,13 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
     constexpr int kBig = 1 << 20;
     for (int r0 = 0; r0 < Smax; r0 += 2) {
         const int r1 = r0 + 1;
-        panel(r0);
+        panel(r0, 0);
         if (r1 < Smax) {
-            region(r1, 1);
-            trailing(r0, 1, 2 * r1, 1, 2 * r1 + 2);           // region r1's two tile columns
-            panel(r1);
-            trailing(r0, 2, 2 * r1 + 2, kBig, 2 * r1 + 4);    // right of region r1, K = 256
-            if (r1 + 1 < Smax) region(r1 + 1, 2);
+            region(r1, 1);           // + its pending K = 128 update from panel r0
+            panel(r1, 1);            // + the pending update of region r1's columns from panel r0
+            // K = 256 right of region r1, including region r0 + 2 itself (factored next, no update)
+            trailing(r0, 2, 2 * r1 + 2, kBig, 2 * r1 + 2);
+            if (r1 + 1 < Smax) region(r1 + 1, 0);
         }
     }
     for (int J = Kmax - 1; J >= 0; --J) {
@@ -297,6 +345,12 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_panel),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kTiledLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kTrail3Lds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing2),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kTrail2Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kTiledLds)) != hipSuccess) {
@@ -359,6 +413,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->bytes_per_snp = bps;
     p->kpad = round_up(pr->n_ref, gram::kKS);
     p->bed_len = pr->bed_len;
+    if (const char* e = getenv("DBSLMM_TRAIL_DMA")) p->trail_dma = atoi(e) != 0;
     p->n_s = pr->s_ptr[pr->num_block];
     p->n_l = has_l ? pr->l_ptr[pr->num_block] : 0;
 
@@ -601,8 +656,14 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
         switch (L.kind) {
         case 0: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, 0, 0, act, L.n); break;
         case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, L.step, L.nk, act, L.n); break;
-        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, act, L.items); break;
+        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, L.nk, act, L.items); break;
         case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, L.n, L.nk, act, L.items); break;
+        case 5:
+            if (p->trail_dma)
+                hipLaunchKernelGGL(dbslmm_tchol_trailing3, g, dim3(512), kTrail3Lds, st, ta, L.step, L.n, L.nk, act, L.items);
+            else
+                hipLaunchKernelGGL(dbslmm_tchol_trailing2, g, dim3(512), kTrail2Lds, st, ta, L.step, L.n, L.nk, act, L.items);
+            break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }
     }
