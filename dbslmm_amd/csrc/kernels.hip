@@ -173,7 +173,8 @@ struct GramTile { int32_t block, ti, tj, pad; };
 __device__ __forceinline__ void gram_tile32(
     const int8_t* __restrict__ G, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
     int r0, int c0, int lane, const double* __restrict__ S, const double* __restrict__ mu,
-    const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M,
+    int32_t ncopy, int64_t cstride) {
     const int8_t* pa = G + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kpad + 16 * (lane >> 5);
     const int8_t* pb = G + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kpad + 16 * (lane >> 5);
 
@@ -247,7 +248,7 @@ __device__ __forceinline__ void gram_tile32(
         }
         double v = scale * (c * rsd[si] * rj);
         if (li == lj) v += 1.0 - tau;
-        M[moff + static_cast<int64_t>(li) * ld + lj] = v;
+        for (int cp = 0; cp < ncopy; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
     }
 }
 
@@ -258,14 +259,15 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
     const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
-    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M,
+    int32_t ncopy, int64_t cstride) {
     const int lane = threadIdx.x & (kWave - 1);
     const int t = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (t >= n_tiles) return;
     const GramTile tile = tiles[t];
     const int b = tile.block;
     gram_tile32(G, kpad, blk_row0[b], blk_m[b], blk_ld[b], blk_matoff[b], (block_flags[b] & 1) != 0,
-                kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M);
+                kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -294,7 +296,8 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
-    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M,
+    int32_t ncopy, int64_t cstride) {
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t glds[];
     if (static_cast<int>(blockIdx.x) >= n_tiles) return;
@@ -312,7 +315,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
             const int r0 = kGT * tile.ti + 32 * si, c0 = kGT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
             gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
-                        tau, M);
+                        tau, M, ncopy, cstride);
         }
         return;
     }
@@ -404,7 +407,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
                 const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
                 double v = scale * (c * rsd[row0 + li] * rj);
                 if (li == lj) v += 1.0 - tau;
-                M[moff + static_cast<int64_t>(li) * ld + lj] = v;
+                for (int cp = 0; cp < ncopy; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
             }
         }
     }
@@ -441,7 +444,8 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
-    double n_ref_d, double pad_k, double tau, double* __restrict__ M) {
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M,
+    int32_t ncopy, int64_t cstride) {
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t hlds[];
     if (static_cast<int>(blockIdx.x) >= n_tiles) return;
@@ -459,7 +463,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             const int r0 = kHT * tile.ti + 32 * si, c0 = kHT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
             gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
-                        tau, M);
+                        tau, M, ncopy, cstride);
         }
         return;
     }
@@ -546,7 +550,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
                 const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
                 double v = scale * (c * rsd[row0 + li] * rj);
                 if (li == lj) v += 1.0 - tau;
-                M[moff + static_cast<int64_t>(li) * ld + lj] = v;
+                for (int cp = 0; cp < ncopy; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
             }
         }
     }

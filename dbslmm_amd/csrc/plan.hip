@@ -748,7 +748,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         hipLaunchKernelGGL(dbslmm_gram_i8, grid, dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
-                           static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M);
+                           static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M, n, p->M_elems);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_htiles > 0) {
@@ -756,7 +756,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_htiles, p->n_htiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M);
+                           p->tau, p->d_M, n, p->M_elems);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_btiles > 0) {
@@ -764,15 +764,12 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M);
+                           p->tau, p->d_M, n, p->M_elems);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (!front && n > 1)
         return (ctx->err = "a multi-copy run needs the Gram front", DBSLMM_E_STATE);
-    // the factorisation overwrites its matrix: copies 1.. of the Gram for the other sigmas
-    for (int c = 1; c < n && p->M_elems > 0; ++c)
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_M + c * p->M_elems, p->d_M, p->M_elems * sizeof(double),
-                                    hipMemcpyDeviceToDevice, s));
+    // (the factorisation overwrites its matrix: the Gram epilogues write all n copies)
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
     if (p->n_nonempty > 0) {
         for (int c = 0; c < n; ++c) {
