@@ -1,26 +1,23 @@
 // chol_tiled.hip -- multi-workgroup Cholesky + solves for the big LD blocks (included by plan.hip
 // after chol.hip).  Same bordered system as chol.hip (z appended as row m, y = L^{-1} z left in
 // row m, beta = L^{-T} y / sqrt n), but every block with m >= the tiled threshold is spread over
-// many workgroups, batched across blocks, one launch per phase of a 64-wide panel step:
+// many workgroups, batched across blocks, one launch per phase (schedule: build_tiled in plan.hip):
 //
-//   tchol_region(r)      factor + invert the 128 x 128 diagonal region r in LDS
-//   tchol_panel(k)       L_ik = A_ik X_kk^T for every tile row i > k     (one workgroup per tile)
-//   tchol_trailing(k)    C_ij -= L_ik L_jk^T, k < j <= i                 (one workgroup per tile)
-//                        -- the first workgroups take tile (k+1, k+1): update, then factor +
-//                           invert it (lookahead), overlapping the rest of the update
-//   tchol_backward(J)    x_J = X_JJ^T v_J, v_{<J} -= L_{J,<J}^T x_J        (one workgroup per
-//                        256 columns; x_J recomputed per workgroup, v_J is read-only in a launch)
+//   tchol_region        factor + invert a 128 x 128 diagonal region in LDS (+ pending updates)
+//   tchol_panel         L_i = A_i L_RR^{-T} per 64-row tile below the region (+ pending update)
+//   tchol_trailing2/3   C_IJ -= L_I L_J^T on 128 x 128 tiles, K = 128 x regions per super step
+//   tchol_backward(J)   x_J = X_JJ^T v_J, v_{<J} -= L_{J,<J}^T x_J        (one workgroup per
+//                       256 columns; x_J recomputed per workgroup, v_J is read-only in a launch)
 //
 // A 64 x 64 diagonal tile is factored as 2 x 2 tiles of 32 by chol::factor_diag:
 //   L00, X00 = L00^{-1};  L10 = A10 X00^T;  A11 -= L10 L10^T;  L11, X11;  X10 = -X11 L10 X00
 // and stored as: strict lower = L, diagonal + upper (r, c >= r) = X[c][r] (X = L_kk^{-1}).
 //
-// Work lists are per step: the blocks active at that step and the prefix of their work-item
-// counts; a workgroup finds its block by binary search (no per-item tables).
+// Work items of the region / panel / trailing launches are int32 pairs [block or tile,
+// (local step << 8) | count]: every block runs at its own step inside a shared launch.
 namespace chol {
 
 constexpr int kBT = 64;                          // tiled-path tile edge (half the panel width)
-constexpr int kJRun = 4;                         // trailing tiles per workgroup run
 constexpr int kSub = kT * kTS;                   // one 32x32 LDS sub-tile (stride 34)
 // LDS carve of the tiled kernels (doubles): 8 sub-tiles = two 64x64 operands
 constexpr int kTiledDoubles = 8 * kSub + 2 * kT + 8;
@@ -108,15 +105,10 @@ __device__ __forceinline__ void stage64(double* S, const double* A, int ld, int 
 
 }  // namespace chol
 
-// ---------------------------------------------------------------- 128-column outer steps
-// Outer step s covers tile columns k0 = 2s, k1 = 2s + 1 (columns c0 = 128 s ..).  Its 128 x 128
-// diagonal region is factored by dbslmm_tchol_region and holds, after it: strict lower = L,
-// each 64 x 64 diagonal tile's diagonal + upper (r, c >= r) = X[c][r] of its own inverse (what the
-// panel and the backward solve read).
-// panel(s):    L_i = A_i L_RR^{-T} for 64-row tiles i below the region (substitution over the
-//              region's two 64-column halves)
-// trailing(s): C_IJ -= L_{I,s} L_{J,s}^T with K = 128 (two 64-deep phases, C in registers)
-//              for the tile rows below region s+1.
+// ---------------------------------------------------------------- 128-column regions
+// Region r (columns c0 = 128 r ..) is factored by dbslmm_tchol_region and holds, after it: strict
+// lower = L, each 64 x 64 diagonal tile's diagonal + upper (r, c >= r) = X[c][r] of its own
+// inverse (what the panel and the backward solve read).
 namespace chol {
 
 // X block (64 x 64) in row-major form from the stored upper triangle: X[q][r] = A(rr0 + r,
@@ -275,50 +267,6 @@ __device__ __forceinline__ void lds_to_acc(v4d (&acc)[2][2], const double* W, in
 __device__ __forceinline__ int rsub(int a, int b) { return a * (a + 1) / 2 + b; }
 constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X10 (2) + colb
 
-// C(I, J..) -= L_{I,.} L_{J,.}^T over columns c0 .. c0 + 128 nk, K = 128 nk as 2 nk 64-deep
-// phases, over a run of tiles J0..J1 of tile row I (skips the strictly-upper quadrant of a
-// diagonal tile).  Next phase's operands and the next tile's C are prefetched into registers
-// while the current phase's MFMAs run.
-__device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int J1, int c0, int nk,
-                                           double* lds, int tid) {
-    const int lane = tid & 63, wave = tid >> 6, qi = wave >> 1, qj = wave & 1;
-    double* LI = lds;
-    double* LJ = lds + 4 * kSub;
-    double li[16], lj[16];
-    v4d acc[2][2], nxt[2][2];
-    const int P = 2 * nk;                       // phases per tile
-    const int nph = P * (J1 - J0 + 1);
-    tile_regs_load(li, A, ld, kBT * I, c0, tid);
-    if (I != J0) tile_regs_load(lj, A, ld, kBT * J0, c0, tid);
-    load_acc(acc, A, ld, kBT * I + kT * qi, kBT * J0 + kT * qj, lane);
-    for (int p = 0; p < nph; ++p) {
-        const int J = J0 + p / P;
-        tile_regs_store(li, LI, tid);
-        if (I != J) tile_regs_store(lj, LJ, tid);
-        __syncthreads();
-        if (p + 1 < nph) {
-            const int Jn = J0 + (p + 1) / P, kcn = (p + 1) % P;
-            tile_regs_load(li, A, ld, kBT * I, c0 + kBT * kcn, tid);
-            if (I != Jn) tile_regs_load(lj, A, ld, kBT * Jn, c0 + kBT * kcn, tid);
-            if (kcn == 0) load_acc(nxt, A, ld, kBT * I + kT * qi, kBT * Jn + kT * qj, lane);
-        }
-        const double* LJp = I == J ? LI : LJ;
-        const bool skip = I == J && qj > qi;
-        if (!skip) {
-            mfma_tile(acc, LI + (2 * qi) * kSub, LJp + (2 * qj) * kSub, -1.0, lane);
-            mfma_tile(acc, LI + (2 * qi + 1) * kSub, LJp + (2 * qj + 1) * kSub, -1.0, lane);
-        }
-        if (p % P == P - 1) {
-            if (!skip) store_acc(acc, A, ld, kBT * I + kT * qi, kBT * J + kT * qj, lane);
-#pragma unroll
-            for (int si = 0; si < 2; ++si)
-#pragma unroll
-                for (int sj = 0; sj < 2; ++sj) acc[si][sj] = nxt[si][sj];
-        }
-        __syncthreads();
-    }
-}
-
 }  // namespace chol
 
 // ---------------------------------------------------------------- kernels
@@ -332,12 +280,14 @@ __device__ __forceinline__ void update_run(double* A, int ld, int I, int J0, int
 // upper = its X^T (what the panel and the backward solve read).  Region 0 without update also
 // writes the z row and flags monomorphic SNPs.
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_region(
-    chol::TiledArgs a0, int32_t reg, int32_t update, const int32_t* __restrict__ blocks, int32_t n) {
+    chol::TiledArgs a0, const int32_t* __restrict__ blocks, int32_t n) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n) return;
     int b;
-    const TiledArgs a = a0.view(blocks[blockIdx.x], b);
+    const TiledArgs a = a0.view(blocks[2 * blockIdx.x], b);
+    const int32_t meta = blocks[2 * blockIdx.x + 1];
+    const int reg = meta >> 8, update = meta & 255;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b], ms = a.blk_ms[b];
     double* A = a.M + a.blk_matoff[b];
@@ -477,13 +427,15 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
 // panel of outer step s, one workgroup per 64-row tile i below region s (item (block << 16) |
 // (i << 8)): L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of
 // the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).  upd: first apply
-// the pending update of A_i from the panel of region s-1.
+// the pending update of A_i from the panels of regions s-upd .. s-1.
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_panel(
-    chol::TiledArgs a0, int32_t s, int32_t upd, const int32_t* __restrict__ items, int32_t n_items) {
+    chol::TiledArgs a0, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
-    const int32_t it = items[blockIdx.x];
+    const int32_t it = items[2 * blockIdx.x];
+    const int32_t meta = items[2 * blockIdx.x + 1];
+    const int s = meta >> 8, upd = meta & 255;
     const int i = (it >> 8) & 255;
     int b;
     const TiledArgs a = a0.view(it >> 16, b);
@@ -500,14 +452,14 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     v4d cc[2][2];
     v4d u0[2][2];
     if (upd) {
-        // pending K = 128 update from the panel of region s-1 (what a trailing launch of region
-        // s's columns would do): A_i -= L_{i,s-1} L_{R,s-1}^T, R = region s's 128 rows; wave
-        // (qi, qj) updates its quadrant of both 64-column halves, operands staged 32 columns
-        // at a time (sub-tiles 0-1: rows of tile i, 2-5: rows of the region)
-        const int cp = c0 - 2 * kBT;
+        // pending K = 128 upd update from the panels of regions s-upd .. s-1 (what a trailing
+        // launch of region s's columns would do): A_i -= L_{i,.} L_{R,.}^T, R = region s's 128
+        // rows; wave (qi, qj) updates its quadrant of both 64-column halves, operands staged 32
+        // columns at a time (sub-tiles 0-1: rows of tile i, 2-5: rows of the region)
+        const int cp = c0 - 2 * kBT * upd;
         load_acc(u0, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);
         if (two) load_acc(cc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);
-        for (int kc = 0; kc < 4; ++kc) {
+        for (int kc = 0; kc < 4 * upd; ++kc) {
             for (int q = wave; q < 6; q += 4)
                 stage_tile(lds + q * kSub, A, ld, q < 2 ? kBT * i + kT * q : c0 + kT * (q - 2), cp + kT * kc, lane);
             __syncthreads();
@@ -544,29 +496,6 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     zero_acc(acc);
     for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
     store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);     // L_i1
-}
-
-// trailing update with the panels of regions s .. s+nk-1 (K = 128 nk).  Items (block << 16) |
-// (I << 8) | J0, -1 = padding: a run of
-// tiles (I, J0 .. J0 + run - 1) (clipped to the lower triangle; run = kJRun while the step has
-// plenty of tiles, 1 in the short tail steps), for tile rows below region
-// s+1 (which dbslmm_tchol_region updates and factors itself); per-XCD queues (item e runs on
-// XCD e % 8; the runs of one tile row I of a block share an XCD, so L_I is served by its L2).
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_trailing(
-    chol::TiledArgs a0, int32_t s, int32_t run, int32_t nk, const int32_t* __restrict__ items,
-    int32_t n_items) {
-    using namespace chol;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    if (static_cast<int>(blockIdx.x) >= n_items) return;
-    const int32_t it = items[blockIdx.x];
-    if (it < 0) return;
-    const int I = (it >> 8) & 255, J0 = it & 255;
-    int b;
-    const TiledArgs a = a0.view(it >> 16, b);
-    const int m = a.blk_m[b], ld = a.blk_ld[b];
-    const int T = (m + kBT - 1) / kBT;
-    double* A = a.M + a.blk_matoff[b];
-    update_run(A, ld, I, J0, min(J0 + run - 1, min(I, T - 1)), 2 * kBT * s, nk, lds, threadIdx.x);
 }
 
 // ---------------------------------------------------------------- 128 x 128 trailing update
@@ -651,13 +580,14 @@ __device__ __forceinline__ void t2_mfma_stage(v4d (&acc)[4][2], const double* S,
 }  // namespace chol
 
 extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing2(
-    chol::TiledArgs a0, int32_t s, int32_t run, int32_t nk, const int32_t* __restrict__ items,
-    int32_t n_items) {
+    chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
-    const int32_t it = items[blockIdx.x];
+    const int32_t it = items[2 * blockIdx.x];
     if (it < 0) return;
+    const int32_t meta = items[2 * blockIdx.x + 1];
+    const int s = meta >> 8, nk = meta & 255;
     const int I = (it >> 8) & 255, J0 = it & 255;
     int b;
     const TiledArgs a = a0.view(it >> 16, b);
@@ -772,13 +702,14 @@ __device__ __forceinline__ void t3_mfma_stage(v4d (&acc)[4][2], const double* SA
 }  // namespace chol
 
 extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
-    chol::TiledArgs a0, int32_t s, int32_t run, int32_t nk, const int32_t* __restrict__ items,
-    int32_t n_items) {
+    chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     if (static_cast<int>(blockIdx.x) >= n_items) return;
-    const int32_t it = items[blockIdx.x];
+    const int32_t it = items[2 * blockIdx.x];
     if (it < 0) return;
+    const int32_t meta = items[2 * blockIdx.x + 1];
+    const int s = meta >> 8, nk = meta & 255;
     const int I = (it >> 8) & 255, J0 = it & 255;
     int b;
     const TiledArgs a = a0.view(it >> 16, b);

@@ -47,8 +47,8 @@ constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
-    int kind;         // 0 region 0, 1 panel, 2 trailing, 3 backward, 4 region `step` with update,
-                      // 5 trailing on 128 x 128 tiles
+    int kind;         // 1 panel, 3 backward, 4 region, 5 trailing (128 x 128 tiles); items of
+                      // kinds 1/4/5 are int32 pairs carrying each block's own step
     int step;
     int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
     int32_t n;
@@ -149,166 +149,160 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
     return e;
 }
 
-// Launch list of the tiled sequence: region 0, then super steps of 256 columns, then the backward
-// steps, for the blocks `tb` (plan block indices), each replicated over `copies` independent
-// factorisations (h2f tuning: item block id bq = b + c * nb addresses copy c of the matrices).
-//   super step (regions r0 = 2S, r1 = 2S + 1; 64-tile columns 4S .. 4S+3):
-//   panel(r0) -> region(r1) [+ pending K = 128 update from panel r0] ->
-//   panel(r1) [+ pending K = 128 update of its rows' region-r1 columns from panel r0] ->
-//   trailing K = 256 of everything right of region r1, region r0 + 2 included (panels r0, r1) ->
-//   region(r0 + 2).  Each C tile below is read and written once per 256 columns; the chain of
-//   dependent launches is 5 per 256 columns.
+// Launch list of the tiled sequence for the blocks `tb0` (plan block indices), each replicated over
+// `copies` independent factorisations (h2f tuning: item block id bq = b + c * nb addresses copy c).
+// A block's factorisation is a chain of super steps of R regions (128 columns each; R = 2, env
+// DBSLMM_SUPER): region(0), then per super step
+//   panel(r0) -> for r = r0+1 .. r0+R-1: region(r) [+ its pending update from panels r0 .. r-1]
+//   -> panel(r) [+ the pending update of its rows' region-r columns] -> trailing K = 128 R of
+//   everything right of the super step (the next first region included) -> region(r0 + R),
+// then the backward steps (64-row tiles, descending).  Every launch of a given slot holds the
+// same kind of work for all blocks, each at its OWN local step (work items carry it): blocks are
+// left-aligned (all start at launch 0); env DBSLMM_ALIGN=1 right-aligns them (a block with fewer
+// super steps starts later, so its heavy first steps overlap the largest block's latency-bound
+// last steps -- no gain measured at configs 3-5).  Each work item is two int32:
+// [block / tile, (local step << 8) | pending panels or K multiple].
 static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
                         int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
-    // trailing updates on 128 x 128 tiles (dbslmm_tchol_trailing2) unless DBSLMM_TRAIL64=1
-    const char* t64 = getenv("DBSLMM_TRAIL64");
-    const bool t128 = !(t64 && atoi(t64) != 0);
-    std::vector<std::pair<int32_t, int32_t>> tb;   // (plan block, item block id)
+    struct Blk { int32_t bq; int T64, Tz64, T2, Tz2, nr, S, off; };
+    int R = 2;
+    if (const char* e = getenv("DBSLMM_SUPER")) R = std::max(1, std::min(8, atoi(e)));
+    bool right = false;     // measured: no gain at configs 3-5 (the sequence is throughput-bound)
+    if (const char* e = getenv("DBSLMM_ALIGN")) right = atoi(e) != 0;
+    int run2 = chol::kRun2;
+    if (const char* e = getenv("DBSLMM_RUN2")) run2 = std::max(1, atoi(e));
+    std::vector<Blk> bl;
+    int G = 0, Kmax = 0;
     for (int c = 0; c < copies; ++c)
-        for (int32_t b : tb0) tb.push_back({b, b + c * nb});
-    int Kmax = 0;
-    for (const auto& e : tb) Kmax = std::max<int>(Kmax, (mv[e.first] + chol::kBT - 1) / chol::kBT);
-    auto add = [&](int kind, int step, const std::vector<int32_t>& act, const std::vector<int32_t>& cnt,
-                   int extra) {
+        for (int32_t b : tb0) {
+            Blk k;
+            k.bq = b + c * nb;
+            k.T64 = (mv[b] + chol::kBT - 1) / chol::kBT;
+            k.Tz64 = mv[b] / chol::kBT;
+            k.T2 = (mv[b] + 127) / 128;
+            k.Tz2 = mv[b] / 128;
+            k.nr = (k.T64 + 1) / 2;
+            k.S = (k.nr + R - 1) / R;
+            G = std::max(G, k.S);
+            Kmax = std::max(Kmax, k.T64);
+            bl.push_back(k);
+        }
+    for (auto& k : bl) k.off = right ? G - k.S : 0;
+    auto push_pairs = [&](int kind, const std::vector<int32_t>& v) {   // plain pair list
+        if (v.empty()) return;
+        TLaunch L{kind, 0, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(v.size() / 2),
+                  static_cast<int32_t>(v.size() / 2)};
+        tlist.insert(tlist.end(), v.begin(), v.end());
+        tl.push_back(L);
+    };
+    auto region_launch = [&](const std::vector<int32_t>& v) { push_pairs(4, v); };
+    auto panel_launch = [&](const std::vector<int32_t>& v) { push_pairs(1, v); };
+    auto trailing_launch = [&](std::vector<std::vector<int32_t>>& q, int run) {
+        TLaunch L{5, 0, static_cast<int32_t>(tlist.size()), run, 0};
+        size_t qmax = 0;
+        for (const auto& v : q) qmax = std::max(qmax, v.size() / 2);
+        // work item e (pair) runs on XCD e % 8
+        for (size_t i = 0; i < qmax; ++i)
+            for (int x = 0; x < kXcd; ++x) {
+                if (2 * i < q[x].size()) {
+                    tlist.push_back(q[x][2 * i]);
+                    tlist.push_back(q[x][2 * i + 1]);
+                } else {
+                    tlist.push_back(-1);
+                    tlist.push_back(0);
+                }
+            }
+        L.items = static_cast<int32_t>((tlist.size() - L.off) / 2);
+        if (L.items > 0) tl.push_back(L);
+    };
+    {   // region 0 of the blocks that start at super step 0
+        std::vector<int32_t> v;
+        for (const auto& k : bl)
+            if (k.off == 0) { v.push_back(k.bq); v.push_back(0); }
+        region_launch(v);
+    }
+    for (int g = 0; g < G; ++g) {
+        auto active = [&](const Blk& k) { return g >= k.off && g - k.off < k.S; };
+        std::vector<int32_t> v;
+        for (const auto& k : bl)      // panel(r0)
+            if (active(k)) {
+                const int r0 = (g - k.off) * R;
+                for (int i = 2 * r0 + 2; i <= k.Tz64; ++i) { v.push_back((k.bq << 16) | (i << 8)); v.push_back(r0 << 8); }
+            }
+        panel_launch(v);
+        for (int j = 1; j < R; ++j) {
+            std::vector<int32_t> rv, pv;
+            for (const auto& k : bl)
+                if (active(k)) {
+                    const int r = (g - k.off) * R + j;
+                    if (r >= k.nr) continue;
+                    rv.push_back(k.bq);
+                    rv.push_back((r << 8) | j);
+                    for (int i = 2 * r + 2; i <= k.Tz64; ++i) { pv.push_back((k.bq << 16) | (i << 8)); pv.push_back((r << 8) | j); }
+                }
+            region_launch(rv);
+            panel_launch(pv);
+        }
+        {   // trailing: 128 x 128 tiles right of the super step, LPT over per-XCD queues by tile row
+            std::vector<std::vector<int32_t>> q(kXcd);
+            std::vector<int64_t> load(kXcd, 0);
+            int64_t ntiles = 0;
+            for (const auto& k : bl)
+                if (active(k)) {
+                    const int r0 = (g - k.off) * R, rl = std::min(r0 + R, k.nr) - 1;
+                    if (rl + 1 >= k.nr) continue;
+                    for (int I = rl + 1; I <= k.Tz2; ++I) ntiles += std::min(I, k.T2 - 1) - rl;
+                }
+            const int run = ntiles >= 1024 ? run2 : 1;
+            for (const auto& k : bl)
+                if (active(k)) {
+                    const int r0 = (g - k.off) * R, rl = std::min(r0 + R, k.nr) - 1;
+                    if (rl + 1 >= k.nr) continue;
+                    const int meta = (r0 << 8) | (rl - r0 + 1);
+                    for (int I = rl + 1; I <= k.Tz2; ++I) {
+                        const int jmax = std::min(I, k.T2 - 1);
+                        const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+                        for (int J = rl + 1; J <= jmax; J += run) {
+                            q[x].push_back((k.bq << 16) | (I << 8) | J);
+                            q[x].push_back(meta);
+                        }
+                        load[x] += jmax - rl;
+                    }
+                }
+            trailing_launch(q, run);
+        }
+        {   // next super step's first region; region 0 of the blocks that start at g + 1
+            std::vector<int32_t> v;
+            for (const auto& k : bl) {
+                if (active(k)) {
+                    const int r0 = (g - k.off) * R, rn = r0 + R;
+                    if (rn < k.nr) { v.push_back(k.bq); v.push_back(rn << 8); }
+                } else if (k.off == g + 1) {
+                    v.push_back(k.bq);
+                    v.push_back(0);
+                }
+            }
+            region_launch(v);
+        }
+    }
+    auto add = [&](int kind, int step, const std::vector<int32_t>& act, const std::vector<int32_t>& cnt) {
         if (act.empty()) return;
         TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(act.size()), 0};
         tlist.insert(tlist.end(), act.begin(), act.end());
         int32_t acc = 0;
         tlist.push_back(0);
         for (int32_t c : cnt) tlist.push_back(acc += c);
-        L.items = acc + extra;
+        L.items = acc;
         tl.push_back(L);
     };
-    if (!tb.empty()) {
-        TLaunch L{0, 0, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(tb.size()),
-                  static_cast<int32_t>(tb.size())};
-        for (const auto& e : tb) tlist.push_back(e.second);
-        tl.push_back(L);
-    }
-    auto add_items = [&](int kind, int step, std::vector<std::vector<int32_t>>& q) {
-        TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), 0, 0};
-        size_t qmax = 0;
-        for (const auto& v : q) qmax = std::max(qmax, v.size());
-        // item e runs on XCD e % 8 (L.off is kept a multiple of 8 by the padding below)
-        while ((tlist.size() - L.off) % kXcd) tlist.push_back(-1);
-        for (size_t i = 0; i < qmax; ++i)
-            for (int x = 0; x < kXcd; ++x) tlist.push_back(i < q[x].size() ? q[x][i] : -1);
-        L.items = static_cast<int32_t>(tlist.size() - L.off);
-        if (L.items > 0) tl.push_back(L);
-        return L.items > 0;
-    };
-    const int Smax = (Kmax + 1) / 2;             // 128-column regions
-    auto trailing2 = [&](int r, int nk, int Jlo, int Jhi_rel, int Ilo) {
-        // the same tile set in 128 x 128 tiles (Jlo, Ilo, Jhi_rel + 1 even in 64-tile units)
-        std::vector<std::vector<int32_t>> q(kXcd);
-        std::vector<int64_t> load(kXcd, 0);
-        const int jl = Jlo / 2, il = Ilo / 2, jh = (Jhi_rel + 1) / 2 - 1;
-        int64_t ntiles = 0;
-        for (const auto& e : tb) {
-            const int T = (mv[e.first] + 127) / 128, Tz = mv[e.first] / 128;
-            for (int I = il; I <= Tz; ++I) ntiles += std::max(0, std::min({I, T - 1, jl + jh}) - jl + 1);
-        }
-        int run2 = chol::kRun2;
-        if (const char* e = getenv("DBSLMM_RUN2")) run2 = std::max(1, atoi(e));
-        const int run = std::min(ntiles >= 1024 ? run2 : 1, jh + 1);
-        for (const auto& e : tb) {
-            const int T = (mv[e.first] + 127) / 128, Tz = mv[e.first] / 128;
-            for (int I = il; I <= Tz; ++I) {
-                const int jmax = std::min({I, T - 1, jl + jh});
-                if (jmax < jl) continue;
-                const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                for (int J = jl; J <= jmax; J += run) q[x].push_back((e.second << 16) | (I << 8) | J);
-                load[x] += jmax - jl + 1;
-            }
-        }
-        // within an XCD, walk each block's rows in windows of 8 tile columns: the workgroups in
-        // flight on the XCD then share both their L_I and their L_J strips in its L2
-        if (const char* e = getenv("DBSLMM_TRAIL_ORDER"); !(e && atoi(e) == 0))
-            for (auto& v : q)
-                std::stable_sort(v.begin(), v.end(), [](int32_t u, int32_t w) {
-                    const int bu = u >> 16, bw = w >> 16;
-                    if (bu != bw) return bu < bw;
-                    const int ju = (u & 255) >> 3, jw = (w & 255) >> 3;
-                    if (ju != jw) return ju < jw;
-                    return (u & 0xffff) < (w & 0xffff);
-                });
-        if (add_items(5, r, q)) {
-            tl.back().n = run;
-            tl.back().nk = nk;
-        }
-    };
-    auto trailing = [&](int r, int nk, int Jlo, int Jhi_rel, int Ilo) {
-        // tiles (I >= Ilo, Jlo <= J <= min(I, T-1, Jlo + Jhi_rel)), K = 128 nk from region r
-        if (t128) return trailing2(r, nk, Jlo, Jhi_rel, Ilo);
-        std::vector<std::vector<int32_t>> q(kXcd);
-        std::vector<int64_t> load(kXcd, 0);
-        int64_t ntiles = 0;
-        for (const auto& e : tb) {
-            const int T = (mv[e.first] + chol::kBT - 1) / chol::kBT, Tz = mv[e.first] / chol::kBT;
-            for (int I = Ilo; I <= Tz; ++I) ntiles += std::max(0, std::min({I, T - 1, Jlo + Jhi_rel}) - Jlo + 1);
-        }
-        // a run never crosses Jlo + Jhi_rel (the kernel clips runs only at min(I, T-1))
-        const int run = std::min(ntiles >= 4096 ? chol::kJRun : 1, Jhi_rel + 1);
-        for (const auto& e : tb) {
-            const int T = (mv[e.first] + chol::kBT - 1) / chol::kBT, Tz = mv[e.first] / chol::kBT;
-            for (int I = Ilo; I <= Tz; ++I) {
-                const int jmax = std::min({I, T - 1, Jlo + Jhi_rel});
-                if (jmax < Jlo) continue;
-                const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                for (int J = Jlo; J <= jmax; J += run) q[x].push_back((e.second << 16) | (I << 8) | J);
-                load[x] += jmax - Jlo + 1;
-            }
-        }
-        if (add_items(2, r, q)) {
-            tl.back().n = run;
-            tl.back().nk = nk;
-        }
-    };
-    auto panel = [&](int r, int upd) {
-        std::vector<int32_t> items;
-        for (const auto& e : tb) {
-            const int Tz = mv[e.first] / chol::kBT;
-            for (int i = 2 * r + 2; i <= Tz; ++i) items.push_back((e.second << 16) | (i << 8));
-        }
-        if (items.empty()) return;
-        TLaunch L{1, r, static_cast<int32_t>(tlist.size()), 0, static_cast<int32_t>(items.size())};
-        L.nk = upd;
-        tlist.insert(tlist.end(), items.begin(), items.end());
-        tl.push_back(L);
-    };
-    auto region = [&](int r, int nk) {   // region r of every block that has it, nk pending panels
-        std::vector<int32_t> regs;
-        for (const auto& e : tb)
-            if (2 * r <= (mv[e.first] + chol::kBT - 1) / chol::kBT - 1) regs.push_back(e.second);
-        if (regs.empty()) return;
-        TLaunch L{4, r, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(regs.size()),
-                  static_cast<int32_t>(regs.size())};
-        L.nk = nk;
-        tlist.insert(tlist.end(), regs.begin(), regs.end());
-        tl.push_back(L);
-    };
-    constexpr int kBig = 1 << 20;
-    for (int r0 = 0; r0 < Smax; r0 += 2) {
-        const int r1 = r0 + 1;
-        panel(r0, 0);
-        if (r1 < Smax) {
-            region(r1, 1);           // + its pending K = 128 update from panel r0
-            panel(r1, 1);            // + the pending update of region r1's columns from panel r0
-            // K = 256 right of region r1, including region r0 + 2 itself (factored next, no update)
-            trailing(r0, 2, 2 * r1 + 2, kBig, 2 * r1 + 2);
-            if (r1 + 1 < Smax) region(r1 + 1, 0);
-        }
-    }
     for (int J = Kmax - 1; J >= 0; --J) {
         std::vector<int32_t> ba, bc;
-        for (const auto& e : tb) {
-            const int T = (mv[e.first] + chol::kBT - 1) / chol::kBT;
-            if (T > J) {
-                ba.push_back(e.second);
+        for (const auto& k : bl)
+            if (k.T64 > J) {
+                ba.push_back(k.bq);
                 bc.push_back(std::max(1, (chol::kBT * J + chol::kLargeThreads - 1) / chol::kLargeThreads));
             }
-        }
-        add(3, J, ba, bc, 0);
+        add(3, J, ba, bc);
     }
 }
 
@@ -350,10 +344,7 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                             static_cast<int>(kTrail3Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing2),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTrail2Lds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTiledLds)) != hipSuccess) {
+                            static_cast<int>(kTrail2Lds)) != hipSuccess) {
         dbslmm_ctx_destroy(c);
         return DBSLMM_E_HIP;
     }
@@ -654,15 +645,13 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
         const int32_t* pfx = act + L.n;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
         switch (L.kind) {
-        case 0: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, 0, 0, act, L.n); break;
-        case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, L.step, L.nk, act, L.n); break;
-        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, L.step, L.nk, act, L.items); break;
-        case 2: hipLaunchKernelGGL(dbslmm_tchol_trailing, g, blk, kTiledLds, st, ta, L.step, L.n, L.nk, act, L.items); break;
+        case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, act, L.items); break;
+        case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, act, L.items); break;
         case 5:
             if (p->trail_dma)
-                hipLaunchKernelGGL(dbslmm_tchol_trailing3, g, dim3(512), kTrail3Lds, st, ta, L.step, L.n, L.nk, act, L.items);
+                hipLaunchKernelGGL(dbslmm_tchol_trailing3, g, dim3(512), kTrail3Lds, st, ta, L.n, act, L.items);
             else
-                hipLaunchKernelGGL(dbslmm_tchol_trailing2, g, dim3(512), kTrail2Lds, st, ta, L.step, L.n, L.nk, act, L.items);
+                hipLaunchKernelGGL(dbslmm_tchol_trailing2, g, dim3(512), kTrail2Lds, st, ta, L.n, act, L.items);
             break;
         default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
         }

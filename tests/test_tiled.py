@@ -163,3 +163,18 @@ def test_run_multi_merged_copies_bit_identical(monkeypatch, tiled_min):
     plan.set_sigma(sig[0])
     plan.run()
     np.testing.assert_array_equal(plan.download()[0], multi[0][0])
+
+
+@pytest.mark.parametrize("R", ["1", "3", "4"])
+def test_super_step_sizes_match_oracle(monkeypatch, R):
+    """Super steps of R regions (K = 128 R trailing updates, pending updates of up to R-1 panels
+    inside the region and panel kernels) give the same beta as the oracle and as R = 2."""
+    monkeypatch.setenv("DBSLMM_SUPER", R)
+    prob = _problem(seed=9)
+    ref, _ = _oracle(prob)
+    got, st = _solve(prob, 64, monkeypatch)
+    monkeypatch.setenv("DBSLMM_SUPER", "2")
+    two, _ = _solve(prob, 64, monkeypatch)
+    assert np.all(st == 0)
+    assert normwise(got, ref) < 1e-10
+    assert normwise(got, two) < 1e-11

@@ -23,6 +23,7 @@ int main(int argc, char** argv) {
         const int jmax = std::min(I, T2 - 1);
         for (int J = jl; J <= jmax; J += run) {
             items.push_back((0 << 16) | (I << 8) | J);
+            items.push_back(nk);                           // (step 0 << 8) | nk
             for (int j = J; j <= std::min(J + run - 1, jmax); ++j) flops += 2.0 * 128 * 128 * 128 * nk * (j == I ? 0.75 : 1.0);
         }
     }
@@ -54,20 +55,20 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     for (int k = 0; k < 2; ++k) {
         for (int w = 0; w < 2; ++w)
-            if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size()), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, 0, run, nk, d_items, (int)items.size());
-            else hipLaunchKernelGGL(dbslmm_tchol_trailing2, dim3(items.size()), dim3(512), sizeof(double) * chol::kTrail2Doubles, 0, ta, 0, run, nk, d_items, (int)items.size());
+            if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, (int)items.size() / 2);
+            else hipLaunchKernelGGL(dbslmm_tchol_trailing2, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail2Doubles, 0, ta, run, d_items, (int)items.size() / 2);
         CK(hipEventRecord(e0));
         const int reps = 5;
         for (int r = 0; r < reps; ++r)
-            if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size()), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, 0, run, nk, d_items, (int)items.size());
-            else hipLaunchKernelGGL(dbslmm_tchol_trailing2, dim3(items.size()), dim3(512), sizeof(double) * chol::kTrail2Doubles, 0, ta, 0, run, nk, d_items, (int)items.size());
+            if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, (int)items.size() / 2);
+            else hipLaunchKernelGGL(dbslmm_tchol_trailing2, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail2Doubles, 0, ta, run, d_items, (int)items.size() / 2);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
         printf("%s m=%d nk=%d run=%d items=%zu  %.3f ms  %.1f TF/s (%.1f%% of 78.6)\n", k ? "trailing3(dma)" : "trailing2(regs)",
-               m, nk, run, items.size(), ms, flops / ms * 1e-9, flops / ms * 1e-9 / 78.6 * 100);
+               m, nk, run, items.size() / 2, ms, flops / ms * 1e-9, flops / ms * 1e-9 / 78.6 * 100);
     }
     return 0;
 }
