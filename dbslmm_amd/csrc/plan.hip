@@ -418,6 +418,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     // the 256-tile kernel pays once its K loop outweighs its 512 KB fp64 epilogue per tile
     int64_t gram_huge_min = p->kpad >= 4096 ? kGramHugeMinDefault : 2 * kGramHugeMinDefault;
     if (const char* env = getenv("DBSLMM_GRAM_HUGE_MIN")) gram_huge_min = std::max<int64_t>(1, atoll(env));
+    int gram_sq = 4;                   // 2D tile squares per XCD for the 256-tile Gram (env)
+    if (const char* env = getenv("DBSLMM_GRAM_SQ")) gram_sq = std::max(1, atoi(env));
     std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd);
     std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0);
     int64_t moff = 0;
@@ -470,12 +472,26 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             slot_out.push_back(INT32_MIN);
             z.push_back(0.0);
         }
-        if (m >= gram_huge_min) {   // 256 x 256 tiles; each tile row on the least-loaded XCD
+        if (m >= gram_huge_min) {   // 256 x 256 tiles
             const int T = static_cast<int>((m + gram::kHT - 1) / gram::kHT);
-            for (int ti = 0; ti < T; ++ti) {
-                const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
-                for (int tj = 0; tj <= ti; ++tj) hq[x].push_back({nb, ti, tj, 0});
-                hload[x] += ti + 1;
+            if (gram_sq > 1) {
+                // squares of gram_sq x gram_sq tiles (lower triangle), each on the least-loaded
+                // XCD: the workgroups in flight on an XCD share gram_sq row panels of each operand
+                for (int si = 0; si < T; si += gram_sq)
+                    for (int sj = 0; sj <= si; sj += gram_sq) {
+                        const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
+                        for (int ti = si; ti < std::min(T, si + gram_sq); ++ti)
+                            for (int tj = sj; tj < std::min(ti + 1, sj + gram_sq); ++tj) {
+                                hq[x].push_back({nb, ti, tj, 0});
+                                hload[x] += 1;
+                            }
+                    }
+            } else {                 // each tile row on the least-loaded XCD
+                for (int ti = 0; ti < T; ++ti) {
+                    const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
+                    for (int tj = 0; tj <= ti; ++tj) hq[x].push_back({nb, ti, tj, 0});
+                    hload[x] += ti + 1;
+                }
             }
             ops_exec += 2.0 * p->kpad * gram::kHT * gram::kHT * (T * (T + 1) / 2);
         } else if (m >= gram_big_min) {   // 128 x 128 tiles, the block's queue on the least-loaded XCD
