@@ -54,7 +54,11 @@ struct TLaunch {
     int32_t n;
     int32_t items;    // workgroups
     int32_t nk = 1;   // trailing: K = 128 nk (regions step .. step+nk-1); region: pending panels
+    int strm = 0;     // 0: the chain stream (stream2), 1: the bulk-trailing stream (stream3)
 };
+// sync entries of a launch list (lookahead): kind 6 records tiled event `step` on stream `strm`,
+// kind 7 makes stream `strm` wait for it
+constexpr int kTlRecord = 6, kTlWait = 7;
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 }  // namespace
@@ -63,6 +67,7 @@ struct dbslmm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // main stream (unpack, gram, large-block Cholesky)
     hipStream_t stream2 = nullptr;   // tiled (multi-workgroup) Cholesky sequence, forked/joined
+    hipStream_t stream3 = nullptr;   // its bulk trailing updates (lookahead), forked/joined
     hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
     std::string err;
 };
@@ -117,6 +122,7 @@ struct dbslmm_plan {
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;  // kEvPerRun per run
+    std::vector<hipEvent_t> tev; // dependencies between the tiled sequence's two streams
     int runs_pending = 0;
     double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0, 0};
     int32_t ms_runs = 0;
@@ -171,6 +177,8 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
     if (const char* e = getenv("DBSLMM_ALIGN")) right = atoi(e) != 0;
     int run2 = chol::kRun2;
     if (const char* e = getenv("DBSLMM_RUN2")) run2 = std::max(1, atoi(e));
+    bool lookahead = true;  // env DBSLMM_LOOKAHEAD=0: one trailing launch per super step, one stream
+    if (const char* e = getenv("DBSLMM_LOOKAHEAD")) lookahead = atoi(e) != 0;
     std::vector<Blk> bl;
     int G = 0, Kmax = 0;
     for (int c = 0; c < copies; ++c)
@@ -197,8 +205,14 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
     };
     auto region_launch = [&](const std::vector<int32_t>& v) { push_pairs(4, v); };
     auto panel_launch = [&](const std::vector<int32_t>& v) { push_pairs(1, v); };
-    auto trailing_launch = [&](std::vector<std::vector<int32_t>>& q, int run) {
+    auto sync = [&](int kind, int ev, int strm) {
+        TLaunch L{kind, ev, 0, 0, 0};
+        L.strm = strm;
+        tl.push_back(L);
+    };
+    auto trailing_launch = [&](std::vector<std::vector<int32_t>>& q, int run, int strm) {
         TLaunch L{5, 0, static_cast<int32_t>(tlist.size()), run, 0};
+        L.strm = strm;
         size_t qmax = 0;
         for (const auto& v : q) qmax = std::max(qmax, v.size() / 2);
         // work item e (pair) runs on XCD e % 8
@@ -243,7 +257,9 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             region_launch(rv);
             panel_launch(pv);
         }
-        {   // trailing: 128 x 128 tiles right of the super step, LPT over per-XCD queues by tile row
+        // trailing: 128 x 128 tiles (I, J) right of the super step, rl + jlo <= J <= rl + jhi, LPT
+        // over per-XCD queues by tile row
+        auto trailing = [&](int jlo, int jhi, int strm, int run_force) {
             std::vector<std::vector<int32_t>> q(kXcd);
             std::vector<int64_t> load(kXcd, 0);
             int64_t ntiles = 0;
@@ -251,25 +267,42 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
                 if (active(k)) {
                     const int r0 = (g - k.off) * R, rl = std::min(r0 + R, k.nr) - 1;
                     if (rl + 1 >= k.nr) continue;
-                    for (int I = rl + 1; I <= k.Tz2; ++I) ntiles += std::min(I, k.T2 - 1) - rl;
+                    for (int I = rl + jlo; I <= k.Tz2; ++I) {
+                        const int jm = std::min(std::min(I, k.T2 - 1), rl + jhi);
+                        if (jm >= rl + jlo) ntiles += jm - (rl + jlo) + 1;
+                    }
                 }
-            const int run = ntiles >= 1024 ? run2 : 1;
+            const int run = run_force ? run_force : (ntiles >= 1024 ? run2 : 1);
             for (const auto& k : bl)
                 if (active(k)) {
                     const int r0 = (g - k.off) * R, rl = std::min(r0 + R, k.nr) - 1;
                     if (rl + 1 >= k.nr) continue;
                     const int meta = (r0 << 8) | (rl - r0 + 1);
-                    for (int I = rl + 1; I <= k.Tz2; ++I) {
-                        const int jmax = std::min(I, k.T2 - 1);
+                    for (int I = rl + jlo; I <= k.Tz2; ++I) {
+                        const int jm = std::min(std::min(I, k.T2 - 1), rl + jhi);
+                        if (jm < rl + jlo) continue;
                         const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                        for (int J = rl + 1; J <= jmax; J += run) {
+                        for (int J = rl + jlo; J <= jm; J += run) {
                             q[x].push_back((k.bq << 16) | (I << 8) | J);
                             q[x].push_back(meta);
                         }
-                        load[x] += jmax - rl;
+                        load[x] += jm - (rl + jlo) + 1;
                     }
                 }
-            trailing_launch(q, run);
+            trailing_launch(q, run, strm);
+        };
+        if (lookahead) {
+            // the next super step's R tile columns ("near": chain stream, one tile per work item)
+            // are updated first; the rest ("far": stream 1) overlaps the next super step's
+            // regions and panels.  Tiles of near(g) were far(g-1)'s.
+            sync(kTlRecord, 2 * g, 0);
+            if (g > 0) sync(kTlWait, 2 * g - 1, 0);
+            trailing(1, R, 0, 1);
+            sync(kTlWait, 2 * g, 1);
+            trailing(R + 1, 1 << 20, 1, 0);
+            sync(kTlRecord, 2 * g + 1, 1);
+        } else {
+            trailing(1, 1 << 20, 0, 0);
         }
         {   // next super step's first region; region 0 of the blocks that start at g + 1
             std::vector<int32_t> v;
@@ -295,6 +328,7 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
         L.items = acc;
         tl.push_back(L);
     };
+    if (lookahead && G > 0) sync(kTlWait, 2 * G - 1, 0);   // the last far update
     for (int J = Kmax - 1; J >= 0; --J) {
         std::vector<int32_t> ba, bc;
         for (const auto& k : bl)
@@ -323,6 +357,7 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
@@ -357,6 +392,7 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->join3) (void)hipEventDestroy(ctx->join3);
@@ -376,6 +412,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : p->tev) (void)hipEventDestroy(e);
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
     if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
     delete p;
@@ -566,7 +603,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[9] = p->n_large;
     p->wl[10] = chol_flops_tiled;
     p->wl[11] = p->n_tiled;
-    p->wl[12] = static_cast<double>(p->tl.size());
+    p->wl[12] = static_cast<double>(std::count_if(p->tl.begin(), p->tl.end(),
+                                                  [](const TLaunch& L) { return L.kind < kTlRecord; }));
 
     // ---- device allocations
     hipError_t e = hipSetDevice(ctx->device);
@@ -654,8 +692,18 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
                              p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, p->d_dshift, isn,
                              p->d_y, p->d_beta_s, p->d_beta_l, p->d_status, p->n_nonempty,
                              p->M_elems, p->n_slots, p->n_s, p->n_l, p->nbk};
-    hipStream_t st = ctx->stream2;
+    int nev = 0;
+    for (const TLaunch& L : tl)
+        if (L.kind == kTlRecord) nev = std::max(nev, L.step + 1);
+    while (static_cast<int>(p->tev.size()) < nev) {
+        hipEvent_t e;
+        HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        p->tev.push_back(e);
+    }
     for (const TLaunch& L : tl) {
+        hipStream_t st = L.strm ? ctx->stream3 : ctx->stream2;
+        if (L.kind == kTlRecord) { HIP_TRY(ctx, hipEventRecord(p->tev[L.step], st)); continue; }
+        if (L.kind == kTlWait) { HIP_TRY(ctx, hipStreamWaitEvent(st, p->tev[L.step], 0)); continue; }
         if (L.items == 0) continue;
         const int32_t* act = d_tlist + L.off;
         const int32_t* pfx = act + L.n;
@@ -817,7 +865,14 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             // the tiled sequence (~2.5 launches per 128 columns) is replayed from a graph
             // captured on first use (sigma is read from device scalars, so it stays valid)
             hipGraphExec_t& gx = n > 1 ? p->graph_multi : p->graph_exec;
-            if (!gx) {
+            static const bool use_graph = [] {
+                const char* e = getenv("DBSLMM_TGRAPH");
+                return !e || atoi(e) != 0;
+            }();
+            if (!use_graph) {
+                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist);
+                if (rc != DBSLMM_OK) return rc;
+            } else if (!gx) {
                 hipGraph_t gr = nullptr;
                 HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
                 const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist);
@@ -831,7 +886,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                 (void)hipGraphDestroy(gr);
                 HIP_TRY(ctx, ie);
             }
-            HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
+            if (use_graph) HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));
         HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
