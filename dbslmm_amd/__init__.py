@@ -152,7 +152,8 @@ class Plan:
         self.ctx.check(self.ctx.lib.dbslmm_plan_workload(self.h, _ptr(w)), "plan_workload")
         keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
                 "gram_ops_exec", "chol_flops_large", "blocks", "gram_tiles", "chol_flops_small",
-                "blocks_large", "chol_flops_tiled", "blocks_tiled", "tiled_launches")
+                "blocks_large", "chol_flops_tiled", "blocks_tiled", "tiled_launches", "trsv_bytes",
+                "cheb_iters", "cheb_base")
         return dict(zip(keys, w.tolist()))
 
     def download(self):

@@ -813,7 +813,10 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_b
     };
     if (first) {
         tile_x(A, ld, c1, jmax, zrow, D, vl, red, xs, tid);
-        if (chunk == 0 && tid < jmax) put_beta(c1, tid, xs[tid]);
+        if (chunk == 0 && tid < jmax) {
+            v[c1 + tid] = xs[tid];      // x complete in y (the h2f iteration starts from it)
+            put_beta(c1, tid, xs[tid]);
+        }
     } else {
         if (tid < kBT) xs[tid] = tid < jmax ? v[c1 + tid] : 0.0;
         __syncthreads();

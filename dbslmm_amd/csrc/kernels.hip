@@ -167,6 +167,16 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
 // ------------------------------------------------------------------------------------------
 struct GramTile { int32_t block, ti, tj, pad; };
 
+// Factorisation copies an epilogue writes (h2f tuning): copies [0, ncopy) of every block, except
+// that with tcopy >= 0 a tiled block (m >= tmin) gets copy tcopy only -- the other h2f solves of
+// the tiled blocks iterate on that one factor (trsv.hip) and need no matrix of their own.
+__device__ __forceinline__ int copy_lo(int m, int32_t tmin, int32_t tcopy) {
+    return tcopy >= 0 && m >= tmin ? tcopy : 0;
+}
+__device__ __forceinline__ int copy_hi(int m, int32_t tmin, int32_t tcopy, int32_t ncopy) {
+    return tcopy >= 0 && m >= tmin ? tcopy + 1 : ncopy;
+}
+
 // One 32 x 32 output tile (rows r0.., cols c0.. of block-local slots) on one wave, K over all
 // kpad individuals with operands straight from G (L2).  missing: the four products GG, GO, OG,
 // OO of the observed-call expansion.
@@ -174,7 +184,7 @@ __device__ __forceinline__ void gram_tile32(
     const int8_t* __restrict__ G, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
     int r0, int c0, int lane, const double* __restrict__ S, const double* __restrict__ mu,
     const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
     const int8_t* pa = G + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kpad + 16 * (lane >> 5);
     const int8_t* pb = G + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kpad + 16 * (lane >> 5);
 
@@ -248,7 +258,8 @@ __device__ __forceinline__ void gram_tile32(
         }
         double v = scale * (c * rsd[si] * rj);
         if (li == lj) v += 1.0 - tau;
-        for (int cp = 0; cp < ncopy; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
+        const int c_lo = copy_lo(m, tmin, tcopy), c_hi = copy_hi(m, tmin, tcopy, ncopy);
+        for (int cp = c_lo; cp < c_hi; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
     }
 }
 
@@ -260,14 +271,15 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
     double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
     const int lane = threadIdx.x & (kWave - 1);
     const int t = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (t >= n_tiles) return;
     const GramTile tile = tiles[t];
     const int b = tile.block;
     gram_tile32(G, kpad, blk_row0[b], blk_m[b], blk_ld[b], blk_matoff[b], (block_flags[b] & 1) != 0,
-                kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride);
+                kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride,
+                tmin, tcopy);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -297,7 +309,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
     double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t glds[];
     if (static_cast<int>(blockIdx.x) >= n_tiles) return;
@@ -315,7 +327,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
             const int r0 = kGT * tile.ti + 32 * si, c0 = kGT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
             gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
-                        tau, M, ncopy, cstride);
+                        tau, M, ncopy, cstride, tmin, tcopy);
         }
         return;
     }
@@ -407,7 +419,8 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
                 const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
                 double v = scale * (c * rsd[row0 + li] * rj);
                 if (li == lj) v += 1.0 - tau;
-                for (int cp = 0; cp < ncopy; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
+                for (int cp = copy_lo(m, tmin, tcopy); cp < copy_hi(m, tmin, tcopy, ncopy); ++cp)
+                    M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
             }
         }
     }
@@ -445,7 +458,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
     double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t hlds[];
     if (static_cast<int>(blockIdx.x) >= n_tiles) return;
@@ -463,7 +476,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             const int r0 = kHT * tile.ti + 32 * si, c0 = kHT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
             gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
-                        tau, M, ncopy, cstride);
+                        tau, M, ncopy, cstride, tmin, tcopy);
         }
         return;
     }
@@ -550,7 +563,8 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
                 const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
                 double v = scale * (c * rsd[row0 + li] * rj);
                 if (li == lj) v += 1.0 - tau;
-                for (int cp = 0; cp < ncopy; ++cp) M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
+                for (int cp = copy_lo(m, tmin, tcopy); cp < copy_hi(m, tmin, tcopy, ncopy); ++cp)
+                    M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
             }
         }
     }

@@ -30,11 +30,13 @@
 #include "chol.hip"
 #include "chol_tiled.hip"
 #include "variance.hip"
+#include "trsv.hip"
 
 namespace {
 // events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large,
-// [4] / [5] around chol_small (main stream), [6] / [7] around the tiled sequence (stream2)
-constexpr int kEvPerRun = 8;
+// [4] / [5] around chol_small (main stream), [6] / [8] around the tiled factorisation sequence,
+// [8] / [7] around the h2f Chebyshev iterations (stream2)
+constexpr int kEvPerRun = 9;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
@@ -69,6 +71,7 @@ struct dbslmm_ctx {
     hipStream_t stream2 = nullptr;   // tiled (multi-workgroup) Cholesky sequence, forked/joined
     hipStream_t stream3 = nullptr;   // its bulk trailing updates (lookahead), forked/joined
     hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
+    int n_cu = 256;                  // compute units (persistent substitution grid)
     std::string err;
 };
 
@@ -123,8 +126,21 @@ struct dbslmm_plan {
     bool timing = false;
     std::vector<hipEvent_t> ev;  // kEvPerRun per run
     std::vector<hipEvent_t> tev; // dependencies between the tiled sequence's two streams
+    // h2f tuning by Chebyshev on one factor (trsv.hip): tile work lists of the tiled blocks in
+    // forward / backward dependency order, tile flags (+ ticket counter, error word) and the
+    // iteration vectors [Y, Z, X, R, D, S] x kMaxR x n_slots
+    int32_t *d_tri_f = nullptr, *d_tri_b = nullptr, *d_foff = nullptr, *d_tflags = nullptr, *d_tb = nullptr;
+    int32_t n_titems = 0, n_tflags = 0;
+    int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
+    int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
+    double* d_cheb = nullptr;
+    double* d_coef = nullptr;
+    int32_t coef_cap = 0;
+    std::vector<hipGraphExec_t> graph_copy;  // the single-copy tiled sequence on copy c
+    int32_t cheb_base = -1;                  // base copy of the last Chebyshev run (-1: none)
+    bool cheb_pending_var = false;           // copy var_copy's tiled blocks are not factored yet
     int runs_pending = 0;
-    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0, 0};
+    double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0, 0, 0};
     int32_t ms_runs = 0;
     bool ran = false;
 };
@@ -340,6 +356,16 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
     }
 }
 
+template <int NR>
+static hipError_t set_trsv_lds() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_fwd<NR>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(trsv::kLdsBytes));
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_bwd<NR>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
+}
+
 extern "C" {
 
 int dbslmm_abi_version(void) { return DBSLMM_ABI_VERSION; }
@@ -379,7 +405,9 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                             static_cast<int>(kTrail3Lds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing2),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTrail2Lds)) != hipSuccess) {
+                            static_cast<int>(kTrail2Lds)) != hipSuccess ||
+        set_trsv_lds<1>() != hipSuccess || set_trsv_lds<2>() != hipSuccess ||
+        hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         dbslmm_ctx_destroy(c);
         return DBSLMM_E_HIP;
     }
@@ -408,13 +436,16 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
-                    p->d_tlist_multi};
+                    p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
+                    p->d_cheb, p->d_coef};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : p->tev) (void)hipEventDestroy(e);
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
     if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
+    for (hipGraphExec_t g : p->graph_copy)
+        if (g) (void)hipGraphExecDestroy(g);
     delete p;
 }
 
@@ -463,6 +494,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
     if (const char* env = getenv("DBSLMM_TILED_MIN")) tiled_min = std::max<int64_t>(64, atoll(env));
+    p->tiled_min = static_cast<int32_t>(std::min<int64_t>(tiled_min, INT32_MAX));
     std::vector<char> is_tiled;
     for (int b = 0; b < pr->num_block; ++b) {
         const int64_t s0 = pr->s_ptr[b], ms = pr->s_ptr[b + 1] - s0;
@@ -590,6 +622,45 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         p->h_tb = tb;
         build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist);
     }
+    // substitution work lists (trsv.hip): 64-row tiles of the tiled blocks; forward in order of
+    // (tile, block), backward in order of (tiles from the end, block) -- every dependency of an
+    // item comes earlier in its list
+    std::vector<int32_t> tri_f, tri_b, foff(std::max(1, p->n_nonempty), 0);
+    {
+        int32_t nf = 0, tmax = 0;
+        for (int32_t b : p->h_tb) {
+            foff[b] = nf;
+            const int T = (mv[b] + trsv::kT - 1) / trsv::kT;
+            nf += T;
+            tmax = std::max(tmax, T);
+        }
+        p->n_tflags = nf;
+        (void)tmax;
+        // ticket order: tile position relative to the block's length (ties: longer block first),
+        // monotone in the position within each block, so every dependency comes earlier
+        struct It { double key; int T; int32_t b, I; };
+        std::vector<It> v;
+        for (int32_t b : p->h_tb) {
+            const int T = (mv[b] + trsv::kT - 1) / trsv::kT;
+            for (int I = 0; I < T; ++I) v.push_back({static_cast<double>(I) / T, T, b, I});
+        }
+        std::stable_sort(v.begin(), v.end(), [](const It& x, const It& y) {
+            return x.key != y.key ? x.key < y.key : x.T > y.T;
+        });
+        for (const It& x : v) {
+            tri_f.push_back(x.b);
+            tri_f.push_back(x.I);
+            tri_b.push_back(x.b);
+            tri_b.push_back(x.T - 1 - x.I);   // backward: the same order from the other end
+        }
+        p->n_titems = static_cast<int32_t>(tri_f.size() / 2);
+        double tb = 0.0;   // factor bytes one substitution launch reads: T (T + 1) / 2 tiles per block
+        for (int32_t b : p->h_tb) {
+            const double T = (mv[b] + trsv::kT - 1) / trsv::kT;
+            tb += T * (T + 1) / 2 * trsv::kT * trsv::kT * sizeof(double);
+        }
+        p->wl[13] = tb;
+    }
     const double n_snp = static_cast<double>(p->n_s + p->n_l);
     p->wl[0] = n_snp;
     p->wl[1] = n_snp * bps;
@@ -605,6 +676,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[11] = p->n_tiled;
     p->wl[12] = static_cast<double>(std::count_if(p->tl.begin(), p->tl.end(),
                                                   [](const TLaunch& L) { return L.kind < kTlRecord; }));
+    p->wl[14] = 0;
+    p->wl[15] = -1;
 
     // ---- device allocations
     hipError_t e = hipSetDevice(ctx->device);
@@ -636,6 +709,12 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_btiles, btiles)) != hipSuccess) return fail("upload tiles");
     if ((e = dev_upload(&p->d_htiles, htiles)) != hipSuccess) return fail("upload tiles");
     if ((e = dev_upload(&p->d_tlist, tlist)) != hipSuccess) return fail("upload tiled lists");
+    if ((e = dev_upload(&p->d_tri_f, tri_f)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = dev_upload(&p->d_tri_b, tri_b)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = dev_upload(&p->d_foff, foff)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = dev_upload(&p->d_tb, p->h_tb)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 2) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
+    if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 2) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
     if ((e = hipMalloc(&p->d_mu, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -673,7 +752,7 @@ static int collect_timing(dbslmm_plan* p) {
     dbslmm_ctx* ctx = p->ctx;
     for (int r = 0; r < p->runs_pending; ++r) {
         hipEvent_t* e = &p->ev[kEvPerRun * r];
-        const int from[DBSLMM_K_COUNT] = {0, 1, 2, 4, 6}, to[DBSLMM_K_COUNT] = {1, 2, 3, 5, 7};
+        const int from[DBSLMM_K_COUNT] = {0, 1, 2, 4, 6, 8}, to[DBSLMM_K_COUNT] = {1, 2, 3, 5, 8, 7};
         for (int k = 0; k < DBSLMM_K_COUNT; ++k) {
             float ms = 0.f;
             HIP_TRY(ctx, hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
@@ -686,11 +765,16 @@ static int collect_timing(dbslmm_plan* p) {
 }
 
 // Enqueue a tiled launch list on stream2.
-static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist) {
+// copy: the list is a single-copy list applied to factorisation copy `copy` (its matrix, sigma
+// scalar, scratch, betas and status); multi-copy lists address the copies themselves (copy 0).
+static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist,
+                         int copy = 0) {
     dbslmm_ctx* ctx = p->ctx;
-    const chol::TiledArgs ta{p->d_M, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
-                             p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, p->d_dshift, isn,
-                             p->d_y, p->d_beta_s, p->d_beta_l, p->d_status, p->n_nonempty,
+    const int64_t c = copy;
+    const chol::TiledArgs ta{p->d_M + c * p->M_elems, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
+                             p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd, p->d_dshift + c, isn,
+                             p->d_y + c * p->n_slots, p->d_beta_s + c * p->n_s, p->d_beta_l + c * p->n_l,
+                             p->d_status + c * p->nbk, p->n_nonempty,
                              p->M_elems, p->n_slots, p->n_s, p->n_l, p->nbk};
     int nev = 0;
     for (const TLaunch& L : tl)
@@ -747,6 +831,198 @@ static int ensure_copies(dbslmm_plan* p, int n) {
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
     if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
     p->graph_exec = p->graph_multi = nullptr;
+    for (hipGraphExec_t& g : p->graph_copy)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    return DBSLMM_OK;
+}
+
+static bool tiled_use_graph() {
+    static const bool v = [] {
+        const char* e = getenv("DBSLMM_TGRAPH");
+        return !e || atoi(e) != 0;
+    }();
+    return v;
+}
+
+// The single-copy tiled sequence on factorisation copy `copy` (stream2), replayed from a graph
+// captured per copy.
+static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
+    dbslmm_ctx* ctx = p->ctx;
+    if (!tiled_use_graph()) return enqueue_tiled(p, isn, p->tl, p->d_tlist, copy);
+    if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
+    hipGraphExec_t& gx = p->graph_copy[copy];
+    if (!gx) {
+        hipGraph_t gr = nullptr;
+        HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
+        const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy);
+        hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
+        if (rc != DBSLMM_OK) {
+            if (gr) (void)hipGraphDestroy(gr);
+            return rc;
+        }
+        HIP_TRY(ctx, ce);
+        hipError_t ie = hipGraphInstantiate(&gx, gr, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(gr);
+        HIP_TRY(ctx, ie);
+    }
+    HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
+    return DBSLMM_OK;
+}
+
+// ---- h2f tuning by Chebyshev on one factor (trsv.hip)
+struct ChebPlan {
+    int base = -1;
+    std::vector<int> others;          // copies solved by iteration, in launch groups of kMaxR
+    std::vector<int> iters;           // per group
+    std::vector<double> coef;         // per group: [iters][nr][3] {alpha, beta, delta}
+    std::vector<size_t> coef_off;
+};
+
+// Base = the median of the shifts d_c = 1/(sigma_c n); per other copy the spectrum of
+// M_b^{-1} M_c lies in [1, 1 + delta / (d_b + 1 - tau)] (delta > 0) or its mirror (delta < 0).
+// Not applicable (false): tau outside (0, 1], or more than 60 iterations needed.
+static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPlan& cp) {
+    const char* env = getenv("DBSLMM_H2F_CHEB");
+    const bool enabled = !env || atoi(env) != 0;
+    if (!enabled || n < 2 || p->n_tiled == 0 || !(p->tau > 0.0 && p->tau <= 1.0)) return false;
+    std::vector<int> idx(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return sigmas[a] < sigmas[b]; });
+    cp.base = idx[n / 2];
+    const double nobs = static_cast<double>(p->n_obs);
+    const double db = 1.0 / (sigmas[cp.base] * nobs);
+    const double floor_ = db + 1.0 - p->tau;
+    for (int c = 0; c < n; ++c)
+        if (c != cp.base) cp.others.push_back(c);
+    for (size_t g0 = 0; g0 < cp.others.size(); g0 += trsv::kMaxR) {
+        const int nr = static_cast<int>(std::min<size_t>(trsv::kMaxR, cp.others.size() - g0));
+        std::vector<double> lo(nr), hi(nr), dl(nr);
+        int K = 1;
+        for (int j = 0; j < nr; ++j) {
+            const double dc = 1.0 / (sigmas[cp.others[g0 + j]] * nobs);
+            dl[j] = dc - db;
+            const double ext = dl[j] / floor_;
+            lo[j] = std::min(1.0, 1.0 + ext) * (1.0 - 1e-6);
+            hi[j] = std::max(1.0, 1.0 + ext) * (1.0 + 1e-6);
+            if (!(lo[j] > 0.0)) return false;
+            // Chebyshev: error <= 2 q^K x the initial error x_c - x_b, itself <= |ext| relative
+            // (the same bound); K so that the final error is 1e-14 of the solution
+            const double kap = hi[j] / lo[j], q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
+            const double e0 = std::max(std::fabs(ext), 1e-300);
+            const int k = q < 1e-300 ? 1 : std::max(1, static_cast<int>(std::ceil(std::log(0.5e-14 / e0) / std::log(q))));
+            K = std::max(K, k);
+        }
+        if (K > 60) return false;
+        cp.iters.push_back(K);
+        cp.coef_off.push_back(cp.coef.size());
+        std::vector<double> rho(nr);
+        for (int k = 0; k < K; ++k)
+            for (int j = 0; j < nr; ++j) {
+                const double th = 0.5 * (hi[j] + lo[j]), de = 0.5 * (hi[j] - lo[j]), sg = th / de;
+                double al, be;
+                if (k == 0) {
+                    rho[j] = 1.0 / sg;
+                    al = 0.0;
+                    be = 1.0 / th;
+                } else {
+                    const double rn = 1.0 / (2.0 * sg - rho[j]);
+                    al = rn * rho[j];
+                    be = 2.0 * rn / de;
+                    rho[j] = rn;
+                }
+                cp.coef.push_back(al);
+                cp.coef.push_back(be);
+                cp.coef.push_back(dl[j]);
+            }
+    }
+    return true;
+}
+
+extern "C++" {
+template <int NR>
+static void launch_trsv(bool fwd, int grid, hipStream_t st, const trsv::Args& a) {
+    if (fwd) hipLaunchKernelGGL(dbslmm_trsv_fwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
+    else hipLaunchKernelGGL(dbslmm_trsv_bwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
+}
+}
+
+// Chebyshev iterations of the non-base copies on the base copy's factor (stream2, after the
+// base copy's tiled sequence): every tiled block of copy c gets its beta and status.
+static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
+    dbslmm_ctx* ctx = p->ctx;
+    hipStream_t st = ctx->stream2;
+    const int64_t vs = std::max<int64_t>(1, p->n_slots);
+    if (!p->d_cheb)
+        HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    if (p->coef_cap < static_cast<int32_t>(cp.coef.size())) {
+        if (p->d_coef) (void)hipFree(p->d_coef);
+        p->d_coef = nullptr;
+        HIP_TRY(ctx, hipMalloc(&p->d_coef, cp.coef.size() * sizeof(double)));
+        p->coef_cap = static_cast<int32_t>(cp.coef.size());
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(p->d_coef, cp.coef.data(), cp.coef.size() * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+    const int64_t blk = trsv::kMaxR * vs;
+    double *Y = p->d_cheb, *Z = Y + blk, *X = Z + blk, *R = X + blk, *D = R + blk, *S = D + blk;
+    const int grid = std::max(1, std::min(ctx->n_cu, p->n_titems));
+    for (size_t g = 0; g < cp.iters.size(); ++g) {
+        const size_t g0 = g * trsv::kMaxR;
+        const int nr = static_cast<int>(std::min<size_t>(trsv::kMaxR, cp.others.size() - g0));
+        int cix[trsv::kMaxR] = {0, 0};
+        for (int j = 0; j < nr; ++j) cix[j] = cp.others[g0 + j];
+        const double* coef = p->d_coef + cp.coef_off[g];
+        hipLaunchKernelGGL(dbslmm_cheb_init, dim3(p->n_tiled), dim3(256), 0, st, p->d_tb, p->d_row0, p->d_m,
+                           p->d_ms, p->d_blk_id, p->d_y + static_cast<int64_t>(cp.base) * p->n_slots, coef,
+                           nr, vs, X, R, D, S, p->d_status + cp.base * p->nbk, p->d_status, p->nbk,
+                           cix[0], cix[1]);
+        HIP_TRY(ctx, hipGetLastError());
+        trsv::Args a{};
+        a.M = p->d_M + static_cast<int64_t>(cp.base) * p->M_elems;
+        a.matoff = p->d_matoff;
+        a.ld = p->d_ld;
+        a.m = p->d_m;
+        a.ms = p->d_ms;
+        a.row0 = p->d_row0;
+        a.blk_id = p->d_blk_id;
+        a.slot_out = p->d_slot_out;
+        a.n_items = p->n_titems;
+        a.foff = p->d_foff;
+        a.flags = p->d_tflags;
+        a.ctr = p->d_tflags + p->n_tflags;
+        a.err = p->d_tflags + p->n_tflags + 1;
+        a.vs = vs;
+        a.X = X;
+        a.R = R;
+        a.D = D;
+        a.S = S;
+        a.inv_sqrt_n = isn;
+        a.beta_s = p->d_beta_s;
+        a.beta_l = p->d_beta_l;
+        a.ns_stride = p->n_s;
+        a.nl_stride = p->n_l;
+        for (int j = 0; j < trsv::kMaxR; ++j) a.cix[j] = cix[j];
+        a.status = p->d_status + cp.base * p->nbk;
+        const int K = cp.iters[g];
+        a.grid = grid;
+        for (int k = 0; k < K; ++k) {
+            for (int pass = 0; pass < 2; ++pass) {
+                const bool fwd = pass == 0;
+                if (++p->trsv_epoch == INT32_MAX) {   // flags restart from a clean slate
+                    HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
+                    p->trsv_epoch = 1;
+                }
+                a.epoch = p->trsv_epoch;
+                a.items = fwd ? p->d_tri_f : p->d_tri_b;
+                a.src = fwd ? R : Y;
+                a.dst = fwd ? Y : Z;
+                a.coef = coef + static_cast<int64_t>(k) * nr * 3;
+                a.last = k == K - 1;
+                if (nr == 1) launch_trsv<1>(fwd, grid, st, a);
+                else launch_trsv<2>(fwd, grid, st, a);
+                HIP_TRY(ctx, hipGetLastError());
+            }
+        }
+    }
     return DBSLMM_OK;
 }
 
@@ -771,6 +1047,10 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             p->multi_n = n;
         }
     }
+    // h2f: the tiled blocks are factored once (copy cp.base) and the other copies iterate on it
+    ChebPlan cp;
+    const bool cheb = front && p->n_nonempty > 0 && cheb_plan(p, sigmas, n, cp);
+    const int32_t tcopy = cheb ? cp.base : -1;   // Gram epilogues: tiled blocks write this copy only
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
     if (p->timing) {
@@ -801,7 +1081,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         hipLaunchKernelGGL(dbslmm_gram_i8, grid, dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
-                           static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M, n, p->M_elems);
+                           static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M, n, p->M_elems,
+                           p->tiled_min, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_htiles > 0) {
@@ -809,7 +1090,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_htiles, p->n_htiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems);
+                           p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_btiles > 0) {
@@ -817,7 +1098,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems);
+                           p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (!front && n > 1)
@@ -846,7 +1127,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
         // single-wave blocks: concurrently on stream2 when there is no tiled sequence, else
         // behind the single-workgroup kernel (each stream keeps its own hardware queue)
-        const std::vector<TLaunch>& tl = n > 1 ? p->tl_multi : p->tl;
+        const std::vector<TLaunch>& tl = n > 1 && !cheb ? p->tl_multi : p->tl;
         hipStream_t ss = tl.empty() ? ctx->stream2 : s;
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ss));
         for (int c = 0; c < n && p->n_small > 0; ++c) {
@@ -865,11 +1146,15 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             // the tiled sequence (~2.5 launches per 128 columns) is replayed from a graph
             // captured on first use (sigma is read from device scalars, so it stays valid)
             hipGraphExec_t& gx = n > 1 ? p->graph_multi : p->graph_exec;
-            static const bool use_graph = [] {
-                const char* e = getenv("DBSLMM_TGRAPH");
-                return !e || atoi(e) != 0;
-            }();
-            if (!use_graph) {
+            const bool use_graph = tiled_use_graph() && !cheb;
+            if (cheb) {
+                // h2f: factor only the base copy, iterate the others on its factor
+                int rc = run_tiled_copy(p, isn, cp.base);
+                if (rc != DBSLMM_OK) return rc;
+                if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                rc = run_cheb(p, isn, cp);
+                if (rc != DBSLMM_OK) return rc;
+            } else if (!use_graph) {
                 const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist);
                 if (rc != DBSLMM_OK) return rc;
             } else if (!gx) {
@@ -888,6 +1173,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             }
             if (use_graph) HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
         }
+        if (ev && !cheb) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));
         HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
         if (ss != s) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
@@ -898,11 +1184,20 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         HIP_TRY(ctx, hipEventRecord(ev[4], s));
         HIP_TRY(ctx, hipEventRecord(ev[5], s));
         HIP_TRY(ctx, hipEventRecord(ev[6], s));
+        HIP_TRY(ctx, hipEventRecord(ev[8], s));
         HIP_TRY(ctx, hipEventRecord(ev[7], s));
     }
     p->ran = true;
     p->sigma_run = sigmas[n - 1];
     p->var_copy = n - 1;
+    {
+        p->cheb_base = cheb ? cp.base : -1;
+        int iters = 0;
+        for (int k : cp.iters) iters += k;
+        p->wl[14] = cheb ? iters : 0;
+        p->wl[15] = p->cheb_base;
+        p->cheb_pending_var = cheb && cp.base != n - 1;   // no factor of the last copy's tiled blocks
+    }
     return DBSLMM_OK;
 }
 
@@ -911,6 +1206,15 @@ static int download_copy(dbslmm_plan* p, int c, double* beta_s, double* beta_l, 
     if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (p->d_tflags && p->cheb_base >= 0) {
+        int32_t werr = 0;
+        HIP_TRY(ctx, hipMemcpy(&werr, p->d_tflags + p->n_tflags + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (werr) {
+            (void)hipMemset(p->d_tflags + p->n_tflags + 1, 0, sizeof(int32_t));
+            ctx->err = "substitution hand-off wait gave up (trsv)";
+            return DBSLMM_E_HIP;
+        }
+    }
     if (beta_s && p->n_s)
         HIP_TRY(ctx, hipMemcpy(beta_s, p->d_beta_s + c * p->n_s, p->n_s * sizeof(double), hipMemcpyDeviceToHost));
     if (beta_l && p->n_l)
@@ -997,6 +1301,14 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     dbslmm_ctx* ctx = p->ctx;
     if (!p->ran) { ctx->err = "plan_variance before plan_run"; return DBSLMM_E_STATE; }
     ARG_CHECK(ctx, tp && tp->bed && tp->indicator && tp->n_total > 0, "bad test panel");
+    if (p->cheb_pending_var) {
+        // the last h2f run iterated the last sigma's tiled blocks on another copy's factor and
+        // wrote no matrix for them: re-run that sigma alone (Gram + factorisation) for its factor
+        const double sg = p->sigma_run;
+        p->cheb_pending_var = false;
+        const int rc = run_impl(p, true, &sg, 1);
+        if (rc != DBSLMM_OK) return rc;
+    }
     ARG_CHECK(ctx, p->n_s == 0 || tp->s_pos, "test panel s_pos missing");
     ARG_CHECK(ctx, p->n_l == 0 || tp->l_pos, "test panel l_pos missing");
     std::vector<int32_t> sel;

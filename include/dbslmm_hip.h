@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 3
+#define DBSLMM_ABI_VERSION 4
 
 enum {
     DBSLMM_OK = 0,
@@ -92,7 +92,9 @@ enum {
     DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold (env
                                  DBSLMM_TILED_MIN, default 512), many workgroups per block,
                                  one launch per panel phase (third stream); the whole sequence */
-    DBSLMM_K_COUNT = 5
+    DBSLMM_K_TRSV = 5,        /* dbslmm_trsv_fwd/bwd: h2f tuning's Chebyshev iterations of the
+                                 tiled blocks on the base copy's factor (run_multi; 0 otherwise) */
+    DBSLMM_K_COUNT = 6
 };
 
 int dbslmm_abi_version(void);
@@ -137,8 +139,10 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * sum_b n_ref*m_b*(m_b+1)), [4] Gram ops as executed on padded tiles, [5] Cholesky+solve fp64
  * flops of the large blocks (sum_b m_b^3/3 + 2 m_b^2), [6] non-empty blocks, [7] gram tiles,
  * [8] the same fp64 flops for the small blocks, [9] large blocks, [10] the same fp64 flops for
- * the tiled blocks, [11] tiled blocks, [12] launches of the tiled sequence per run. */
-#define DBSLMM_WORKLOAD_LEN 13
+ * the tiled blocks, [11] tiled blocks, [12] launches of the tiled sequence per run, [13] bytes of
+ * the factor read by one substitution launch over the tiled blocks (64-row tiles), [14] Chebyshev
+ * iterations of the latest run_multi (0: none), [15] its base copy (-1: none). */
+#define DBSLMM_WORKLOAD_LEN 16
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
 
 /* Test-set variance (the `diags` matrix DBSLMMFIT::est saves to variance.txt,

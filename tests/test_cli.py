@@ -112,11 +112,22 @@ def test_cli_lmm_only_tau08(tmp_path):
     assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-10
 
 
+def _eff_rows(text):
+    rows = [l.split() for l in text.splitlines() if l.strip()]
+    keys = [(r[0], r[1], r[4]) for r in rows]
+    vals = np.array([[float(r[2]), float(r[3])] for r in rows])
+    return keys, vals
+
+
 @pytest.mark.gpu
-def test_cli_h2f_tuning_matches_separate_runs(tmp_path):
+@pytest.mark.parametrize("cheb", ["0", "1"])
+def test_cli_h2f_tuning_matches_separate_runs(tmp_path, monkeypatch, cheb):
     """-h2f 0.8,1,1.2 (one Gram, three solves) writes the R driver's file names
     (<prefix>_h2f<hh>.dbslmm.txt, software/DBSLMM.R:204-219) with the same rows as three runs
-    with -h 0.5*hh."""
+    with -h 0.5*hh: identical with the merged factorisations (DBSLMM_H2F_CHEB=0); with the
+    Chebyshev path (one factor, the other factors iterated) the same rows and values within
+    1e-12 of the largest |beta| (the base factor's file stays identical)."""
+    monkeypatch.setenv("DBSLMM_H2F_CHEB", cheb)
     s, l = split_summary(tmp_path)
     base = ["-s", s, "-l", l, "-r", REF, "-b", BLOCKS_EUR1, "-n", "2400", "-nsnp", "996",
             "-mafMax", "0.2", "--precise-out"]
@@ -128,4 +139,11 @@ def test_cli_h2f_tuning_matches_separate_runs(tmp_path):
         single = str(tmp_path / f"single{hh}")
         r = run(base + ["-h", repr(0.5 * float(hh)), "-eff", single])
         assert r.returncode == 0, r.stderr
-        assert tuned == open(single + ".txt").read()
+        ref = open(single + ".txt").read()
+        if cheb == "0" or hh == "1":
+            assert tuned == ref
+        else:
+            kt, vt = _eff_rows(tuned)
+            kr, vr = _eff_rows(ref)
+            assert kt == kr
+            assert np.max(np.abs(vt - vr)) <= 1e-12 * np.max(np.abs(vr))

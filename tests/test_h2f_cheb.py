@@ -1,0 +1,89 @@
+"""h2f tuning by Chebyshev iteration on one factor (trsv.hip): for the tiled blocks only the base
+copy (median sigma) is factored; the other copies iterate M_b x = z - delta P_s x with the
+persistent forward / backward substitution kernels.  Every copy must match a fresh single-sigma
+solve to fp64 accuracy (normwise 1e-12), the base copy bit for bit; statuses and the NaN of a
+monomorphic block carry over; the merged-factorisation path (DBSLMM_H2F_CHEB=0) stays
+bit-identical."""
+import numpy as np
+import pytest
+
+from _common import normwise
+from test_tiled import _oracle, _problem
+
+pytestmark = pytest.mark.gpu
+
+
+def _fresh(prob, sig):
+    from dbslmm_amd import DBSLMMFIT
+    fit = DBSLMMFIT(0)
+    out = []
+    for f in sig:
+        prob.sigma_s = f
+        out.append(fit.est(prob))
+    return out
+
+
+def _cat(r):
+    return np.concatenate([r[0], r[1]])
+
+
+def _finite_normwise(a, b):
+    ok = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), ok)
+    return normwise(a[ok], b[ok])
+
+
+@pytest.mark.parametrize("tiled_min", ["64", "512"])
+@pytest.mark.parametrize("factors", [(0.8, 1.0, 1.2), (1.2, 0.8), (0.5, 0.7, 1.0, 1.3, 1.6, 2.0)])
+def test_cheb_copies_match_fresh_solves(monkeypatch, tiled_min, factors):
+    from dbslmm_amd import Context, Plan
+    monkeypatch.setenv("DBSLMM_TILED_MIN", tiled_min)
+    prob = _problem(seed=5, mono_block=3)
+    s0 = prob.sigma_s
+    sig = [s0 * f for f in factors]
+    plan = Plan(Context(0), prob)
+    multi = plan.run_multi(sig)
+    fresh = _fresh(prob, sig)
+    base = int(np.argsort(sig, kind="stable")[len(sig) // 2])
+    for c, (got, ref) in enumerate(zip(multi, fresh)):
+        np.testing.assert_array_equal(got[2], ref[2])
+        assert got[2][3] == 3
+        if c == base:
+            np.testing.assert_array_equal(_cat(got), _cat(ref))
+        else:
+            assert _finite_normwise(_cat(got), _cat(ref)) < 1e-12, c
+    # against the oracle's direct solve of the reference equations too
+    prob.sigma_s = sig[0]
+    ref, _ = _oracle(prob)
+    ok = np.isfinite(ref) & np.isfinite(_cat(multi[0]))
+    assert normwise(_cat(multi[0])[ok], ref[ok]) < 1e-10
+
+
+def test_cheb_off_is_bit_identical(monkeypatch):
+    from dbslmm_amd import Context, Plan
+    monkeypatch.setenv("DBSLMM_TILED_MIN", "64")
+    monkeypatch.setenv("DBSLMM_H2F_CHEB", "0")
+    prob = _problem(seed=6)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    multi = Plan(Context(0), prob).run_multi(sig)
+    for got, ref in zip(multi, _fresh(prob, sig)):
+        np.testing.assert_array_equal(_cat(got), _cat(ref))
+
+
+def test_cheb_repeatable_and_followed_by_plain_run(monkeypatch):
+    """Two h2f runs give identical betas (fixed iteration count, fixed reduction order), and a
+    plain run afterwards equals a fresh single-sigma plan."""
+    from dbslmm_amd import Context, Plan
+    monkeypatch.setenv("DBSLMM_TILED_MIN", "64")
+    prob = _problem(seed=8)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    plan = Plan(Context(0), prob)
+    a = plan.run_multi(sig)
+    b = plan.run_multi(sig)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(_cat(x), _cat(y))
+    plan.set_sigma(sig[0])
+    plan.run()
+    got = plan.download()
+    ref = _fresh(prob, sig[:1])[0]
+    np.testing.assert_array_equal(_cat(got), _cat(ref))

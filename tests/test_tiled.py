@@ -145,6 +145,7 @@ def test_run_multi_merged_copies_bit_identical(monkeypatch, tiled_min):
     (the last sigma) stay consistent."""
     from dbslmm_amd import Context, DBSLMMFIT, Plan
     monkeypatch.setenv("DBSLMM_TILED_MIN", tiled_min)
+    monkeypatch.setenv("DBSLMM_H2F_CHEB", "0")   # the merged path (tests/test_h2f_cheb.py: the other)
     prob = _problem(seed=5, mono_block=3)
     plan = Plan(Context(0), prob)
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
