@@ -133,6 +133,7 @@ struct dbslmm_plan {
     int32_t n_titems = 0, n_tflags = 0;
     int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
+    unsigned long long* d_stamps = nullptr;  // diagnostics only (DBSLMM_TRSV_STAMPS; not owned)
     double* d_cheb = nullptr;
     double* d_coef = nullptr;
     int32_t coef_cap = 0;
@@ -640,9 +641,21 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         // monotone in the position within each block, so every dependency comes earlier
         struct It { double key; int T; int32_t b, I; };
         std::vector<It> v;
+        int32_t only = -1;   // diagnostics: DBSLMM_TRSV_ONLY_BIGGEST=1 keeps the largest block alone
+        if (getenv("DBSLMM_TRSV_ONLY_BIGGEST") && !p->h_tb.empty()) {
+            only = p->h_tb[0];
+            for (int32_t b : p->h_tb) if (mv[b] > mv[only]) only = b;
+        }
+        int order = 0;   // 0: I / T, 1: I - T (longest remaining chain first), 2: I, 3: I - T / 2
+        if (const char* e = getenv("DBSLMM_TRSV_ORDER")) order = atoi(e);
         for (int32_t b : p->h_tb) {
+            if (only >= 0 && b != only) continue;
             const int T = (mv[b] + trsv::kT - 1) / trsv::kT;
-            for (int I = 0; I < T; ++I) v.push_back({static_cast<double>(I) / T, T, b, I});
+            for (int I = 0; I < T; ++I) {
+                const double key = order == 1 ? I - T : order == 2 ? I : order == 3 ? I - 0.5 * T
+                                                                                      : static_cast<double>(I) / T;
+                v.push_back({key, T, b, I});
+            }
         }
         std::stable_sort(v.begin(), v.end(), [](const It& x, const It& y) {
             return x.key != y.key ? x.key < y.key : x.T > y.T;
@@ -1002,6 +1015,15 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
         a.nl_stride = p->n_l;
         for (int j = 0; j < trsv::kMaxR; ++j) a.cix[j] = cix[j];
         a.status = p->d_status + cp.base * p->nbk;
+        static unsigned long long* d_stamps = nullptr;   // diagnostics: the largest tiled block
+        if (getenv("DBSLMM_TRSV_STAMPS")) {
+            int bmax = p->h_tb[0];
+            for (int32_t b : p->h_tb) if (p->h_m[b] > p->h_m[bmax]) bmax = b;
+            if (!d_stamps) HIP_TRY(ctx, hipMalloc(&d_stamps, 8 * 4096 * sizeof(unsigned long long)));
+            a.stamps = d_stamps;
+            a.stamp_b = bmax;
+            p->d_stamps = d_stamps;
+        }
         const int K = cp.iters[g];
         a.grid = grid;
         for (int k = 0; k < K; ++k) {
@@ -1266,6 +1288,14 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* p, double* ms_out, int32_t* launches_out)
     for (int k = 0; k < DBSLMM_K_COUNT; ++k) ms_out[k] = p->ms_runs ? p->ms_acc[k] / p->ms_runs : 0.0;
     if (launches_out) *launches_out = p->ms_runs;
     return DBSLMM_OK;
+}
+
+// diagnostics (not in the public header): the substitution stamps of the last forward launch
+extern "C" int dbslmm_diag_trsv_stamps(dbslmm_plan* p, unsigned long long* out, int n) {
+    if (!p || !p->d_stamps) return DBSLMM_E_STATE;
+    if (hipDeviceSynchronize() != hipSuccess) return DBSLMM_E_HIP;
+    return hipMemcpy(out, p->d_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess
+               ? DBSLMM_OK : DBSLMM_E_HIP;
 }
 
 int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {

@@ -82,7 +82,12 @@ struct Args {
     int64_t ns_stride, nl_stride;
     int32_t cix[kMaxR];
     const int32_t* status;       // the base copy's block status
+    unsigned long long* stamps;  // diagnostics (env DBSLMM_TRSV_STAMPS): per tile of block stamp_b,
+    int32_t stamp_b;             // 100 MHz times [claim, last hand-off staged, stream done, publish]
 };
+__device__ __forceinline__ void stamp(const Args& a, int b, int I, int k) {
+    if (a.stamps && b == a.stamp_b) a.stamps[8 * I + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // LDS control words of the ring
 struct Ring {
@@ -197,8 +202,10 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* ring = lds;                       // [kNS][64][NR]
     double* vs = ring + kNS * kT * NR;        // [64][NR]: r_I - sum_J L_IJ y_J
-    Ring* rg = reinterpret_cast<Ring*>(vs + kT * NR);
+    double* rt = vs + kT * NR;                // [8 waves][8 NR][65]: lane partial sums (transpose)
+    Ring* rg = reinterpret_cast<Ring*>(rt + kSW * 8 * NR * (kT + 1));
     const int tid = threadIdx.x, row = tid >> 3, part = tid & 7, lane = tid & 63, wave = tid >> 6;
+    constexpr int kV = 8 * NR, kG = kT / kV;  // row sums per wave; lanes per row sum
     for (;;) {
         const int it = take_ticket(a, rg, tid);
         if (it >= a.n_items) break;
@@ -208,8 +215,10 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
         const int r0 = kT * I, jmax = min(kT, m - r0);
         const int32_t* flag = a.flags + a.foff[b];
         double xd[8];
+        if (tid == 0) stamp(a, b, I, 0);
         if (wave == kSW) {
             control<NR>(a, rg, ring, flag, g0, m, 0, 1, I, lane);
+            if (lane == 0) stamp(a, b, I, 1);
         } else {
             // xd[k] = X[row][8 part + k] = A(r0 + 8 part + k, r0 + row) (8 part + k <= row)
 #pragma unroll
@@ -218,6 +227,9 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
                 const double x = A[static_cast<int64_t>(r0 + rr) * ld + r0 + row];   // inside ld x ld
                 xd[k] = (rr <= row && row < jmax) ? x : 0.0;
             }
+            // this lane's share of r_I, read now (off the dependency chain): value v = lane / kG
+            const int vv = lane / kG, vk = vv / NR, vc = vv - vk * NR, vr = 8 * wave + vk;
+            const double rsrc = vr < jmax ? a.src[vc * a.vs + g0 + r0 + vr] : 0.0;
             const double* Lw = A + static_cast<int64_t>(r0 + 8 * wave) * ld + lane;
             double acc[8][NR];
 #pragma unroll
@@ -250,29 +262,28 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
                     }
                 }
             }
-            // row sums over the 64 lanes
+            if (tid == 0) stamp(a, b, I, 2);
+            // row sums over the 64 lanes: transpose through LDS (wave-private region), then lane
+            // group g of kG lanes sums value v = lane / kG over 64 / kG lanes each
+            double* rw = rt + wave * kV * (kT + 1);
 #pragma unroll
             for (int k = 0; k < 8; ++k)
 #pragma unroll
-                for (int c = 0; c < NR; ++c) {
-                    double v = acc[k][c];
-                    v += __shfl_xor(v, 32);
-                    v += __shfl_xor(v, 16);
-                    v += __shfl_xor(v, 8);
-                    acc[k][c] = red8(v);
-                }
-            if (lane < NR) {
+                for (int c = 0; c < NR; ++c) rw[(k * NR + c) * (kT + 1) + lane] = acc[k][c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double sum = 0.0;
+            const int q0 = (lane % kG) * (kT / kG);
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int rr = 8 * wave + k;
-                    double s = 0.0;
+            for (int q = 0; q < kT / kG; ++q) sum += rw[vv * (kT + 1) + q0 + q];
 #pragma unroll
-                    for (int c = 0; c < NR; ++c) s = lane == c ? acc[k][c] : s;
-                    vs[rr * NR + lane] = rr < jmax ? a.src[lane * a.vs + g0 + r0 + rr] - s : 0.0;
-                }
-            }
+            for (int sft = 1; sft < kG; sft <<= 1) sum += __shfl_xor(sum, sft);
+            if (tid == 0) stamp(a, b, I, 4);
+            if (lane % kG == 0) vs[vr * NR + vc] = vr < jmax ? rsrc - sum : 0.0;
         }
         __syncthreads();
+        if (tid == 0) stamp(a, b, I, 5);
         if (wave < kSW) {
             double y[NR];
 #pragma unroll
@@ -288,7 +299,9 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
                 for (int c = 0; c < NR; ++c) st_sc1(a.dst + c * a.vs + g0 + r0 + row, y[c]);
             }
         }
+        if (tid == 0) stamp(a, b, I, 6);
         publish(a.flags + a.foff[b] + I, a.epoch, tid);   // (its barrier also frees vs)
+        if (tid == 0) stamp(a, b, I, 3);
     }
 }
 
@@ -316,6 +329,8 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
         const int r0 = kT * I, jmax = min(kT, m - r0);
         const int32_t* flag = a.flags + a.foff[b];
         const int cnt = T - 1 - I;                // later tiles, taken from the last one down
+        // y_I for the final subtraction, read now (off the dependency chain)
+        const double ysrc = tid < kT * NR && tid / NR < jmax ? a.src[(tid % NR) * a.vs + g0 + r0 + tid / NR] : 0.0;
         double xd[8];
         if (wave == kSW) {
             control<NR>(a, rg, ring, flag, g0, m, T - 1, -1, cnt, lane);
@@ -368,7 +383,7 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
             double s = 0.0;
 #pragma unroll
             for (int w = 0; w < kSW; ++w) s += red[(w * kT + col) * NR + c];
-            ws[tid] = col < jmax ? a.src[c * a.vs + g0 + r0 + col] - s : 0.0;
+            ws[tid] = col < jmax ? ysrc - s : 0.0;
         }
         __syncthreads();
         if (wave < kSW) {
