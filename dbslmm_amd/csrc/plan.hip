@@ -781,7 +781,7 @@ static int collect_timing(dbslmm_plan* p) {
 // copy: the list is a single-copy list applied to factorisation copy `copy` (its matrix, sigma
 // scalar, scratch, betas and status); multi-copy lists address the copies themselves (copy 0).
 static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist,
-                         int copy = 0) {
+                         int copy = 0, bool skip_bwd = false) {
     dbslmm_ctx* ctx = p->ctx;
     const int64_t c = copy;
     const chol::TiledArgs ta{p->d_M + c * p->M_elems, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
@@ -801,7 +801,7 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
         hipStream_t st = L.strm ? ctx->stream3 : ctx->stream2;
         if (L.kind == kTlRecord) { HIP_TRY(ctx, hipEventRecord(p->tev[L.step], st)); continue; }
         if (L.kind == kTlWait) { HIP_TRY(ctx, hipStreamWaitEvent(st, p->tev[L.step], 0)); continue; }
-        if (L.items == 0) continue;
+        if (L.items == 0 || (skip_bwd && L.kind == 3)) continue;
         const int32_t* act = d_tlist + L.off;
         const int32_t* pfx = act + L.n;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
@@ -857,17 +857,80 @@ static bool tiled_use_graph() {
     return v;
 }
 
+extern "C++" {
+template <int NR>
+static void launch_trsv(bool fwd, int grid, hipStream_t st, const trsv::Args& a) {
+    if (fwd) hipLaunchKernelGGL(dbslmm_trsv_fwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
+    else hipLaunchKernelGGL(dbslmm_trsv_bwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
+}
+}
+
+static bool persistent_bwd() {   // env DBSLMM_PBWD=0: the per-tile backward launches instead
+    const char* e = getenv("DBSLMM_PBWD");
+    return !e || atoi(e) != 0;
+}
+
+// Backward substitution of factorisation copy `copy`'s tiled blocks in one persistent launch
+// (trsv.hip, plain mode): y = the bordered z row, x -> y scratch of the copy, beta of the copy.
+static int run_pbwd(dbslmm_plan* p, double isn, int copy) {
+    dbslmm_ctx* ctx = p->ctx;
+    hipStream_t st = ctx->stream2;
+    const int64_t vs = std::max<int64_t>(1, p->n_slots);
+    if (!p->d_cheb) HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    const int64_t c = copy;
+    trsv::Args a{};
+    a.M = p->d_M + c * p->M_elems;
+    a.matoff = p->d_matoff;
+    a.ld = p->d_ld;
+    a.m = p->d_m;
+    a.ms = p->d_ms;
+    a.row0 = p->d_row0;
+    a.blk_id = p->d_blk_id;
+    a.slot_out = p->d_slot_out;
+    a.items = p->d_tri_b;
+    a.n_items = p->n_titems;
+    a.grid = std::max(1, std::min(ctx->n_cu, p->n_titems));
+    a.foff = p->d_foff;
+    a.flags = p->d_tflags;
+    a.ctr = p->d_tflags + p->n_tflags;
+    a.err = p->d_tflags + p->n_tflags + 1;
+    a.vs = vs;
+    a.dst = p->d_cheb + trsv::kMaxR * vs;          // the Z hand-off buffer
+    a.X = p->d_y + c * p->n_slots;
+    a.inv_sqrt_n = isn;
+    a.beta_s = p->d_beta_s;
+    a.beta_l = p->d_beta_l;
+    a.ns_stride = p->n_s;
+    a.nl_stride = p->n_l;
+    a.cix[0] = copy;
+    a.status = p->d_status + c * p->nbk;
+    a.mode = 1;
+    if (++p->trsv_epoch == INT32_MAX) {
+        HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
+        p->trsv_epoch = 1;
+    }
+    a.epoch = p->trsv_epoch;
+    launch_trsv<1>(false, a.grid, st, a);
+    HIP_TRY(ctx, hipGetLastError());
+    return DBSLMM_OK;
+}
+
 // The single-copy tiled sequence on factorisation copy `copy` (stream2), replayed from a graph
-// captured per copy.
+// captured per copy; its backward substitution is one persistent launch (run_pbwd) unless
+// DBSLMM_PBWD=0.
 static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
     dbslmm_ctx* ctx = p->ctx;
-    if (!tiled_use_graph()) return enqueue_tiled(p, isn, p->tl, p->d_tlist, copy);
+    const bool pb = persistent_bwd();
+    if (!tiled_use_graph()) {
+        const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy, pb);
+        return rc != DBSLMM_OK || !pb ? rc : run_pbwd(p, isn, copy);
+    }
     if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
     hipGraphExec_t& gx = p->graph_copy[copy];
     if (!gx) {
         hipGraph_t gr = nullptr;
         HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-        const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy);
+        const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy, pb);
         hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
         if (rc != DBSLMM_OK) {
             if (gr) (void)hipGraphDestroy(gr);
@@ -879,7 +942,7 @@ static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
         HIP_TRY(ctx, ie);
     }
     HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
-    return DBSLMM_OK;
+    return pb ? run_pbwd(p, isn, copy) : DBSLMM_OK;
 }
 
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
@@ -951,13 +1014,6 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
     return true;
 }
 
-extern "C++" {
-template <int NR>
-static void launch_trsv(bool fwd, int grid, hipStream_t st, const trsv::Args& a) {
-    if (fwd) hipLaunchKernelGGL(dbslmm_trsv_fwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
-    else hipLaunchKernelGGL(dbslmm_trsv_bwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
-}
-}
 
 // Chebyshev iterations of the non-base copies on the base copy's factor (stream2, after the
 // base copy's tiled sequence): every tiled block of copy c gets its beta and status.
@@ -1168,8 +1224,12 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             // the tiled sequence (~2.5 launches per 128 columns) is replayed from a graph
             // captured on first use (sigma is read from device scalars, so it stays valid)
             hipGraphExec_t& gx = n > 1 ? p->graph_multi : p->graph_exec;
-            const bool use_graph = tiled_use_graph() && !cheb;
-            if (cheb) {
+            const bool single = n == 1 && persistent_bwd();   // one copy: run_tiled_copy's path
+            const bool use_graph = tiled_use_graph() && !cheb && !single;
+            if (single) {
+                const int rc = run_tiled_copy(p, isn, 0);
+                if (rc != DBSLMM_OK) return rc;
+            } else if (cheb) {
                 // h2f: factor only the base copy, iterate the others on its factor
                 int rc = run_tiled_copy(p, isn, cp.base);
                 if (rc != DBSLMM_OK) return rc;
@@ -1177,12 +1237,14 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                 rc = run_cheb(p, isn, cp);
                 if (rc != DBSLMM_OK) return rc;
             } else if (!use_graph) {
-                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist);
+                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist, 0,
+                                             persistent_bwd());
                 if (rc != DBSLMM_OK) return rc;
             } else if (!gx) {
                 hipGraph_t gr = nullptr;
                 HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist);
+                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist, 0,
+                                             persistent_bwd());
                 hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
                 if (rc != DBSLMM_OK) {
                     if (gr) (void)hipGraphDestroy(gr);
@@ -1194,6 +1256,11 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                 HIP_TRY(ctx, ie);
             }
             if (use_graph) HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
+            if (!single && !cheb && persistent_bwd())   // merged copies: one backward launch each
+                for (int c = 0; c < n; ++c) {
+                    const int rc = run_pbwd(p, isn, c);
+                    if (rc != DBSLMM_OK) return rc;
+                }
         }
         if (ev && !cheb) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));

@@ -82,6 +82,8 @@ struct Args {
     int64_t ns_stride, nl_stride;
     int32_t cix[kMaxR];
     const int32_t* status;       // the base copy's block status
+    int32_t mode;                // backward: 0 Chebyshev epilogue; 1 plain solve of the factored
+                                 // system (y = the matrix's z row, x -> X, beta of copy cix[0])
     unsigned long long* stamps;  // diagnostics (env DBSLMM_TRSV_STAMPS): per tile of block stamp_b,
     int32_t stamp_b;             // 100 MHz times [claim, last hand-off staged, stream done, publish]
 };
@@ -330,7 +332,10 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
         const int32_t* flag = a.flags + a.foff[b];
         const int cnt = T - 1 - I;                // later tiles, taken from the last one down
         // y_I for the final subtraction, read now (off the dependency chain)
-        const double ysrc = tid < kT * NR && tid / NR < jmax ? a.src[(tid % NR) * a.vs + g0 + r0 + tid / NR] : 0.0;
+        double ysrc = 0.0;
+        if (tid < kT * NR && tid / NR < jmax)
+            ysrc = a.mode ? A[static_cast<int64_t>(m) * ld + r0 + tid]   // bordered row m: y = L^-1 z
+                          : a.src[(tid % NR) * a.vs + g0 + r0 + tid / NR];
         double xd[8];
         if (wave == kSW) {
             control<NR>(a, rg, ring, flag, g0, m, T - 1, -1, cnt, lane);
@@ -414,6 +419,15 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
                 const int64_t gi = g0 + i;
                 const bool small = i < a.ms[b];
                 const bool fail = a.status[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
+                if (a.mode) {   // plain solve: x and beta (NR = 1)
+                    const double x = zt[tid];
+                    a.X[gi] = x;
+                    const double v = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
+                    const int so = a.slot_out[gi];
+                    if (so >= 0) a.beta_s[a.cix[0] * a.ns_stride + so] = v;
+                    else a.beta_l[a.cix[0] * a.nl_stride - 1 - so] = v;
+                    continue;
+                }
                 const double al = a.coef[3 * c], be = a.coef[3 * c + 1], de = a.coef[3 * c + 2];
                 const int64_t o = c * a.vs + gi;
                 const double d = al * a.D[o] + be * zt[tid];
