@@ -119,7 +119,10 @@ def pmc_traffic(kernel, args, n_solve):
     k = d.get("kernels", {}).get(kernel)
     if not k:
         return None, None
-    per = k["hbm_bytes"] * (n_solve if kernel.startswith("dbslmm_chol") or kernel == "dbslmm_tchol" else 1)
+    if "hbm_bytes_per_step" in k:             # composite phases (tiled sequence, h2f substitutions)
+        per = k["hbm_bytes_per_step"]
+    else:
+        per = k["hbm_bytes"] * (n_solve if kernel.startswith("dbslmm_chol") else 1)
     return per, os.path.relpath(files[-1], ROOT)
 
 

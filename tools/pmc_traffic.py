@@ -4,9 +4,11 @@ FETCH_SIZE and WRITE_SIZE are in KB.  On gfx950 FETCH_SIZE reports half of the b
 coalesced streaming read (MI355X_MICROARCH.md, HBM section): the read side is doubled here.
     python tools/pmc_traffic.py gpurun_out/pmc profiles/r01/pmc_traffic_c4.json [bench args]
 
-Also records launches per kernel and, for the tiled Cholesky (a sequence of dbslmm_tchol_*
-launches per solve), the summed HBM bytes per solve under "dbslmm_tchol" (solves = launches of
-dbslmm_set_scalar, one per factorisation).
+Also records launches per kernel and, for the composite phases the bench times as one slot --
+the tiled Cholesky (dbslmm_tchol_* launches plus the persistent backward substitution
+dbslmm_trsv_bwd<1>) and the h2f Chebyshev substitutions (dbslmm_trsv_fwd/bwd<2>) -- the summed
+HBM bytes per run (= per bench step; runs = launches of dbslmm_unpack_stats) under
+"dbslmm_tchol" and "dbslmm_trsv" (key "hbm_bytes_per_step").
 """
 import collections
 import csv
@@ -31,18 +33,24 @@ def main(src, dst, bench_args=""):
                      f"`python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline {bench_args}`".rstrip(),
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
            "kernels": {}}
-    solves = f.get("dbslmm_set_scalar", (0, 0))[1]
-    seq = 0.0
+    runs = f.get("dbslmm_unpack_stats", (0, 0))[1]
+    seq = trsv = 0.0
     for k in sorted(set(f) | set(w)):
-        if not k.startswith("dbslmm_"):
+        name = k[5:] if k.startswith("void ") else k
+        if not name.startswith("dbslmm_"):
             continue
         (fk, n), (wk, _) = f.get(k, (0.0, 0)), w.get(k, (0.0, 0))
-        out["kernels"][k] = dict(fetch_kb=fk, write_kb=wk, hbm_bytes=(2 * fk + wk) * 1024.0, launches=n)
-        if k.startswith("dbslmm_tchol_"):
+        out["kernels"][name] = dict(fetch_kb=fk, write_kb=wk, hbm_bytes=(2 * fk + wk) * 1024.0, launches=n)
+        if name.startswith("dbslmm_tchol_") or name.startswith("dbslmm_trsv_bwd<1>"):
             seq += (2 * fk + wk) * 1024.0 * n
-    if solves and seq:
-        out["kernels"]["dbslmm_tchol"] = dict(hbm_bytes=seq / solves, solves=solves,
-                                              note="sum over dbslmm_tchol_* launches per solve")
+        elif name.startswith("dbslmm_trsv_"):
+            trsv += (2 * fk + wk) * 1024.0 * n
+    if runs and seq:
+        out["kernels"]["dbslmm_tchol"] = dict(hbm_bytes_per_step=seq / runs, runs=runs,
+                                              note="dbslmm_tchol_* + persistent backward, per run")
+    if runs and trsv:
+        out["kernels"]["dbslmm_trsv"] = dict(hbm_bytes_per_step=trsv / runs, runs=runs,
+                                             note="h2f Chebyshev substitutions, per run")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
