@@ -367,6 +367,23 @@ static hipError_t set_trsv_lds() {
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
 }
 
+// The lookahead's bulk-trailing stream.  Env DBSLMM_CHAIN_CUS=k (diagnostic): a CU mask keeps
+// k CUs (spread over the XCDs) free of the bulk so the latency-bound chain kernels of the other
+// stream find them idle.
+static hipError_t create_far_stream(int device, hipStream_t* st) {
+    int k = 0;
+    if (const char* e = getenv("DBSLMM_CHAIN_CUS")) k = atoi(e);
+    int ncu = 0;
+    if (k <= 0 || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        ncu <= k)
+        return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    const int stride = ncu / k;
+    for (int i = 0; i < ncu; ++i)
+        if (!(i % stride == stride - 1 && i / stride < k)) mask[i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(st, static_cast<uint32_t>(mask.size()), mask.data());
+}
+
 extern "C" {
 
 int dbslmm_abi_version(void) { return DBSLMM_ABI_VERSION; }
@@ -384,7 +401,7 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+        create_far_stream(device, &c->stream3) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
@@ -646,14 +663,18 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             only = p->h_tb[0];
             for (int32_t b : p->h_tb) if (mv[b] > mv[only]) only = b;
         }
-        int order = 0;   // 0: I / T, 1: I - T (longest remaining chain first), 2: I, 3: I - T / 2
+        int order = 0;   // 0: I / T - alpha T / Tmax, 1: I - T, 2: I, 3: I - T / 2
         if (const char* e = getenv("DBSLMM_TRSV_ORDER")) order = atoi(e);
+        double alpha = 0.25; // bigger blocks' tiles are claimed earlier (their chains are longer)
+        if (const char* e = getenv("DBSLMM_TRSV_ALPHA")) alpha = atof(e);
+        int tmx = 1;
+        for (int32_t b : p->h_tb) tmx = std::max(tmx, (mv[b] + trsv::kT - 1) / trsv::kT);
         for (int32_t b : p->h_tb) {
             if (only >= 0 && b != only) continue;
             const int T = (mv[b] + trsv::kT - 1) / trsv::kT;
             for (int I = 0; I < T; ++I) {
                 const double key = order == 1 ? I - T : order == 2 ? I : order == 3 ? I - 0.5 * T
-                                                                                      : static_cast<double>(I) / T;
+                                   : static_cast<double>(I) / T - alpha * T / tmx;
                 v.push_back({key, T, b, I});
             }
         }
@@ -1098,6 +1119,12 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
                 if (nr == 1) launch_trsv<1>(fwd, grid, st, a);
                 else launch_trsv<2>(fwd, grid, st, a);
                 HIP_TRY(ctx, hipGetLastError());
+                if (getenv("DBSLMM_TRSV_SYNC")) {   // diagnostics: one launch at a time
+                    fprintf(stderr, "trsv g%zu k%d pass%d nr%d n_items %d grid %d ...", g, k, pass, nr,
+                            a.n_items, grid);
+                    HIP_TRY(ctx, hipStreamSynchronize(st));
+                    fprintf(stderr, " done\n");
+                }
             }
         }
     }
