@@ -263,6 +263,22 @@ __device__ __forceinline__ void lds_to_acc(v4d (&acc)[2][2], const double* W, in
                 acc[si][sj][q] = W[(16 * si + (lane >> 4) + 4 * q) * kTS + 16 * sj + (lane & 15)];
 }
 
+// acc (a 32 x 32 piece of L at rows r0.., columns c0..) also stored transposed into the upper
+// triangle (rows c0.., columns r0..) for the row-streaming backward substitution (trsv.hip);
+// rows >= m (the bordered z row, padding) are not copied
+__device__ __forceinline__ void store_acc_t(const v4d (&acc)[2][2], double* A, int ld, int r0, int c0, int m,
+                                            int lane) {
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + 16 * si + (lane >> 4) + 4 * q;
+                if (r < m) A[static_cast<int64_t>(c0 + 16 * sj + (lane & 15)) * ld + r] = acc[si][sj][q];
+            }
+}
+
 // lower sub-tiles (a >= b) of a 128 x 128 region, 4 x 4 of 32
 __device__ __forceinline__ int rsub(int a, int b) { return a * (a + 1) / 2 + b; }
 constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X10 (2) + colb
@@ -396,6 +412,15 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             A[static_cast<int64_t>(gr) * ld + gc] = S[rr * kTS + cc];
         }
     }
+    for (int u = 0; u < 4; ++u) {      // the region's off-diagonal 64 x 64 tile L10, transposed
+        const int aa = 2 + (u >> 1), bb = u & 1;
+        const double* S = R + rsub(aa, bb) * kSub;
+        for (int e = tid; e < kT * kT; e += kLargeThreads) {
+            const int rr = e & 31, cc = e >> 5;
+            const int gr = c0 + kT * aa + rr, gc = c0 + kT * bb + cc;
+            if (gr < m && gc < m) A[static_cast<int64_t>(gc) * ld + gr] = S[rr * kTS + cc];
+        }
+    }
     for (int t = 0; t < 4; ++t) {      // diagonal + upper of the 32-level diagonal sub-tiles: X^T
         const int jm = min(kT, m - (c0 + kT * t));
         if (jm <= 0) break;
@@ -483,6 +508,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     zero_acc(acc);
     for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
     store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);           // L_i0
+    store_acc_t(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, m, lane);
     if (!two) return;
     __syncthreads();
     acc_to_lds(acc, W + (2 * qi + qj) * kSub, lane);
@@ -496,6 +522,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     zero_acc(acc);
     for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
     store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);     // L_i1
+    store_acc_t(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, m, lane);
 }
 
 // ---------------------------------------------------------------- 128 x 128 trailing update

@@ -48,6 +48,9 @@ constexpr int kMaxR = 2;                     // right-hand sides per launch
 constexpr int kNS = 16;                      // LDS ring slots (tiles) of handed-off vectors
 constexpr int kGrp = 8;                      // tiles the control wave stages per round trip
 constexpr size_t kLdsBytes = 96 * 1024;      // one workgroup per CU (sc1 hand-off condition)
+// the larger carve (backward): ring + w + z + transpose + ring words
+static_assert((kNS * kT * kMaxR + 2 * kT * kMaxR + kSW * 8 * kMaxR * (kT + 1)) * sizeof(double) + 64 <= kLdsBytes,
+              "TRSV LDS carve");
 
 struct Args {
     const double* M;             // the factored base copy
@@ -307,20 +310,23 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
     }
 }
 
-// Backward substitution L^T z = y, then the Chebyshev update of the tile's rows.  Streaming wave w
-// reads rows 8 w .. 8 w + 7 of each later tile J (lane = column of tile I): acc += L_JI^T z_J,
-// its 8 z_J values broadcast from the control wave's LDS ring; the 8 waves' partial sums meet in
-// LDS.
+// Backward substitution L^T z = y, then the Chebyshev update of the tile's rows.  It reads L^T
+// from the upper triangle (the panel / region kernels store each off-diagonal 64 x 64 tile of L
+// transposed there too), so it streams rows exactly like the forward kernel: wave w owns rows
+// 8 w .. 8 w + 7 of tile I, lane = column of the later tile J (J = T - 1 down to I + 1),
+// acc += (L^T)_IJ z_J with z_J from the control wave's LDS ring, then row sums through the
+// wave-private LDS transpose.
 template <int NR>
 __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args a) {
     using namespace trsv;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* ring = lds;                       // [kNS][64][NR]
-    double* red = ring + kNS * kT * NR;       // [8 waves][64][NR]
-    double* ws = red + kSW * kT * NR;         // [64][NR]
+    double* ws = ring + kNS * kT * NR;        // [64][NR]: y_I - sum_J (L^T)_IJ z_J
     double* zt = ws + kT * NR;                // [64][NR] this tile's z
-    Ring* rg = reinterpret_cast<Ring*>(zt + kT * NR);
+    double* rt = zt + kT * NR;                // [8 waves][8 NR][65]: lane partial sums (transpose)
+    Ring* rg = reinterpret_cast<Ring*>(rt + kSW * 8 * NR * (kT + 1));
     const int tid = threadIdx.x, row = tid >> 3, part = tid & 7, wave = tid >> 6, lane = tid & 63;
+    constexpr int kV = 8 * NR, kG = kT / kV;  // row sums per wave; lanes per row sum
     for (;;) {
         const int it = take_ticket(a, rg, tid);
         if (it >= a.n_items) break;
@@ -331,11 +337,6 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
         const int r0 = kT * I, jmax = min(kT, m - r0);
         const int32_t* flag = a.flags + a.foff[b];
         const int cnt = T - 1 - I;                // later tiles, taken from the last one down
-        // y_I for the final subtraction, read now (off the dependency chain)
-        double ysrc = 0.0;
-        if (tid < kT * NR && tid / NR < jmax)
-            ysrc = a.mode ? A[static_cast<int64_t>(m) * ld + r0 + tid]   // bordered row m: y = L^-1 z
-                          : a.src[(tid % NR) * a.vs + g0 + r0 + tid / NR];
         double xd[8];
         if (wave == kSW) {
             control<NR>(a, rg, ring, flag, g0, m, T - 1, -1, cnt, lane);
@@ -347,17 +348,24 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
                 const double x = A[static_cast<int64_t>(r0 + row) * ld + r0 + q];
                 xd[k] = (q >= row && q < jmax) ? x : 0.0;
             }
-            const double* Lw = A + static_cast<int64_t>(8 * wave) * ld + r0 + lane;
-            double acc[NR];
+            // this lane's share of y_I (value v = lane / kG), read now (off the dependency chain)
+            const int vv = lane / kG, vk = vv / NR, vc = vv - vk * NR, vr = 8 * wave + vk;
+            const double ysrc = vr >= jmax ? 0.0
+                                : a.mode ? A[static_cast<int64_t>(m) * ld + r0 + vr]   // bordered row m: y = L^-1 z
+                                         : a.src[vc * a.vs + g0 + r0 + vr];
+            const double* Uw = A + static_cast<int64_t>(r0 + 8 * wave) * ld + lane;   // rows of tile I
+            double acc[8][NR];
 #pragma unroll
-            for (int c = 0; c < NR; ++c) acc[c] = 0.0;
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int c = 0; c < NR; ++c) acc[k][c] = 0.0;
             double lr[kPF][8];
             auto issue = [&](int u, int t) {
-                const int j = T - 1 - t;
+                const int cj = kT * (T - 1 - t);          // columns of tile J: cj + lane < 64 T <= ld
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    const double x = Lw[static_cast<int64_t>(kT * j + k) * ld];   // rows < 64 T <= ld
-                    lr[u][k] = kT * j + 8 * wave + k < m ? x : 0.0;
+                    const double x = Uw[static_cast<int64_t>(k) * ld + cj];
+                    lr[u][k] = cj + lane < m ? x : 0.0;   // past m: bordered row / padding
                 }
             };
 #pragma unroll
@@ -369,26 +377,31 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
                     const int t = t0 + u;
                     if (t < cnt) {
                         wait_ready(rg, t);
-                        const double* z = ring + ((t % kNS) * kT + 8 * wave) * NR;
+                        const double* z = ring + ((t % kNS) * kT + lane) * NR;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
 #pragma unroll
-                            for (int c = 0; c < NR; ++c) acc[c] += lr[u][k] * z[k * NR + c];
+                            for (int c = 0; c < NR; ++c) acc[k][c] += lr[u][k] * z[c];
                         if (lane == 0) lds_put(&rg->done[wave], t + 1);
                         if (t + kPF < cnt) issue(u, t + kPF);
                     }
                 }
             }
+            double* rw = rt + wave * kV * (kT + 1);
 #pragma unroll
-            for (int c = 0; c < NR; ++c) red[(wave * kT + lane) * NR + c] = acc[c];
-        }
-        __syncthreads();
-        if (tid < kT * NR) {
-            const int col = tid / NR, c = tid - col * NR;
-            double s = 0.0;
+            for (int k = 0; k < 8; ++k)
 #pragma unroll
-            for (int w = 0; w < kSW; ++w) s += red[(w * kT + col) * NR + c];
-            ws[tid] = col < jmax ? ysrc - s : 0.0;
+                for (int c = 0; c < NR; ++c) rw[(k * NR + c) * (kT + 1) + lane] = acc[k][c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double sum = 0.0;
+            const int q0 = (lane % kG) * (kT / kG);
+#pragma unroll
+            for (int q = 0; q < kT / kG; ++q) sum += rw[vv * (kT + 1) + q0 + q];
+#pragma unroll
+            for (int sft = 1; sft < kG; sft <<= 1) sum += __shfl_xor(sum, sft);
+            if (lane % kG == 0) ws[vr * NR + vc] = vr < jmax ? ysrc - sum : 0.0;
         }
         __syncthreads();
         if (wave < kSW) {
