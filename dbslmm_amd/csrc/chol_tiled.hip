@@ -309,6 +309,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     double* A = a.M + a.blk_matoff[b];
     const double dshift = *a.dshift;
     const int c0 = 2 * kBT * reg;
+    STAMP_DECL
+    STAMP_BEGIN();
     double* R = lds;
     double* X32 = lds + 10 * kSub;
     double* X10 = lds + 14 * kSub;
@@ -348,6 +350,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     for (int u = 0; u < 3; ++u)
         if (wave + 4 * u < 10) acc_to_lds(acc[u], R + (wave + 4 * u) * kSub, lane);
     __syncthreads();
+    STAMP_END(0);
+    STAMP_BEGIN();
     // 2) four 32-column steps inside the region
     for (int t = 0; t < 4; ++t) {
         if (c0 + kT * t >= m) break;
@@ -357,6 +361,9 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             if (f && lane == 0) *fflag = 1;
         }
         __syncthreads();
+        if (t == 0) STAMP_END(7);
+        else STAMP_END(4);
+        STAMP_BEGIN();
         {   // panel: R[i][t] <- R[i][t] X_t^T
             const int i = t + 1 + wave;
             if (i <= 3 && c0 + kT * i <= m) {
@@ -367,6 +374,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             }
         }
         __syncthreads();
+        STAMP_END(5);
+        STAMP_BEGIN();
         {   // trailing: R[i][j] -= R[i][t] R[j][t]^T, t < j <= i <= 3
             const int nt = 3 - t, np = nt * (nt + 1) / 2;
             for (int pq = wave; pq < np; pq += 4) {
@@ -381,7 +390,11 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             }
         }
         __syncthreads();
+        STAMP_END(6);
+        STAMP_BEGIN();
     }
+    STAMP_END(1);
+    STAMP_BEGIN();
     // 3) 64-level inverse blocks: X10_p = -X_{2p+1} (L_{2p+1,2p} X_{2p}), p = wave (0, 1)
     if (wave < 2 && c0 + kBT * wave + kT <= m) {
         const int p = wave;
@@ -398,6 +411,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
         }
     }
     __syncthreads();
+    STAMP_END(2);
+    STAMP_BEGIN();
     // 4) write-back
     for (int q = 0; q < 10; ++q) {
         int aa = 0;
@@ -439,6 +454,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             A[static_cast<int64_t>(c0 + kBT * p + rr) * ld + c0 + kBT * p + kT + cc] = X[cc * kTS + rr];
         }
     }
+    STAMP_END(3);
     const bool fail = *fflag != 0;
     if (reg == 0 && !update) {
         chol::BlockArgs ba{a.blk_row0, a.blk_m, a.blk_ms, a.blk_ld, a.blk_matoff, a.blk_id, a.z_slot,

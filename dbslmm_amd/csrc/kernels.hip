@@ -61,24 +61,22 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* __restrict__ bas
     return __builtin_amdgcn_alignbyte(w1, w0, static_cast<uint32_t>(off & 3));
 }
 
-// Expand one packed dword (16 genotype codes, code j in bits 2j..2j+1) into 16 int8 dosages.
-// Output word k holds codes {k, 4+k, 8+k, 12+k} in bytes 0..3: individuals are stored in a
-// fixed within-16 permutation, which every Gram entry is invariant to (it sums over all
-// individuals of two rows stored the same way).  code 0 -> 2, 2 -> 1, 3 -> 0, 1 -> 0x80 (missing).
-__device__ __forceinline__ v4i expand16(uint32_t w, uint32_t valid_mask_2bit) {
-    // padding individuals (>= n_ref) must contribute 0: force their code to 3 (dosage 0)
-    w |= ~valid_mask_2bit & 0x55555555u;
-    w |= (~valid_mask_2bit & 0x55555555u) << 1;
+// The Gram operand Gp: per slot, kpad / 16 dwords of 2-bit DOSAGE codes (0, 1, 2; 3 = missing;
+// padding individuals 0), re-coded from the PLINK codes of one .bed dword (individual j in bits
+// 2j..2j+1; 00 -> 2, 10 -> 1, 11 -> 0, 01 -> missing: d0 = lo ^ hi, d1 = ~hi).  A quarter of the
+// bytes of an int8 operand; the Gram kernels expand it on the fly (expand_dose).
+__device__ __forceinline__ uint32_t dose_code16(uint32_t w, uint32_t valid_mask_2bit) {
+    const uint32_t lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
+    const uint32_t d0 = (lo ^ hi) & valid_mask_2bit, d1 = ~hi & valid_mask_2bit;
+    return d0 | (d1 << 1);
+}
+// One Gp dword -> 16 int8 codes.  Output word k holds individuals {k, 4+k, 8+k, 12+k} in bytes
+// 0..3: a fixed within-16 permutation, which every Gram entry is invariant to (both operands of
+// a product are expanded the same way).  Blocks without missing calls: the codes are the dosages.
+__device__ __forceinline__ v4i expand_dose(uint32_t w) {
     v4i out;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t y = (w >> (2 * k)) & 0x03030303u;
-        const uint32_t L = y & 0x01010101u;
-        const uint32_t H = (y >> 1) & 0x01010101u;
-        const uint32_t miss = L & ~H;
-        const uint32_t dose = 0x02020202u - L - H - miss;   // per byte: 2,1,0 or 0 for missing
-        out[k] = static_cast<int>(dose | (miss << 7));
-    }
+    for (int k = 0; k < 4; ++k) out[k] = static_cast<int>((w >> (2 * k)) & 0x03030303u);
     return out;
 }
 
@@ -86,7 +84,8 @@ __device__ __forceinline__ v4i expand16(uint32_t w, uint32_t valid_mask_2bit) {
 
 // ------------------------------------------------------------------------------------------
 // Kernel 1: unpack + per-SNP statistics.  One wave per slot (SNP row of a block), 4 waves/WG.
-//   G (optional)   [n_slots][kpad] int8; rows of padding slots (pos < 0) are written as zeros.
+//   Gp (optional)  [n_slots][kpad / 16] dosage-code dwords (dose_code16); padding slots (pos < 0)
+//                  and padding individuals are dosage 0.
 //   stat_*         exact integer statistics over the n_ref individuals.
 //   mu, rsd, S     fp64: mean over observed calls (= the imputation value, dtpr.cpp:358),
 //                  1/sd with the N-1 divisor (nomalizeVec), sum of observed dosages.
@@ -96,7 +95,7 @@ __device__ __forceinline__ v4i expand16(uint32_t w, uint32_t valid_mask_2bit) {
 extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
     const uint8_t* __restrict__ bed, int32_t n_ref, int64_t bytes_per_snp,
     const int32_t* __restrict__ slot_pos, const int32_t* __restrict__ slot_block, int32_t n_slots,
-    int8_t* __restrict__ G, int64_t kpad,
+    uint32_t* __restrict__ Gp, int64_t kpad,
     double* __restrict__ S_out, double* __restrict__ mu_out, double* __restrict__ rsd_out,
     double* __restrict__ maf_out, int32_t* __restrict__ block_flags) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -104,11 +103,10 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
     if (slot >= n_slots) return;
     const int32_t pos = slot_pos[slot];
     const int64_t n_words = kpad / 16;          // 16 individuals per lane-word
-    int8_t* grow = G ? G + static_cast<int64_t>(slot) * kpad : nullptr;
+    uint32_t* grow = Gp ? Gp + static_cast<int64_t>(slot) * n_words : nullptr;
     if (pos < 0) {                              // padding slot
         if (grow)
-            for (int64_t w = lane; w < n_words; w += kWave)
-                *reinterpret_cast<v4i*>(grow + 16 * w) = v4i{0, 0, 0, 0};
+            for (int64_t w = lane; w < n_words; w += kWave) grow[w] = 0u;
         if (lane == 0) {
             if (S_out) S_out[slot] = 0.0;
             if (mu_out) mu_out[slot] = 0.0;
@@ -134,7 +132,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
         cnt += __builtin_popcount(vmask) - n_miss;
         sum += 2 * n_two + n_one;
         sq += 4 * n_two + n_one;
-        if (grow) *reinterpret_cast<v4i*>(grow + first) = expand16(word, vmask);
+        if (grow) grow[w] = dose_code16(word, vmask);
     }
     cnt = wave_sum_i32(cnt);
     sum = wave_sum_i32(sum);
@@ -178,58 +176,56 @@ __device__ __forceinline__ int copy_hi(int m, int32_t tmin, int32_t tcopy, int32
 }
 
 // One 32 x 32 output tile (rows r0.., cols c0.. of block-local slots) on one wave, K over all
-// kpad individuals with operands straight from G (L2).  missing: the four products GG, GO, OG,
-// OO of the observed-call expansion.
+// kpad individuals with operands straight from Gp (L2).  Per 128 individuals (8 Gp dwords) lane
+// (row, h = lane >> 5) loads dwords 4 h .. 4 h + 3 of its row and feeds dword 4 h + s to MFMA s:
+// both operands use the same individual -> k map, so every product sums each individual once.
+// missing: the four products GG, GO, OG, OO of the observed-call expansion.
 __device__ __forceinline__ void gram_tile32(
-    const int8_t* __restrict__ G, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
+    const uint32_t* __restrict__ Gp, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
     int r0, int c0, int lane, const double* __restrict__ S, const double* __restrict__ mu,
     const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M,
     int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
-    const int8_t* pa = G + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kpad + 16 * (lane >> 5);
-    const int8_t* pb = G + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kpad + 16 * (lane >> 5);
+    const int64_t kw = kpad / 16;                 // Gp dwords per slot (kpad: a multiple of 128)
+    const uint32_t* pa = Gp + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kw + 4 * (lane >> 5);
+    const uint32_t* pb = Gp + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kw + 4 * (lane >> 5);
 
     v16i acc = {0};
     v16i acc_go = {0}, acc_og = {0}, acc_oo = {0};
     if (!missing) {
-        int64_t k = 0;
-        for (; k + 128 <= kpad; k += 128) {
-            const v4i a0 = *reinterpret_cast<const v4i*>(pa + k);
-            const v4i b0 = *reinterpret_cast<const v4i*>(pb + k);
-            const v4i a1 = *reinterpret_cast<const v4i*>(pa + k + 32);
-            const v4i b1 = *reinterpret_cast<const v4i*>(pb + k + 32);
-            const v4i a2 = *reinterpret_cast<const v4i*>(pa + k + 64);
-            const v4i b2 = *reinterpret_cast<const v4i*>(pb + k + 64);
-            const v4i a3 = *reinterpret_cast<const v4i*>(pa + k + 96);
-            const v4i b3 = *reinterpret_cast<const v4i*>(pb + k + 96);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a2, b2, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a3, b3, acc, 0, 0, 0);
-        }
-        for (; k < kpad; k += 32) {
-            const v4i a0 = *reinterpret_cast<const v4i*>(pa + k);
-            const v4i b0 = *reinterpret_cast<const v4i*>(pb + k);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc, 0, 0, 0);
+        for (int64_t w = 0; w < kw; w += 8) {
+            const v4i wa = *reinterpret_cast<const v4i*>(pa + w);
+            const v4i wb = *reinterpret_cast<const v4i*>(pb + w);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(expand_dose(static_cast<uint32_t>(wa[q])),
+                                                            expand_dose(static_cast<uint32_t>(wb[q])), acc, 0, 0, 0);
         }
     } else {
-        // x = dosage or 0x80: g = x & 3 (0 for missing), o = 1 - (x >> 7)
-        for (int64_t k = 0; k < kpad; k += 32) {
-            const v4i a0 = *reinterpret_cast<const v4i*>(pa + k);
-            const v4i b0 = *reinterpret_cast<const v4i*>(pb + k);
+        // code y = dosage or 3 (missing): m = y & (y >> 1), g = y without the missing, o = 1 - m
+        for (int64_t w = 0; w < kw; w += 8) {
+          const v4i wa = *reinterpret_cast<const v4i*>(pa + w);
+          const v4i wb = *reinterpret_cast<const v4i*>(pb + w);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const v4i a0 = expand_dose(static_cast<uint32_t>(wa[s4]));
+            const v4i b0 = expand_dose(static_cast<uint32_t>(wb[s4]));
             v4i ga, oa, gb, ob;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t xa = static_cast<uint32_t>(a0[q]);
                 const uint32_t xb = static_cast<uint32_t>(b0[q]);
-                ga[q] = static_cast<int>(xa & 0x03030303u);
-                gb[q] = static_cast<int>(xb & 0x03030303u);
-                oa[q] = static_cast<int>((~xa >> 7) & 0x01010101u);
-                ob[q] = static_cast<int>((~xb >> 7) & 0x01010101u);
+                const uint32_t ma = xa & (xa >> 1) & 0x01010101u;
+                const uint32_t mb = xb & (xb >> 1) & 0x01010101u;
+                ga[q] = static_cast<int>(xa & ~(3u * ma));
+                gb[q] = static_cast<int>(xb & ~(3u * mb));
+                oa[q] = static_cast<int>(ma ^ 0x01010101u);
+                ob[q] = static_cast<int>(mb ^ 0x01010101u);
             }
             acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ga, gb, acc, 0, 0, 0);
             acc_go = __builtin_amdgcn_mfma_i32_32x32x32_i8(ga, ob, acc_go, 0, 0, 0);
             acc_og = __builtin_amdgcn_mfma_i32_32x32x32_i8(oa, gb, acc_og, 0, 0, 0);
             acc_oo = __builtin_amdgcn_mfma_i32_32x32x32_i8(oa, ob, acc_oo, 0, 0, 0);
+          }
         }
     }
 
@@ -264,7 +260,7 @@ __device__ __forceinline__ void gram_tile32(
 }
 
 extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
-    const int8_t* __restrict__ G, int64_t kpad,
+    const uint32_t* __restrict__ Gp, int64_t kpad,
     const GramTile* __restrict__ tiles, int32_t n_tiles,
     const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
     const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
@@ -277,7 +273,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
     if (t >= n_tiles) return;
     const GramTile tile = tiles[t];
     const int b = tile.block;
-    gram_tile32(G, kpad, blk_row0[b], blk_m[b], blk_ld[b], blk_matoff[b], (block_flags[b] & 1) != 0,
+    gram_tile32(Gp, kpad, blk_row0[b], blk_m[b], blk_ld[b], blk_matoff[b], (block_flags[b] & 1) != 0,
                 kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride,
                 tmin, tcopy);
 }
@@ -302,7 +298,7 @@ constexpr int kLdsBytes = 2 * 2 * kOpBytes;   // 2 stages x (A, B) = 73,728 B
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
-    const int8_t* __restrict__ G, int64_t kpad,
+    const uint32_t* __restrict__ Gp, int64_t kpad,
     const GramTile* __restrict__ tiles, int32_t n_tiles,
     const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
     const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
@@ -326,33 +322,35 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
             if (diag && sj > si) continue;
             const int r0 = kGT * tile.ti + 32 * si, c0 = kGT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
-            gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
+            gram_tile32(Gp, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
                         tau, M, ncopy, cstride, tmin, tcopy);
         }
         return;
     }
-    const int8_t* ga = G + static_cast<int64_t>(row0 + kGT * tile.ti) * kpad;
-    const int8_t* gb = G + static_cast<int64_t>(row0 + kGT * tile.tj) * kpad;
-    // staging map: 128 rows x 8 chunks of 16 B per operand; thread t moves chunks t + 256 q.
-    // Two register sets: the global loads of stage s + 2 are issued before stage s's MFMAs.
-    v4i ra0[4], rb0[4], ra1[4], rb1[4];
-    auto gload = [&](v4i (&ra)[4], v4i (&rb)[4], int st) {
-        const int64_t k0 = static_cast<int64_t>(st) * kKS;
+    const int64_t kw = kpad / 16;
+    const uint32_t* ga = Gp + static_cast<int64_t>(row0 + kGT * tile.ti) * kw;
+    const uint32_t* gb = Gp + static_cast<int64_t>(row0 + kGT * tile.tj) * kw;
+    // staging map: 128 rows x 8 Gp dwords (16 individuals each) per operand; thread t moves dwords
+    // t + 256 q and expands them to 16 B of int8 codes on the way into LDS.  Two register sets:
+    // the global loads of stage s + 2 are issued before stage s's MFMAs.
+    uint32_t ra0[4], rb0[4], ra1[4], rb1[4];
+    auto gload = [&](uint32_t (&ra)[4], uint32_t (&rb)[4], int st) {
+        const int64_t w0 = static_cast<int64_t>(st) * (kKS / 16);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = q * 256 + tid, r = e >> 3, c = e & 7;
-            ra[q] = *reinterpret_cast<const v4i*>(ga + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
-            if (!diag) rb[q] = *reinterpret_cast<const v4i*>(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c);
+            ra[q] = ga[static_cast<int64_t>(r) * kw + w0 + c];
+            if (!diag) rb[q] = gb[static_cast<int64_t>(r) * kw + w0 + c];
         }
     };
-    auto lstore = [&](const v4i (&ra)[4], const v4i (&rb)[4], int buf) {
+    auto lstore = [&](const uint32_t (&ra)[4], const uint32_t (&rb)[4], int buf) {
         int8_t* A = glds + buf * 2 * kOpBytes;
         int8_t* B = A + kOpBytes;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = q * 256 + tid, r = e >> 3, c = e & 7;
-            *reinterpret_cast<v4i*>(A + r * kRS + 16 * c) = ra[q];
-            if (!diag) *reinterpret_cast<v4i*>(B + r * kRS + 16 * c) = rb[q];
+            *reinterpret_cast<v4i*>(A + r * kRS + 16 * c) = expand_dose(ra[q]);
+            if (!diag) *reinterpret_cast<v4i*>(B + r * kRS + 16 * c) = expand_dose(rb[q]);
         }
     };
     const int wr = wave >> 1, wc = wave & 1;
@@ -429,29 +427,26 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 // ------------------------------------------------------------------------------------------
 // Kernel 2c: the Gram of the big blocks (m >= 384), 256 x 256 output tile per 512-thread
 // workgroup: wave w computes rows 64 (w & 3) .., columns 128 (w >> 2) .. (2 x 4 MFMA 32x32x32
-// i8 tiles, 128 accumulator registers).  K runs in 64-byte stages through a 3-slot LDS ring
-// filled by LDS-DMA (global_load_lds_dwordx4: no staging registers), two stages in flight:
-// per stage each wave issues its DMA pieces for stage st + 2, waits with a counted vmcnt for
-// stage st, raw s_barrier (a __syncthreads() would drain the DMAs in flight), 16 MFMAs, barrier.
-// The LDS image is lane-linear per DMA piece (1 KiB = 16 rows x 64 B, unpadded), swizzled through
-// the SOURCE address: position p of row r holds K chunk p ^ ((r >> 2) & 3), which puts the 16
-// rows of every ds_read_b128 lane group on 16 distinct bank groups.  Diagonal tiles stage one
-// operand; waves whose 64 x 128 piece is strictly upper skip the MFMAs.  Missing-call blocks:
+// i8 tiles, 128 accumulator registers).  K runs in stages of 64 individuals: every thread loads
+// one row's 4 Gp dwords (16 B, two stages ahead in registers) and expands them to 64 B of int8
+// codes in a double-buffered LDS stage (a quarter of the HBM / L2 operand traffic of an int8
+// image), raw s_barrier per stage, 16 MFMAs per wave.  Position p of LDS row r holds K chunk
+// p ^ ((r >> 2) & 3), which puts the 16 rows of every ds_read_b128 lane group on 16 distinct
+// bank groups.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
+// skip the MFMAs.  Missing-call blocks:
 // exact 4-product path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
 namespace gram {
 constexpr int kHT = 256;                   // output tile edge
 constexpr int kHK = 64;                    // individuals (bytes) per K stage = one row chunk set
 constexpr int kHOp = kHT * kHK;            // one operand stage (16 KiB)
-constexpr int kHSlots = 3;                 // LDS ring depth
-constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 96 KiB
-typedef __attribute__((address_space(1))) const void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
+constexpr int kHSlots = 2;                 // LDS double buffer
+constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 64 KiB
 __device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r >> 2) & 3)); }
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
-    const int8_t* __restrict__ G, int64_t kpad,
+    const uint32_t* __restrict__ Gp, int64_t kpad,
     const GramTile* __restrict__ tiles, int32_t n_tiles,
     const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
     const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
@@ -475,28 +470,29 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             if (diag && sj > si) continue;
             const int r0 = kHT * tile.ti + 32 * si, c0 = kHT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
-            gram_tile32(G, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
+            gram_tile32(Gp, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
                         tau, M, ncopy, cstride, tmin, tcopy);
         }
         return;
     }
-    const int8_t* ga = G + static_cast<int64_t>(row0 + kHT * tile.ti) * kpad;
-    const int8_t* gb = G + static_cast<int64_t>(row0 + kHT * tile.tj) * kpad;
-    // DMA pieces: wave w fills rows 32 w .. 32 w + 31 of each operand (two 16-row pieces)
-    const int prow = lane >> 2, ppos = lane & 3;
-    auto issue = [&](int st) {
-        int8_t* slot = hlds + (st % kHSlots) * 2 * kHOp;
-        const int64_t k0 = static_cast<int64_t>(st) * kHK;
+    // staging: thread t -> operand t >> 8, row t & 255; per stage (64 individuals) one 16-B load
+    // of 4 Gp dwords, expanded on the way into LDS (4 ds_write_b128, swizzled: logical chunk c of
+    // row r at position c ^ ((r >> 2) & 3), which spreads every ds_read_b128 lane group over 16
+    // distinct bank groups).  Loads run two stages ahead in two register sets.
+    const int64_t kw = kpad / 16;
+    const int sop = tid >> 8, srow = tid & 255;
+    const bool stager = !(diag && sop == 1);
+    const uint32_t* gs = Gp + static_cast<int64_t>(row0 + kHT * (sop ? tile.tj : tile.ti) + srow) * kw;
+    const int nst = static_cast<int>(kpad / kHK);   // even: kpad is a multiple of 128
+    // unconditional loads (clamped stage, valid rows for every thread) keep the vmcnt bookkeeping
+    // exact: one newer load in flight at every use
+    auto gload = [&](int st) -> v4i { return *reinterpret_cast<const v4i*>(gs + 4 * min(st, nst - 1)); };
+    auto lstore = [&](const v4i& pk, int st) {
+        if (!stager) return;
+        int8_t* slot = hlds + (st & 1) * 2 * kHOp + sop * kHOp;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int r = 32 * wave + 16 * j + prow;
-            const int c = ppos ^ ((r >> 2) & 3);
-            __builtin_amdgcn_global_load_lds((gptr_t)(ga + static_cast<int64_t>(r) * kpad + k0 + 16 * c),
-                                             (lptr_t)(slot + (32 * wave + 16 * j) * kHK), 16, 0, 0);
-            if (!diag)
-                __builtin_amdgcn_global_load_lds((gptr_t)(gb + static_cast<int64_t>(r) * kpad + k0 + 16 * c),
-                                                 (lptr_t)(slot + kHOp + (32 * wave + 16 * j) * kHK), 16, 0, 0);
-        }
+        for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<v4i*>(slot + swz(srow, c)) = expand_dose(static_cast<uint32_t>(pk[c]));
     };
     const int wr = wave & 3, wc = wave >> 2;       // rows 64 wr .., columns 128 wc ..
     const bool idle = diag && 128 * wc >= 64 * wr + 64;
@@ -508,7 +504,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     const int rsub = lane & 31, csub = lane >> 5;   // row in a 32-row group, 16-B half of a k-step
     auto compute = [&](int st) {
         if (idle) return;
-        const int8_t* A = hlds + (st % kHSlots) * 2 * kHOp;
+        const int8_t* A = hlds + (st & 1) * 2 * kHOp;
         const int8_t* B = diag ? A : A + kHOp;
 #pragma unroll
         for (int kk = 0; kk < kHK / 32; ++kk) {
@@ -527,25 +523,24 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
                     acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
         }
     };
-    const int nst = static_cast<int>(kpad / kHK);
-    issue(0);
-    if (nst > 1) issue(1);
-    for (int st = 0; st < nst; ++st) {
-        if (st + 2 < nst) {
-            issue(st + 2);
-            // this wave's DMAs for stages st+1 and st+2 may stay in flight
-            if (diag) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else if (st + 1 < nst) {
-            if (diag) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();               // stage st is in LDS (every wave waited)
+    v4i p0 = gload(0), p1 = gload(1);
+    lstore(p0, 0);
+    p0 = gload(2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // raw barriers: a __syncthreads() would also drain the loads in flight.  The tail's extra
+    // expansions land in the slot no later stage reads.
+    for (int st = 0; st < nst; st += 2) {
+        lstore(p1, st + 1);                   // stage st is in slot 0
+        p1 = gload(st + 3);
         compute(st);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();               // slot st % 3 may be refilled
+        __builtin_amdgcn_s_barrier();
+        lstore(p0, st + 2);                   // stage st + 1 is in slot 1
+        p0 = gload(st + 4);
+        compute(st + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
     if (idle) return;
     const double scale = tau / n_ref_d;

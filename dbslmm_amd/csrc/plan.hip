@@ -7,7 +7,7 @@
 //             [small SNPs | large SNPs | padding]; per slot: bed row (-1 = pad), block,
 //             z-score, output index (>= 0 small, -1-i large); slot m of a block doubles as
 //             the row that carries z through the bordered Cholesky
-//   G         int8 [n_slots + 128][kpad] dosages, kpad = roundup(n_ref, 128)
+//   Gp        [n_slots + 256][kpad / 16] dwords of 2-bit dosage codes, kpad = roundup(n_ref, 128)
 //   M         fp64 per block ld x ld row-major, lower triangle; row m = z (written by the solve)
 //   stats     S, mu, 1/sd per slot; y (solve scratch) per slot; flags/status per block
 // The whole problem stays resident; plan_run re-executes unpack -> gram -> chol from the
@@ -84,7 +84,7 @@ struct dbslmm_plan {
     int64_t M_elems = 0;
     // device
     uint8_t* d_bed = nullptr;
-    int8_t* d_G = nullptr;
+    uint32_t* d_G = nullptr;   // Gp: 2-bit dosage codes, kpad / 16 dwords per slot
     int32_t *d_slot_pos = nullptr, *d_slot_block = nullptr, *d_slot_out = nullptr;
     double *d_z = nullptr, *d_S = nullptr, *d_mu = nullptr, *d_rsd = nullptr, *d_y = nullptr;
     int32_t *d_flags = nullptr, *d_status = nullptr, *d_order = nullptr, *d_blk_id = nullptr;
@@ -698,7 +698,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     const double n_snp = static_cast<double>(p->n_s + p->n_l);
     p->wl[0] = n_snp;
     p->wl[1] = n_snp * bps;
-    p->wl[2] = static_cast<double>(p->n_slots) * p->kpad;
+    p->wl[2] = static_cast<double>(p->n_slots) * (p->kpad / 4);   // Gp bytes the unpack writes
     p->wl[3] = ops_alg;
     p->wl[4] = ops_exec;
     p->wl[5] = chol_flops_large;
@@ -725,7 +725,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = hipMemset(p->d_bed, 0, pr->bed_len + 16)) != hipSuccess) return fail("hipMemset bed");
     if ((e = hipMemcpy(p->d_bed, pr->bed, pr->bed_len, hipMemcpyHostToDevice)) != hipSuccess) return fail("upload bed");
     // + kHT spare rows: a 256-row Gram tile may read past the last slot (results discarded)
-    const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kHT) * p->kpad;
+    const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kHT) * (p->kpad / 4);
     if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
     if ((e = hipMemset(p->d_G, 0, g_bytes)) != hipSuccess) return fail("hipMemset G");
     if ((e = dev_upload(&p->d_slot_pos, slot_pos)) != hipSuccess) return fail("upload slots");
