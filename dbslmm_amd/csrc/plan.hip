@@ -989,6 +989,8 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
     const double nobs = static_cast<double>(p->n_obs);
     const double db = 1.0 / (sigmas[cp.base] * nobs);
     const double floor_ = db + 1.0 - p->tau;
+    double tol = 1e-13;
+    if (const char* e = getenv("DBSLMM_CHEB_TOL")) tol = std::max(1e-16, atof(e));
     for (int c = 0; c < n; ++c)
         if (c != cp.base) cp.others.push_back(c);
     for (size_t g0 = 0; g0 < cp.others.size(); g0 += trsv::kMaxR) {
@@ -1003,10 +1005,11 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
             hi[j] = std::max(1.0, 1.0 + ext) * (1.0 + 1e-6);
             if (!(lo[j] > 0.0)) return false;
             // Chebyshev: error <= 2 q^K x the initial error x_c - x_b, itself <= |ext| relative
-            // (the same bound); K so that the final error is 1e-14 of the solution
+            // (the same bound); K so that the final error is 1e-13 of the solution (below the
+            // forward error of the fp64 Cholesky solve itself; env DBSLMM_CHEB_TOL overrides)
             const double kap = hi[j] / lo[j], q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
             const double e0 = std::max(std::fabs(ext), 1e-300);
-            const int k = q < 1e-300 ? 1 : std::max(1, static_cast<int>(std::ceil(std::log(0.5e-14 / e0) / std::log(q))));
+            const int k = q < 1e-300 ? 1 : std::max(1, static_cast<int>(std::ceil(std::log(tol / e0) / std::log(q))));
             K = std::max(K, k);
         }
         if (K > 60) return false;
