@@ -201,14 +201,17 @@ __device__ __forceinline__ bool factor_tile_lds(double* T, double* Xo, double* c
             fail |= !(p > 0.0);
             const double rs = rsqrt_f64(p);
             v[j] = (!xlane && r < j) ? 0.0 : v[j] * rs;
-            if (!xlane) colb[r] = v[j];
-            wave_sync();
+            // column j through LDS: one wave, so its LDS operations execute in issue order, and
+            // the compiler keeps the store / loads (possibly aliasing addresses) in program order
+            // -- no wave barrier between the steps, so step j + 1's pivot overlaps step j's FMAs
+            double* cb = colb + kT * (j & 1);   // alternate buffers: no write-after-read on reuse
+            if (!xlane) cb[r] = v[j];
 #pragma unroll
             for (int k0 = (j + 1) & ~7; k0 < kT; k0 += 8) {
                 double col[8];
 #pragma unroll
                 for (int k = 0; k < 8; k += 2) {
-                    const v2d t = *reinterpret_cast<const v2d*>(colb + k0 + k);
+                    const v2d t = *reinterpret_cast<const v2d*>(cb + k0 + k);
                     col[k] = t[0];
                     col[k + 1] = t[1];
                 }
@@ -216,7 +219,6 @@ __device__ __forceinline__ bool factor_tile_lds(double* T, double* Xo, double* c
                 for (int k = 0; k < 8; ++k)
                     if (k0 + k > j) v[k0 + k] -= v[j] * col[k];
             }
-            wave_sync();
         }
     }
     if (!xlane) {

@@ -131,6 +131,11 @@ struct dbslmm_plan {
     // iteration vectors [Y, Z, X, R, D, S] x kMaxR x n_slots
     int32_t *d_tri_f = nullptr, *d_tri_b = nullptr, *d_foff = nullptr, *d_tflags = nullptr, *d_tb = nullptr;
     int32_t n_titems = 0, n_tflags = 0;
+    // h2f split: the tiled blocks whose factorisation ends in the first part of the sequence
+    // ("early": their items first in d_tri_f / d_tri_b, their blocks first in d_tb) run their
+    // backward solve and Chebyshev iterations on the main stream as soon as the sequence has
+    // recorded tev[early_ev], overlapping the chain-bound rest of the big blocks' factorisation
+    int32_t n_titems_early = 0, n_tb_early = 0, early_ev = -1;
     int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
     unsigned long long* d_stamps = nullptr;  // diagnostics only (DBSLMM_TRSV_STAMPS; not owned)
@@ -185,11 +190,32 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 // super steps starts later, so its heavy first steps overlap the largest block's latency-bound
 // last steps -- no gain measured at configs 3-5).  Each work item is two int32:
 // [block / tile, (local step << 8) | pending panels or K multiple].
-static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
-                        int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
-    struct Blk { int32_t bq; int T64, Tz64, T2, Tz2, nr, S, off; };
+// env DBSLMM_CHEB_SPLIT=1: the early group's substitutions overlap the factorisation's tail.
+// Off by default -- measured at config 4 (56.7 ms/step without): the persistent substitution
+// workgroups hold whole CUs (96 KiB LDS each) for the length of a launch, the chain kernels of
+// the big blocks wait for CUs, and the factorisation grows from 29 to 34-43 ms (n_cu / 2 .. n_cu
+// substitution workgroups), more than the 5.5 ms the later substitutions save.
+static bool cheb_split() {
+    const char* e = getenv("DBSLMM_CHEB_SPLIT");
+    return e && atoi(e) != 0;
+}
+
+// regions (128 columns) per super step (env DBSLMM_SUPER)
+static int tiled_R() {
     int R = 2;
     if (const char* e = getenv("DBSLMM_SUPER")) R = std::max(1, std::min(8, atoi(e)));
+    return R;
+}
+
+// g_early >= 0: record event 2 G + 2 on the chain stream after super step g_early's regions and
+// panels (every block whose last super step is <= g_early is then fully factored); *ev_out = its
+// index, or -1
+static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
+                        int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist, int g_early = -1,
+                        int* ev_out = nullptr) {
+    struct Blk { int32_t bq; int T64, Tz64, T2, Tz2, nr, S, off; };
+    const int R = tiled_R();
+    if (ev_out) *ev_out = -1;
     bool right = false;     // measured: no gain at configs 3-5 (the sequence is throughput-bound)
     if (const char* e = getenv("DBSLMM_ALIGN")) right = atoi(e) != 0;
     int run2 = chol::kRun2;
@@ -273,6 +299,10 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
                 }
             region_launch(rv);
             panel_launch(pv);
+        }
+        if (g == g_early && !right) {
+            sync(kTlRecord, 2 * G + 2, 0);
+            if (ev_out) *ev_out = 2 * G + 2;
         }
         // trailing: 128 x 128 tiles (I, J) right of the super step, rl + jlo <= J <= rl + jhi, LPT
         // over per-XCD queues by tile row
@@ -631,6 +661,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                 order.end());
     for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
     std::vector<int32_t> tlist;
+    std::vector<char> is_early(std::max(1, p->n_nonempty), 0);
     {
         std::vector<int32_t> tb;
         for (int b = 0; b < p->n_nonempty; ++b)
@@ -638,7 +669,26 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         p->n_tiled = static_cast<int32_t>(tb.size());
         p->h_m = mv;
         p->h_tb = tb;
-        build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist);
+        // h2f split (env DBSLMM_CHEB_SPLIT=1, see cheb_split): blocks whose last super step is at
+        // most g_early = DBSLMM_SPLIT_FRAC (0.5) of the sequence form the early group
+        const int R = tiled_R();
+        auto last_step = [&](int32_t b) {
+            const int T64 = (mv[b] + chol::kBT - 1) / chol::kBT;
+            return ((T64 + 1) / 2 + R - 1) / R - 1;
+        };
+        int G = 0;
+        for (int32_t b : tb) G = std::max(G, last_step(b) + 1);
+        int g_early = -1;
+        if (cheb_split() && G > 1) {
+            double frac = 0.5;
+            if (const char* e = getenv("DBSLMM_SPLIT_FRAC")) frac = atof(e);
+            g_early = static_cast<int>(frac * (G - 1));
+            int ne = 0;
+            for (int32_t b : tb) ne += last_step(b) <= g_early;
+            if (ne == 0 || ne == static_cast<int>(tb.size())) g_early = -1;
+        }
+        for (int32_t b : tb) is_early[b] = g_early >= 0 && last_step(b) <= g_early;
+        build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist, g_early, &p->early_ev);
     }
     // substitution work lists (trsv.hip): 64-row tiles of the tiled blocks; forward in order of
     // (tile, block), backward in order of (tiles from the end, block) -- every dependency of an
@@ -678,9 +728,12 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                 v.push_back({key, T, b, I});
             }
         }
-        std::stable_sort(v.begin(), v.end(), [](const It& x, const It& y) {
+        // early group first (its launches take the prefix of the lists)
+        std::stable_sort(v.begin(), v.end(), [&](const It& x, const It& y) {
+            if (is_early[x.b] != is_early[y.b]) return is_early[x.b] > is_early[y.b];
             return x.key != y.key ? x.key < y.key : x.T > y.T;
         });
+        for (const It& x : v) p->n_titems_early += is_early[x.b] ? 1 : 0;
         for (const It& x : v) {
             tri_f.push_back(x.b);
             tri_f.push_back(x.I);
@@ -746,9 +799,16 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_tri_f, tri_f)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_tri_b, tri_b)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_foff, foff)) != hipSuccess) return fail("upload trsv lists");
-    if ((e = dev_upload(&p->d_tb, p->h_tb)) != hipSuccess) return fail("upload trsv lists");
-    if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 2) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
-    if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 2) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
+    {
+        std::vector<int32_t> tbg;
+        for (int32_t b : p->h_tb) if (is_early[b]) tbg.push_back(b);
+        p->n_tb_early = static_cast<int32_t>(tbg.size());
+        for (int32_t b : p->h_tb) if (!is_early[b]) tbg.push_back(b);
+        if ((e = dev_upload(&p->d_tb, tbg)) != hipSuccess) return fail("upload trsv lists");
+    }
+    // [tile flags | ticket counter | error word | ticket counter of the early group's launches]
+    if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
+    if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
     if ((e = hipMalloc(&p->d_mu, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -893,9 +953,36 @@ static bool persistent_bwd() {   // env DBSLMM_PBWD=0: the per-tile backward lau
 
 // Backward substitution of factorisation copy `copy`'s tiled blocks in one persistent launch
 // (trsv.hip, plain mode): y = the bordered z row, x -> y scratch of the copy, beta of the copy.
-static int run_pbwd(dbslmm_plan* p, double isn, int copy) {
+// A set of tiled blocks whose substitutions run as one launch sequence: items [item_off,
+// item_off + n_items) of d_tri_f / d_tri_b, blocks [tb_off, tb_off + n_tb) of d_tb, on stream st
+// with ticket counter ctr
+struct TGroup {
+    int32_t item_off, n_items, tb_off, n_tb;
+    hipStream_t st;
+    int32_t* ctr;
+    int grid;
+};
+static TGroup tgroup_all(const dbslmm_plan* p) {
+    return TGroup{0, p->n_titems, 0, p->n_tiled, p->ctx->stream2, p->d_tflags + p->n_tflags,
+                  std::max(1, std::min(p->ctx->n_cu, p->n_titems))};
+}
+static TGroup tgroup_late(const dbslmm_plan* p) {
+    const int32_t n = p->n_titems - p->n_titems_early;
+    return TGroup{p->n_titems_early, n, p->n_tb_early, p->n_tiled - p->n_tb_early, p->ctx->stream2,
+                  p->d_tflags + p->n_tflags, std::max(1, std::min(p->ctx->n_cu, n))};
+}
+// the early group shares the GPU with the rest of the tiled sequence: at most DBSLMM_SPLIT_GRID
+// (default n_cu / 2) workgroups, so the chain kernels of the big blocks keep CUs
+static TGroup tgroup_early(const dbslmm_plan* p) {
+    int cap = p->ctx->n_cu / 2;
+    if (const char* e = getenv("DBSLMM_SPLIT_GRID")) cap = std::max(1, atoi(e));
+    return TGroup{0, p->n_titems_early, 0, p->n_tb_early, p->ctx->stream, p->d_tflags + p->n_tflags + 2,
+                  std::max(1, std::min(cap, p->n_titems_early))};
+}
+
+static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     dbslmm_ctx* ctx = p->ctx;
-    hipStream_t st = ctx->stream2;
+    hipStream_t st = grp.st;
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
     if (!p->d_cheb) HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
     const int64_t c = copy;
@@ -908,12 +995,12 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy) {
     a.row0 = p->d_row0;
     a.blk_id = p->d_blk_id;
     a.slot_out = p->d_slot_out;
-    a.items = p->d_tri_b;
-    a.n_items = p->n_titems;
-    a.grid = std::max(1, std::min(ctx->n_cu, p->n_titems));
+    a.items = p->d_tri_b + 2 * grp.item_off;
+    a.n_items = grp.n_items;
+    a.grid = grp.grid;
     a.foff = p->d_foff;
     a.flags = p->d_tflags;
-    a.ctr = p->d_tflags + p->n_tflags;
+    a.ctr = grp.ctr;
     a.err = p->d_tflags + p->n_tflags + 1;
     a.vs = vs;
     a.dst = p->d_cheb + trsv::kMaxR * vs;          // the Z hand-off buffer
@@ -931,7 +1018,7 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy) {
         p->trsv_epoch = 1;
     }
     a.epoch = p->trsv_epoch;
-    launch_trsv<1>(false, a.grid, st, a);
+    if (a.n_items > 0) launch_trsv<1>(false, a.grid, st, a);
     HIP_TRY(ctx, hipGetLastError());
     return DBSLMM_OK;
 }
@@ -944,7 +1031,7 @@ static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
     const bool pb = persistent_bwd();
     if (!tiled_use_graph()) {
         const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy, pb);
-        return rc != DBSLMM_OK || !pb ? rc : run_pbwd(p, isn, copy);
+        return rc != DBSLMM_OK || !pb ? rc : run_pbwd(p, isn, copy, tgroup_all(p));
     }
     if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
     hipGraphExec_t& gx = p->graph_copy[copy];
@@ -963,7 +1050,7 @@ static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
         HIP_TRY(ctx, ie);
     }
     HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
-    return pb ? run_pbwd(p, isn, copy) : DBSLMM_OK;
+    return pb ? run_pbwd(p, isn, copy, tgroup_all(p)) : DBSLMM_OK;
 }
 
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
@@ -1041,9 +1128,11 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
 
 // Chebyshev iterations of the non-base copies on the base copy's factor (stream2, after the
 // base copy's tiled sequence): every tiled block of copy c gets its beta and status.
-static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
+
+// Chebyshev coefficients and iteration vectors: uploaded / allocated on stream st before any
+// group's iterations (run_impl: on the main stream ahead of the fork)
+static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
     dbslmm_ctx* ctx = p->ctx;
-    hipStream_t st = ctx->stream2;
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
     if (!p->d_cheb)
         HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
@@ -1055,16 +1144,24 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
     }
     HIP_TRY(ctx, hipMemcpyAsync(p->d_coef, cp.coef.data(), cp.coef.size() * sizeof(double),
                                 hipMemcpyHostToDevice, st));
+    return DBSLMM_OK;
+}
+
+static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup& grp) {
+    dbslmm_ctx* ctx = p->ctx;
+    hipStream_t st = grp.st;
+    if (grp.n_items == 0) return DBSLMM_OK;
+    const int64_t vs = std::max<int64_t>(1, p->n_slots);
     const int64_t blk = trsv::kMaxR * vs;
     double *Y = p->d_cheb, *Z = Y + blk, *X = Z + blk, *R = X + blk, *D = R + blk, *S = D + blk;
-    const int grid = std::max(1, std::min(ctx->n_cu, p->n_titems));
+    const int grid = grp.grid;
     for (size_t g = 0; g < cp.iters.size(); ++g) {
         const size_t g0 = g * trsv::kMaxR;
         const int nr = static_cast<int>(std::min<size_t>(trsv::kMaxR, cp.others.size() - g0));
         int cix[trsv::kMaxR] = {0, 0};
         for (int j = 0; j < nr; ++j) cix[j] = cp.others[g0 + j];
         const double* coef = p->d_coef + cp.coef_off[g];
-        hipLaunchKernelGGL(dbslmm_cheb_init, dim3(p->n_tiled), dim3(256), 0, st, p->d_tb, p->d_row0, p->d_m,
+        hipLaunchKernelGGL(dbslmm_cheb_init, dim3(grp.n_tb), dim3(256), 0, st, p->d_tb + grp.tb_off, p->d_row0, p->d_m,
                            p->d_ms, p->d_blk_id, p->d_y + static_cast<int64_t>(cp.base) * p->n_slots, coef,
                            nr, vs, X, R, D, S, p->d_status + cp.base * p->nbk, p->d_status, p->nbk,
                            cix[0], cix[1]);
@@ -1078,10 +1175,10 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
         a.row0 = p->d_row0;
         a.blk_id = p->d_blk_id;
         a.slot_out = p->d_slot_out;
-        a.n_items = p->n_titems;
+        a.n_items = grp.n_items;
         a.foff = p->d_foff;
         a.flags = p->d_tflags;
-        a.ctr = p->d_tflags + p->n_tflags;
+        a.ctr = grp.ctr;
         a.err = p->d_tflags + p->n_tflags + 1;
         a.vs = vs;
         a.X = X;
@@ -1114,7 +1211,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp) {
                     p->trsv_epoch = 1;
                 }
                 a.epoch = p->trsv_epoch;
-                a.items = fwd ? p->d_tri_f : p->d_tri_b;
+                a.items = (fwd ? p->d_tri_f : p->d_tri_b) + 2 * grp.item_off;
                 a.src = fwd ? R : Y;
                 a.dst = fwd ? Y : Z;
                 a.coef = coef + static_cast<int64_t>(k) * nr * 3;
@@ -1219,6 +1316,10 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift + c, dshift);
         }
         const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
+        if (cheb) {
+            const int rc = cheb_prepare(p, cp, s);
+            if (rc != DBSLMM_OK) return rc;
+        }
         // fork: the tiled sequence runs on stream2 (high priority: the critical path) while the
         // single-workgroup and single-wave kernels run on the main stream.
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
@@ -1259,12 +1360,25 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             if (single) {
                 const int rc = run_tiled_copy(p, isn, 0);
                 if (rc != DBSLMM_OK) return rc;
+            } else if (cheb && p->early_ev >= 0 && p->n_titems_early > 0 && persistent_bwd() && cheb_split()) {
+                // h2f, split: the sequence by direct launches (its early-group event is waited on
+                // by the main stream), the early group's backward solve + iterations on the main
+                // stream as soon as its blocks are factored, the rest after the sequence
+                int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, cp.base, true);
+                if (rc != DBSLMM_OK) return rc;
+                HIP_TRY(ctx, hipStreamWaitEvent(s, p->tev[p->early_ev], 0));
+                const TGroup ge = tgroup_early(p), gl = tgroup_late(p);
+                if ((rc = run_pbwd(p, isn, cp.base, ge)) != DBSLMM_OK) return rc;
+                if ((rc = run_cheb(p, isn, cp, ge)) != DBSLMM_OK) return rc;
+                if ((rc = run_pbwd(p, isn, cp.base, gl)) != DBSLMM_OK) return rc;
+                if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                if ((rc = run_cheb(p, isn, cp, gl)) != DBSLMM_OK) return rc;
             } else if (cheb) {
                 // h2f: factor only the base copy, iterate the others on its factor
                 int rc = run_tiled_copy(p, isn, cp.base);
                 if (rc != DBSLMM_OK) return rc;
                 if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
-                rc = run_cheb(p, isn, cp);
+                rc = run_cheb(p, isn, cp, tgroup_all(p));
                 if (rc != DBSLMM_OK) return rc;
             } else if (!use_graph) {
                 const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist, 0,
@@ -1288,7 +1402,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             if (use_graph) HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
             if (!single && !cheb && persistent_bwd())   // merged copies: one backward launch each
                 for (int c = 0; c < n; ++c) {
-                    const int rc = run_pbwd(p, isn, c);
+                    const int rc = run_pbwd(p, isn, c, tgroup_all(p));
                     if (rc != DBSLMM_OK) return rc;
                 }
         }
