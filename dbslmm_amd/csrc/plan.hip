@@ -195,10 +195,14 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 // workgroups hold whole CUs (96 KiB LDS each) for the length of a launch, the chain kernels of
 // the big blocks wait for CUs, and the factorisation grows from 29 to 34-43 ms (n_cu / 2 .. n_cu
 // substitution workgroups), more than the 5.5 ms the later substitutions save.
-static bool cheb_split() {
+// DBSLMM_CHEB_SPLIT=2: both groups after the factorisation, concurrently on two streams with
+// disjoint workgroup budgets: the big blocks' chains (DBSLMM_LATE_GRID workgroups, default 96)
+// and the bandwidth-bound rest (the other CUs).
+static int cheb_split_mode() {
     const char* e = getenv("DBSLMM_CHEB_SPLIT");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) : 0;
 }
+static bool cheb_split() { return cheb_split_mode() != 0; }
 
 // regions (128 columns) per super step (env DBSLMM_SUPER)
 static int tiled_R() {
@@ -962,19 +966,25 @@ struct TGroup {
     int32_t* ctr;
     int grid;
 };
+static int late_grid(const dbslmm_plan* p) {
+    int g = 96;
+    if (const char* e = getenv("DBSLMM_LATE_GRID")) g = atoi(e);
+    return std::max(8, std::min(p->ctx->n_cu - 8, g));
+}
 static TGroup tgroup_all(const dbslmm_plan* p) {
     return TGroup{0, p->n_titems, 0, p->n_tiled, p->ctx->stream2, p->d_tflags + p->n_tflags,
                   std::max(1, std::min(p->ctx->n_cu, p->n_titems))};
 }
 static TGroup tgroup_late(const dbslmm_plan* p) {
     const int32_t n = p->n_titems - p->n_titems_early;
+    const int cap = cheb_split_mode() == 2 ? late_grid(p) : p->ctx->n_cu;
     return TGroup{p->n_titems_early, n, p->n_tb_early, p->n_tiled - p->n_tb_early, p->ctx->stream2,
-                  p->d_tflags + p->n_tflags, std::max(1, std::min(p->ctx->n_cu, n))};
+                  p->d_tflags + p->n_tflags, std::max(1, std::min(cap, n))};
 }
 // the early group shares the GPU with the rest of the tiled sequence: at most DBSLMM_SPLIT_GRID
 // (default n_cu / 2) workgroups, so the chain kernels of the big blocks keep CUs
 static TGroup tgroup_early(const dbslmm_plan* p) {
-    int cap = p->ctx->n_cu / 2;
+    int cap = cheb_split_mode() == 2 ? p->ctx->n_cu - late_grid(p) : p->ctx->n_cu / 2;
     if (const char* e = getenv("DBSLMM_SPLIT_GRID")) cap = std::max(1, atoi(e));
     return TGroup{0, p->n_titems_early, 0, p->n_tb_early, p->ctx->stream, p->d_tflags + p->n_tflags + 2,
                   std::max(1, std::min(cap, p->n_titems_early))};
@@ -1026,12 +1036,12 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
 // The single-copy tiled sequence on factorisation copy `copy` (stream2), replayed from a graph
 // captured per copy; its backward substitution is one persistent launch (run_pbwd) unless
 // DBSLMM_PBWD=0.
-static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
+static int run_tiled_copy(dbslmm_plan* p, double isn, int copy, bool with_pbwd = true) {
     dbslmm_ctx* ctx = p->ctx;
     const bool pb = persistent_bwd();
     if (!tiled_use_graph()) {
         const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy, pb);
-        return rc != DBSLMM_OK || !pb ? rc : run_pbwd(p, isn, copy, tgroup_all(p));
+        return rc != DBSLMM_OK || !pb || !with_pbwd ? rc : run_pbwd(p, isn, copy, tgroup_all(p));
     }
     if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
     hipGraphExec_t& gx = p->graph_copy[copy];
@@ -1050,7 +1060,7 @@ static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
         HIP_TRY(ctx, ie);
     }
     HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
-    return pb ? run_pbwd(p, isn, copy, tgroup_all(p)) : DBSLMM_OK;
+    return pb && with_pbwd ? run_pbwd(p, isn, copy, tgroup_all(p)) : DBSLMM_OK;
 }
 
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
@@ -1360,6 +1370,19 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             if (single) {
                 const int rc = run_tiled_copy(p, isn, 0);
                 if (rc != DBSLMM_OK) return rc;
+            } else if (cheb && p->n_titems_early > 0 && persistent_bwd() && cheb_split_mode() == 2) {
+                // h2f, split after the factorisation: the two groups' backward solves and
+                // iterations concurrently, the rest on the main stream
+                int rc = run_tiled_copy(p, isn, cp.base, false);
+                if (rc != DBSLMM_OK) return rc;
+                HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
+                HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join3, 0));
+                const TGroup ge = tgroup_early(p), gl = tgroup_late(p);
+                if ((rc = run_pbwd(p, isn, cp.base, ge)) != DBSLMM_OK) return rc;
+                if ((rc = run_cheb(p, isn, cp, ge)) != DBSLMM_OK) return rc;
+                if ((rc = run_pbwd(p, isn, cp.base, gl)) != DBSLMM_OK) return rc;
+                if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                if ((rc = run_cheb(p, isn, cp, gl)) != DBSLMM_OK) return rc;
             } else if (cheb && p->early_ev >= 0 && p->n_titems_early > 0 && persistent_bwd() && cheb_split()) {
                 // h2f, split: the sequence by direct launches (its early-group event is waited on
                 // by the main stream), the early group's backward solve + iterations on the main
