@@ -87,3 +87,23 @@ def test_cheb_repeatable_and_followed_by_plain_run(monkeypatch):
     got = plan.download()
     ref = _fresh(prob, sig[:1])[0]
     np.testing.assert_array_equal(_cat(got), _cat(ref))
+
+
+@pytest.mark.parametrize("split", ["1", "2"])
+def test_cheb_split_groups_match_joint(monkeypatch, split):
+    """The opt-in block-group split of the substitutions (DBSLMM_CHEB_SPLIT 1: the early group
+    overlapping the factorisation, 2: both groups after it on two streams) gives the joint
+    launches' betas bit for bit: the same per-block arithmetic in the same order."""
+    from dbslmm_amd import Context, Plan
+    monkeypatch.setenv("DBSLMM_TILED_MIN", "64")
+    prob = _problem(seed=9, mono_block=3)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    joint = Plan(Context(0), prob).run_multi(sig)
+    monkeypatch.setenv("DBSLMM_CHEB_SPLIT", split)
+    monkeypatch.setenv("DBSLMM_SPLIT_FRAC", "0.3")
+    plan = Plan(Context(0), prob)
+    for _ in range(2):                       # twice: the second ticket counter resets itself
+        got = plan.run_multi(sig)
+        for x, y in zip(got, joint):
+            np.testing.assert_array_equal(_cat(x), _cat(y))
+            np.testing.assert_array_equal(x[2], y[2])
