@@ -43,6 +43,7 @@ constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
 constexpr size_t kTrail2Lds = sizeof(double) * chol::kTrail2Doubles;
 constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3Doubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
+constexpr int kTiledMinSmall = 256;     // the same when no block reaches kTiledMinDefault
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
@@ -545,7 +546,19 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     int64_t moff = 0;
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
-    if (const char* env = getenv("DBSLMM_TILED_MIN")) tiled_min = std::max<int64_t>(64, atoll(env));
+    if (const char* env = getenv("DBSLMM_TILED_MIN")) {
+        tiled_min = std::max<int64_t>(64, atoll(env));
+    } else {
+        // no block reaches the default: the single-workgroup solve of the largest blocks is then
+        // the critical path itself, and spreading the blocks of >= kTiledMinSmall SNPs over many
+        // workgroups shortens it (config 2: 0.66 -> 0.55 ms/step); with bigger blocks the tiled
+        // sequence is the critical path and the mid-size blocks stay in its shadow
+        int64_t mmax = 0;
+        for (int b = 0; b < pr->num_block; ++b)
+            mmax = std::max<int64_t>(mmax, pr->s_ptr[b + 1] - pr->s_ptr[b] +
+                                               (has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0));
+        if (mmax < kTiledMinDefault) tiled_min = kTiledMinSmall;
+    }
     p->tiled_min = static_cast<int32_t>(std::min<int64_t>(tiled_min, INT32_MAX));
     std::vector<char> is_tiled;
     for (int b = 0; b < pr->num_block; ++b) {
