@@ -985,8 +985,10 @@ static int late_grid(const dbslmm_plan* p) {
     return std::max(8, std::min(p->ctx->n_cu - 8, g));
 }
 static TGroup tgroup_all(const dbslmm_plan* p) {
+    int cap = p->ctx->n_cu;   // env DBSLMM_TRSV_GRID (diagnostic): fewer substitution workgroups
+    if (const char* e = getenv("DBSLMM_TRSV_GRID")) cap = std::max(1, atoi(e));
     return TGroup{0, p->n_titems, 0, p->n_tiled, p->ctx->stream2, p->d_tflags + p->n_tflags,
-                  std::max(1, std::min(p->ctx->n_cu, p->n_titems))};
+                  std::max(1, std::min(cap, p->n_titems))};
 }
 static TGroup tgroup_late(const dbslmm_plan* p) {
     const int32_t n = p->n_titems - p->n_titems_early;
