@@ -430,9 +430,8 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 // i8 tiles, 128 accumulator registers).  K runs in stages of 64 individuals: every thread loads
 // one row's 4 Gp dwords (16 B, two stages ahead in registers) and expands them to 64 B of int8
 // codes in a double-buffered LDS stage (a quarter of the HBM / L2 operand traffic of an int8
-// image), raw s_barrier per stage, 16 MFMAs per wave.  Position p of LDS row r holds K chunk
-// p ^ ((r >> 2) & 3), which puts the 16 rows of every ds_read_b128 lane group on 16 distinct
-// bank groups.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
+// image), raw s_barrier per stage, 16 MFMAs per wave.  LDS rows are swizzled (swz) so that both
+// the expansion writes and the operand reads are bank-conflict free.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
 // skip the MFMAs.  Missing-call blocks:
 // exact 4-product path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
@@ -442,7 +441,11 @@ constexpr int kHK = 64;                    // individuals (bytes) per K stage = 
 constexpr int kHOp = kHT * kHK;            // one operand stage (16 KiB)
 constexpr int kHSlots = 2;                 // LDS double buffer
 constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 64 KiB
-__device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r >> 2) & 3)); }
+// logical 16-B chunk c of row r at position c ^ f(r), f(r) = (r ^ r >> 2 ^ r >> 3) & 3: conflict-free
+// for the expansion writes (ds_write_b128: 8-lane groups of consecutive rows, 32 banks) and the
+// MFMA operand reads (ds_read_b128: 16-lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}
+// of 32 rows, 64 banks) -- MI355X_MICROARCH.md LDS table; (r >> 2) & 3 left the writes 2-way
+__device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 3)); }
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
@@ -476,9 +479,8 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         return;
     }
     // staging: thread t -> operand t >> 8, row t & 255; per stage (64 individuals) one 16-B load
-    // of 4 Gp dwords, expanded on the way into LDS (4 ds_write_b128, swizzled: logical chunk c of
-    // row r at position c ^ ((r >> 2) & 3), which spreads every ds_read_b128 lane group over 16
-    // distinct bank groups).  Loads run two stages ahead in two register sets.
+    // of 4 Gp dwords, expanded on the way into LDS (4 ds_write_b128 at swz: conflict-free writes
+    // and reads).  Loads run two stages ahead in two register sets.
     const int64_t kw = kpad / 16;
     const int sop = tid >> 8, srow = tid & 255;
     const bool stager = !(diag && sop == 1);
