@@ -480,7 +480,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     }
     // staging: thread t -> operand t >> 8, row t & 255; per stage (64 individuals) one 16-B load
     // of 4 Gp dwords, expanded on the way into LDS (4 ds_write_b128 at swz: conflict-free writes
-    // and reads).  Loads run two stages ahead in two register sets.
+    // and reads).  Loads run four stages ahead in four register sets.
     const int64_t kw = kpad / 16;
     const int sop = tid >> 8, srow = tid & 255;
     const bool stager = !(diag && sop == 1);
@@ -525,24 +525,26 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
                     acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
         }
     };
-    v4i p0 = gload(0), p1 = gload(1);
+    // four register sets: the loads of stage st + 4 are issued while stage st is multiplied
+    v4i p0 = gload(0), p1 = gload(1), p2 = gload(2), p3 = gload(3);
     lstore(p0, 0);
-    p0 = gload(2);
+    p0 = gload(4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // raw barriers: a __syncthreads() would also drain the loads in flight.  The tail's extra
-    // expansions land in the slot no later stage reads.
-    for (int st = 0; st < nst; st += 2) {
-        lstore(p1, st + 1);                   // stage st is in slot 0
-        p1 = gload(st + 3);
-        compute(st);
+    // raw barriers: a __syncthreads() would also drain the loads in flight.  Expansions past the
+    // last stage land in the slot no later stage reads; every wave runs the same barriers.
+    auto step = [&](v4i& pk, int st) {    // stage st is in slot st & 1; pk holds stage st + 1
+        lstore(pk, st + 1);
+        pk = gload(st + 5);
+        if (st < nst) compute(st);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        lstore(p0, st + 2);                   // stage st + 1 is in slot 1
-        p0 = gload(st + 4);
-        compute(st + 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+    };
+    for (int st = 0; st < nst; st += 4) {
+        step(p1, st);
+        step(p2, st + 1);
+        step(p3, st + 2);
+        step(p0, st + 3);
     }
     if (idle) return;
     const double scale = tau / n_ref_d;
