@@ -427,25 +427,25 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 // ------------------------------------------------------------------------------------------
 // Kernel 2c: the Gram of the big blocks (m >= 384), 256 x 256 output tile per 512-thread
 // workgroup: wave w computes rows 64 (w & 3) .., columns 128 (w >> 2) .. (2 x 4 MFMA 32x32x32
-// i8 tiles, 128 accumulator registers).  K runs in stages of 64 individuals: every thread loads
-// one row's 4 Gp dwords (16 B, two stages ahead in registers) and expands them to 64 B of int8
+// i8 tiles, 128 accumulator registers).  K runs in stages of 128 individuals: every thread loads
+// one row's 8 Gp dwords (32 B, four stages ahead in registers) and expands them to 128 B of int8
 // codes in a double-buffered LDS stage (a quarter of the HBM / L2 operand traffic of an int8
-// image), raw s_barrier per stage, 16 MFMAs per wave.  LDS rows are swizzled (swz) so that both
+// image), raw s_barrier per stage, 32 MFMAs per wave.  LDS rows are swizzled (swz) so that both
 // the expansion writes and the operand reads are bank-conflict free.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
 // skip the MFMAs.  Missing-call blocks:
 // exact 4-product path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
 namespace gram {
 constexpr int kHT = 256;                   // output tile edge
-constexpr int kHK = 64;                    // individuals (bytes) per K stage = one row chunk set
-constexpr int kHOp = kHT * kHK;            // one operand stage (16 KiB)
+constexpr int kHK = 128;                   // individuals (bytes) per K stage = one row chunk set
+constexpr int kHOp = kHT * kHK;            // one operand stage (32 KiB)
 constexpr int kHSlots = 2;                 // LDS double buffer
-constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 64 KiB
-// logical 16-B chunk c of row r at position c ^ f(r), f(r) = (r ^ r >> 2 ^ r >> 3) & 3: conflict-free
+constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 128 KiB
+// logical 16-B chunk c of row r at position c ^ f(r), f(r) = (r ^ r >> 2 ^ r >> 3) & 7: conflict-free
 // for the expansion writes (ds_write_b128: 8-lane groups of consecutive rows, 32 banks) and the
 // MFMA operand reads (ds_read_b128: 16-lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}
 // of 32 rows, 64 banks) -- MI355X_MICROARCH.md LDS table; (r >> 2) & 3 left the writes 2-way
-__device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 3)); }
+__device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 7)); }
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
@@ -478,23 +478,29 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         }
         return;
     }
-    // staging: thread t -> operand t >> 8, row t & 255; per stage (64 individuals) one 16-B load
-    // of 4 Gp dwords, expanded on the way into LDS (4 ds_write_b128 at swz: conflict-free writes
-    // and reads).  Loads run four stages ahead in four register sets.
+    // staging: thread t -> operand t >> 8, row t & 255; per stage (128 individuals) two 16-B
+    // loads of 8 Gp dwords, expanded on the way into LDS (8 ds_write_b128 at swz: conflict-free
+    // writes and reads).  Loads run four stages ahead in four register sets.
     const int64_t kw = kpad / 16;
     const int sop = tid >> 8, srow = tid & 255;
     const bool stager = !(diag && sop == 1);
     const uint32_t* gs = Gp + static_cast<int64_t>(row0 + kHT * (sop ? tile.tj : tile.ti) + srow) * kw;
-    const int nst = static_cast<int>(kpad / kHK);   // even: kpad is a multiple of 128
+    const int nst = static_cast<int>(kpad / kHK);   // kpad is a multiple of 128
     // unconditional loads (clamped stage, valid rows for every thread) keep the vmcnt bookkeeping
-    // exact: one newer load in flight at every use
-    auto gload = [&](int st) -> v4i { return *reinterpret_cast<const v4i*>(gs + 4 * min(st, nst - 1)); };
-    auto lstore = [&](const v4i& pk, int st) {
+    // exact: the newer loads in flight at every use are known
+    struct Pk { v4i lo, hi; };                       // a stage of one row: 8 Gp dwords
+    auto gload = [&](int st) -> Pk {
+        const uint32_t* q = gs + 8 * min(st, nst - 1);
+        return Pk{*reinterpret_cast<const v4i*>(q), *reinterpret_cast<const v4i*>(q + 4)};
+    };
+    auto lstore = [&](const Pk& pk, int st) {
         if (!stager) return;
         int8_t* slot = hlds + (st & 1) * 2 * kHOp + sop * kHOp;
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-            *reinterpret_cast<v4i*>(slot + swz(srow, c)) = expand_dose(static_cast<uint32_t>(pk[c]));
+        for (int c = 0; c < 4; ++c) {
+            *reinterpret_cast<v4i*>(slot + swz(srow, c)) = expand_dose(static_cast<uint32_t>(pk.lo[c]));
+            *reinterpret_cast<v4i*>(slot + swz(srow, 4 + c)) = expand_dose(static_cast<uint32_t>(pk.hi[c]));
+        }
     };
     const int wr = wave & 3, wc = wave >> 2;       // rows 64 wr .., columns 128 wc ..
     const bool idle = diag && 128 * wc >= 64 * wr + 64;
@@ -526,14 +532,14 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         }
     };
     // four register sets: the loads of stage st + 4 are issued while stage st is multiplied
-    v4i p0 = gload(0), p1 = gload(1), p2 = gload(2), p3 = gload(3);
+    Pk p0 = gload(0), p1 = gload(1), p2 = gload(2), p3 = gload(3);
     lstore(p0, 0);
     p0 = gload(4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // raw barriers: a __syncthreads() would also drain the loads in flight.  Expansions past the
     // last stage land in the slot no later stage reads; every wave runs the same barriers.
-    auto step = [&](v4i& pk, int st) {    // stage st is in slot st & 1; pk holds stage st + 1
+    auto step = [&](Pk& pk, int st) {     // stage st is in slot st & 1; pk holds stage st + 1
         lstore(pk, st + 1);
         pk = gload(st + 5);
         if (st < nst) compute(st);
