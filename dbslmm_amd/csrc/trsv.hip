@@ -33,11 +33,12 @@
 // counter in LDS).  vmcnt counts in order per wave, so a hand-off load in a streaming wave would
 // drain its whole L prefetch; split this way the streaming waves keep ~128 KiB per CU in flight
 // and the hand-off latency overlaps the stream.  A launch is bound by the dependency chain of the
-// longest block: about 8 us per 64-row tile (drain + flag + poll + payload round trips and the
-// tile's reductions).
+// longest block (about 3.8 us per 64-row tile alone, 5.7 us under the bulk streaming: drain +
+// flag + poll + payload round trips and the tile's reductions) and by the streaming bandwidth.
 //
 // Factor layout (chol_tiled.hip): strict lower = L; each 64 x 64 diagonal tile holds, on and
-// above its diagonal, X^T with X = L_kk^{-1}.
+// above its diagonal, X^T with X = L_kk^{-1}; every other 64 x 64 tile of the upper triangle holds
+// the transposed L tile (L^T), so the backward substitution streams rows like the forward one.
 namespace trsv {
 
 constexpr int kT = 64;                       // tile rows = the stored diagonal inverse blocks
