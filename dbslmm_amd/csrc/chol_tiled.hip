@@ -11,7 +11,9 @@
 //
 // A 64 x 64 diagonal tile is factored as 2 x 2 tiles of 32 by chol::factor_diag:
 //   L00, X00 = L00^{-1};  L10 = A10 X00^T;  A11 -= L10 L10^T;  L11, X11;  X10 = -X11 L10 X00
-// and stored as: strict lower = L, diagonal + upper (r, c >= r) = X[c][r] (X = L_kk^{-1}).
+// and stored as: strict lower = L, diagonal + upper (r, c >= r) = X[c][r] (X = L_kk^{-1}).  The
+// panel and region kernels also store every off-diagonal 64 x 64 tile of L transposed into the
+// upper triangle (rows < m only), for the row-streaming backward substitution of trsv.hip.
 //
 // Work items of the region / panel / trailing launches are int32 pairs [block or tile,
 // (local step << 8) | count]: every block runs at its own step inside a shared launch.
