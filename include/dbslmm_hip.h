@@ -83,14 +83,16 @@ typedef struct dbslmm_problem {
 
 /* Kernel timing slots reported by dbslmm_plan_kernel_ms. */
 enum {
-    DBSLMM_K_UNPACK = 0,      /* dbslmm_unpack_stats: 2-bit .bed rows -> int8 dosages + stats */
-    DBSLMM_K_GRAM = 1,        /* dbslmm_gram_i8: i8-MFMA grouped syrk + fp64 standardising epilogue */
+    DBSLMM_K_UNPACK = 0,      /* dbslmm_unpack_stats: 2-bit .bed rows -> 2-bit dosage codes + stats */
+    DBSLMM_K_GRAM = 1,        /* dbslmm_gram_i8 / _big / _huge: i8-MFMA grouped syrk (codes expanded
+                                 on the fly) + fp64 standardising epilogue */
     DBSLMM_K_CHOL_LARGE = 2,  /* dbslmm_chol_large: blocks with 64 <= m+1 and m below the tiled
                                  threshold, one workgroup each */
     DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
                                  (concurrent with CHOL_LARGE when there are no tiled blocks) */
     DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold (env
-                                 DBSLMM_TILED_MIN, default 512), many workgroups per block,
+                                 DBSLMM_TILED_MIN; default 512, or 256 when no block reaches
+                                 512), many workgroups per block,
                                  one launch per panel phase (third stream); the whole sequence */
     DBSLMM_K_TRSV = 5,        /* dbslmm_trsv_fwd/bwd: h2f tuning's Chebyshev iterations of the
                                  tiled blocks on the base copy's factor (run_multi; 0 otherwise) */
@@ -135,7 +137,7 @@ int dbslmm_plan_enable_timing(dbslmm_plan* plan, int enable);
 int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/, int32_t* launches_out);
 
 /* Workload figures of the plan (for rooflines): [0] SNPs, [1] packed bytes read by the unpack,
- * [2] int8 bytes written by the unpack, [3] Gram int8 ops (2 per MAC, algorithmic
+ * [2] Gram operand (2-bit dosage code) bytes written by the unpack, [3] Gram int8 ops (2 per MAC, algorithmic
  * sum_b n_ref*m_b*(m_b+1)), [4] Gram ops as executed on padded tiles, [5] Cholesky+solve fp64
  * flops of the large blocks (sum_b m_b^3/3 + 2 m_b^2), [6] non-empty blocks, [7] gram tiles,
  * [8] the same fp64 flops for the small blocks, [9] large blocks, [10] the same fp64 flops for
