@@ -90,7 +90,7 @@ def kernel_roofline(name, ms, wl, n_solve=1):
         return dict(kernel=name, bound="hbm", achieved=a, peak=PEAK_HBM_GBS, unit="GB/s",
                     frac=a / PEAK_HBM_GBS, algorithmic=b, ms=ms,
                     note="factor bytes read by the %d forward + backward substitutions of h2f tuning "
-                         "(iterations on the base copy's factor; chain-bound, ~8 us per 64-row tile)"
+                         "(iterations on the base copy's factor; chain- and streaming-bound, ~5.7 us per 64-row step of the largest block)"
                          % wl["cheb_iters"])
     if name == "dbslmm_tchol" and wl["cheb_iters"] > 0:
         n_solve = 1     # h2f: only the base copy of the tiled blocks is factored
