@@ -679,6 +679,9 @@ extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing2(
 // bank groups.  Two slots; per stage: wait for this wave's DMA, barrier, issue the next stage's
 // DMA into the other slot (every wave has left it), multiply.  acc holds -C (negated on load and
 // store), so the MFMAs add L_I L_J^T.
+#ifndef DBSLMM_T3_DIAG
+#define DBSLMM_T3_DIAG 0
+#endif
 namespace chol {
 constexpr int kOp3 = kT2 * kK2;                // one operand stage, unpadded (32 KiB)
 constexpr int kTrail3Doubles = 4 * kOp3;       // A, B x 2 slots (128 KiB)
@@ -781,7 +784,9 @@ extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
         __builtin_amdgcn_s_barrier();                        // stage g is in LDS; slot g+1 free
         if (g + 1 < total) {
             const int Jn = J0 + (g + 1) / nst, tn = (g + 1) % nst;
+#if DBSLMM_T3_DIAG != 2
             t3_issue(lds + ((g + 1) & 1) * 2 * kOp3, A, ld, I, Jn, c0 + kK2 * tn, I == Jn, wave, lane);
+#endif
             if (tn == 0) t3_load_c(nxt, A, ld, kT2 * I + 64 * wr, kT2 * Jn + 32 * wc, lane);
         }
         if (t == 0 && g > 0) {
@@ -793,7 +798,9 @@ extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
                 for (int j = 0; j < 2; ++j) acc[i][j] = nxt[i][j];
         }
         const bool skip = diag && 32 * wc > 64 * wr + 63;
+#if DBSLMM_T3_DIAG != 1   // diagnostic builds only (1: no MFMAs, 2: no operand DMA)
         if (!skip) t3_mfma_stage(acc, S, diag ? S : S + kOp3, wr, wc, lane);
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     {
