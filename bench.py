@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--gen", choices=("numpy", "gpu"), default=None,
                     help="synthetic panel generator (default: numpy for config 2, gpu above)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host threads (OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
@@ -124,6 +124,159 @@ def pmc_traffic(kernel, args, n_solve):
     else:
         per = k["hbm_bytes"] * (n_solve if kernel.startswith("dbslmm_chol") else 1)
     return per, os.path.relpath(files[-1], ROOT)
+
+
+def host_info():
+    """CPU model, logical CPUs of the machine and the threads this process may use (the GPU box
+    shows the whole machine in nproc; its CPU share is OMP_NUM_THREADS)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    share = int(os.environ.get("OMP_NUM_THREADS") or aff)
+    return dict(cpu_model=model, nproc=nproc, affinity=aff, threads_all=max(1, min(share, aff)))
+
+
+def cpu_leg(args, prob, res, sigmas, wl):
+    """cpu_baseline (the C restatement of the reference, timed on this host) and the beta check.
+
+    Timing: blocks drawn SNP-uniformly (a block with probability ~ its SNP count, so big blocks
+    appear as often as their share of SNPs) until ~args.cpu_seconds of CPU work, once with all
+    host threads (OpenMP over blocks, 1 BLAS thread each -- the reference's -t N build) and once
+    with 1 thread.  The sample's throughput in cost units (block_cost = n_ref m(m+1) + m^3/3) is
+    applied to the whole workload's cost, bounded below by the largest block's single-thread time
+    (a block never spans threads in the reference): value = workload SNPs / that time.
+    Beta check: every block with >= 2000 SNPs against the oracle's direct (Cholesky) solve on all
+    host cores, plus the timed sample against the reference-faithful PCG."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import ref_numpy as R
+    from dbslmm_amd.dist import block_cost, sub_problem
+    blas = O.use_blas(True)
+    hi = host_info()
+    thr = args.cpu_threads or hi["threads_all"]
+    nblk = len(prob.s_ptr) - 1
+    m_b = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
+    cost = block_cost(m_b, prob.n_ref)
+    sig_list = sigmas if sigmas else [prob.sigma_s]
+    rng = np.random.default_rng(0)
+    nz = np.flatnonzero(m_b > 0)
+    order = rng.choice(nz, size=nz.size, replace=False, p=m_b[nz] / m_b[nz].sum())
+
+    def timed(threads, seconds):
+        """Blocks in `order` (skipping those whose own cost exceeds the call budget) until the
+        budget: returns (SNPs, cost, seconds, blocks, outs)."""
+        done_snps, done_cost, tc, used, outs = 0, 0.0, 0.0, [], []
+        rate = 2e9 * threads            # cost units / s, refined after every call
+        i = 0
+        while tc < seconds and i < order.size:
+            # next call: ~1 s of work at the measured rate; a block whose single-thread time
+            # would exceed 40 % of the budget is left out (the reference never splits a block)
+            budget = rate * max(0.2, min(1.0, seconds - tc))
+            cur, acc = [], 0.0
+            while i < order.size and acc < budget:
+                b = order[i]
+                i += 1
+                if cost[b] / (rate / threads) > 0.4 * seconds:
+                    continue
+                cur.append(b)
+                acc += cost[b]
+            if not cur:
+                continue
+            blocks = np.sort(np.array(cur))
+            sub, s_idx, l_idx = sub_problem(prob, blocks)
+            c0 = time.perf_counter()
+            o = [O.est(sub.bed, sub.n_ref, sub.n_obs, sg, sub.s_ptr, sub.s_pos, sub.z_s,
+                       sub.l_ptr, sub.l_pos, sub.z_l, tau=prob.tau, method="pcg", threads=threads)
+                 for sg in sig_list]       # the reference runs dbslmm once per h2f factor
+            tc += time.perf_counter() - c0
+            done_snps += len(s_idx) + len(l_idx)
+            done_cost += acc
+            rate = done_cost / tc
+            used.append(blocks)
+            outs.append((s_idx, l_idx, o))
+        return done_snps, done_cost, tc, used, outs
+
+    snps_t, cost_t, sec_t, used_t, outs_t = timed(thr, args.cpu_seconds)
+    snps_1, cost_1, sec_1, used_1, _ = timed(1, max(2.0, args.cpu_seconds / 2)) if thr > 1 else \
+        (snps_t, cost_t, sec_t, used_t, None)
+    rate_t, rate_1 = cost_t / sec_t, cost_1 / sec_1          # cost units per second
+    total, cmax, m_all = float(cost.sum()), float(cost.max()), float(m_b.sum())
+    t_all = max(total / rate_t, cmax / rate_1)
+    t_one = total / rate_1
+    nb_t = int(sum(len(u) for u in used_t))
+    cpu = dict(
+        value=m_all / t_all, unit="SNPs/s", cores=thr, kind="port",
+        sample=(f"{nb_t} of {nblk} blocks ({snps_t} SNPs, {cost_t / total:.1%} of the workload's "
+                f"cost) drawn SNP-uniformly, {sec_t:.1f} s on {thr} threads (OpenMP over blocks, "
+                f"1 BLAS thread each, {len(sig_list)} solve(s) per SNP as on the GPU); value = "
+                f"workload SNPs / (workload cost at the sample's cost rate, >= the largest block "
+                f"at the 1-thread rate): C restatement of the reference (byte-wise readSNPIm, N-1 "
+                f"standardise, {'OpenBLAS dsyrk/dgemm/dgemv' if blas else 'plain-loop Gram'}, "
+                f"Jacobi-PCG tol 1e-7)"),
+        sample_snps_per_s=snps_t / sec_t,
+        t1=dict(value=m_all / t_one, cores=1, sample_snps=snps_1, seconds=sec_1,
+                sample_snps_per_s=snps_1 / sec_1),
+        host=hi, est_seconds_per_step=t_all)
+    # beta check 1: the timed sample vs the reference-faithful PCG (every h2f solve)
+    mx, nw, ncmp = 0.0, 0.0, 0
+    for s_idx, l_idx, o in outs_t:
+        for c, (rs, rl, _, _) in enumerate(o):
+            ref = np.concatenate([rs, rl])
+            got = np.concatenate([res[c][0][s_idx], res[c][1][l_idx]])
+            ok = np.isfinite(ref)
+            if ok.any():
+                mx = max(mx, float(np.max(np.abs(got[ok] - ref[ok]))))
+                nw = max(nw, float(np.max(np.abs(got[ok] - ref[ok])) / np.max(np.abs(ref[ok]))))
+            ncmp += int(ok.sum())
+    dbeta = dict(max_abs=mx, normwise=nw, snps_compared=ncmp,
+                 vs="CPU reference-faithful PCG (oracle) on the timed sample" +
+                    (", every h2f solve" if sigmas else ""))
+    # beta check 2: every block >= 2000 SNPs vs the direct solve (all host cores per block)
+    big = np.flatnonzero(m_b >= 2000)
+    O.blas_threads(hi["threads_all"])
+    bmx, bnw, bsn = 0.0, 0.0, 0
+    t0 = time.perf_counter()
+    try:
+        for b in big:
+            b = int(b)
+            s0, s1 = int(prob.s_ptr[b]), int(prob.s_ptr[b + 1])
+            Xs = O.read_block_std(prob.bed, prob.n_ref, prob.s_pos[s0:s1], threads=hi["threads_all"])
+            Xl = None
+            if prob.l_ptr is not None and prob.l_ptr[b + 1] > prob.l_ptr[b]:
+                l0, l1 = int(prob.l_ptr[b]), int(prob.l_ptr[b + 1])
+                Xl = O.read_block_std(prob.bed, prob.n_ref, prob.l_pos[l0:l1], threads=hi["threads_all"])
+            Sss, Sls, Sll = R.block_sigmas_tau(Xs, Xl, prob.n_ref, prob.tau)
+            del Xs, Xl
+            for c, sg in enumerate(sig_list):
+                if Sls is None:
+                    ref = R.est_block_s_sigma(Sss, prob.n_obs, sg, prob.z_s[s0:s1], "chol")
+                    got = res[c][0][s0:s1]
+                else:
+                    rs, rl = R.est_block_ls_sigma(Sss, Sls, Sll, prob.n_obs, sg, prob.z_s[s0:s1],
+                                                  prob.z_l[l0:l1], "chol")
+                    ref = np.concatenate([rs, rl])
+                    got = np.concatenate([res[c][0][s0:s1], res[c][1][l0:l1]])
+                d = float(np.max(np.abs(got - ref)))
+                bmx, bnw = max(bmx, d), max(bnw, d / float(np.max(np.abs(ref))))
+                bsn += ref.size
+    finally:
+        O.blas_threads(1)
+    dbeta["big_blocks"] = dict(blocks=int(big.size), max_m=int(m_b.max()), snps_compared=bsn,
+                               max_abs=bmx, normwise_per_block_max=bnw, seconds=time.perf_counter() - t0,
+                               vs="oracle direct fp64 solve (Cholesky) of the reference equations, "
+                                  "every block >= 2000 SNPs" + (", every h2f solve" if sigmas else ""))
+    return cpu, dbeta
 
 
 def main():
@@ -205,73 +358,7 @@ def main():
     cpu = None
     dbeta = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O
-        blas = O.use_blas(True)
-        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        from dbslmm_amd.dist import sub_problem
-        # bounded sample: whole workload repeated if it fits the budget, else blocks in a fixed
-        # random order until the budget is spent (beta compared on exactly those blocks)
-        from dbslmm_amd.dist import block_cost
-        nblk = len(prob.s_ptr) - 1
-        m_b = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
-        cost = block_cost(m_b, prob.n_ref)
-        order = np.random.default_rng(0).permutation(nblk)
-        target = min(cost.sum(), 2e10)            # ~0.1-1 s of 16-thread CPU work per call
-        chunks, cur, acc = [], [], 0.0
-        skipped = int(np.sum(cost > 5 * target))
-        for b in order:
-            if cost[b] > 5 * target:           # keeps one call bounded (largest blocks skipped)
-                continue
-            cur.append(b)
-            acc += cost[b]
-            if acc >= target:
-                chunks.append(np.sort(np.array(cur)))
-                cur, acc = [], 0.0
-        if cur:
-            chunks.append(np.sort(np.array(cur)))
-        reps, tc, snps_done = 0, 0.0, 0
-        cmp_got, cmp_ref = [[] for _ in res], [[] for _ in res]
-        sig_list = sigmas if sigmas else [prob.sigma_s]
-        full_once = False
-        i = 0
-        while tc < args.cpu_seconds and reps < 50:
-            if i >= len(chunks):
-                full_once, i = True, 0
-            blocks = chunks[i]
-            i += 1
-            sub, s_idx, l_idx = sub_problem(prob, blocks)
-            c0 = time.perf_counter()
-            outs = [O.est(sub.bed, sub.n_ref, sub.n_obs, sg, sub.s_ptr, sub.s_pos, sub.z_s,
-                          sub.l_ptr, sub.l_pos, sub.z_l, tau=prob.tau, method="pcg", threads=thr)
-                    for sg in sig_list]      # the reference runs dbslmm once per h2f factor
-            tc += time.perf_counter() - c0
-            snps_done += len(s_idx) + len(l_idx)
-            if not full_once:
-                for c, (rs, rl, _, _) in enumerate(outs):
-                    cmp_ref[c].append(np.concatenate([rs, rl]))
-                    cmp_got[c].append(np.concatenate([res[c][0][s_idx], res[c][1][l_idx]]))
-            if i >= len(chunks):
-                reps += 1
-        what = (f"full workload x{reps}+" if reps else
-                f"{snps_done} of {int(wl['snps'])} SNPs (random block subset"
-                f"{f', {skipped} largest blocks excluded' if skipped else ''})")
-        cpu = dict(value=snps_done / tc, unit="SNPs/s", cores=thr, kind="port",
-                   sample=f"{what} in {tc:.1f} s, {len(sig_list)} solve(s) per SNP as on the GPU: "
-                          f"C restatement of the reference "
-                          f"(byte-wise readSNPIm, N-1 standardise, {'OpenBLAS dsyrk/dgemm/dgemv' if blas else 'plain-loop Gram'}, "
-                          f"Jacobi-PCG tol 1e-7), OpenMP over blocks x{thr}, BLAS 1 thread")
-        mx, nw, ncmp = 0.0, 0.0, 0
-        for c in range(len(res)):
-            ref = np.concatenate(cmp_ref[c])
-            got = np.concatenate(cmp_got[c])
-            ok = np.isfinite(ref)
-            d = float(np.max(np.abs(got[ok] - ref[ok])))
-            mx, nw = max(mx, d), max(nw, d / float(np.max(np.abs(ref[ok]))))
-            ncmp += int(ok.sum())
-        dbeta = dict(max_abs=mx, normwise=nw, snps_compared=ncmp,
-                     vs="CPU reference-faithful PCG (oracle), every h2f solve" if sigmas else
-                        "CPU reference-faithful PCG (oracle)")
+        cpu, dbeta = cpu_leg(args, prob, res, sigmas, wl)
 
     if rank == 0:
         line = {

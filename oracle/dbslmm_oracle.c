@@ -36,6 +36,7 @@ typedef void (*dgemm_fn)(int, int, int, int64_t, int64_t, int64_t, double, const
 typedef void (*dgemv_fn)(int, int, int64_t, int64_t, double, const double*, int64_t, const double*,
                          int64_t, double, double*, int64_t);
 typedef void (*setthr_fn)(int);
+static setthr_fn p_setthr;
 static dsyrk_fn p_dsyrk;
 static dgemm_fn p_dgemm;
 static dgemv_fn p_dgemv;
@@ -47,13 +48,22 @@ int oracle_use_blas(const char* path) {
     p_dsyrk = (dsyrk_fn)dlsym(h, "scipy_cblas_dsyrk64_");
     p_dgemm = (dgemm_fn)dlsym(h, "scipy_cblas_dgemm64_");
     p_dgemv = (dgemv_fn)dlsym(h, "scipy_cblas_dgemv64_");
-    setthr_fn st = (setthr_fn)dlsym(h, "scipy_openblas_set_num_threads64_");
-    if (st) st(1); /* block-level OpenMP over single-threaded BLAS, as the reference */
+    p_setthr = (setthr_fn)dlsym(h, "scipy_openblas_set_num_threads64_");
+    if (p_setthr) p_setthr(1); /* block-level OpenMP over single-threaded BLAS, as the reference */
     if (!p_dsyrk || !p_dgemm || !p_dgemv) { p_dsyrk = 0; p_dgemm = 0; p_dgemv = 0; return -2; }
     return 0;
 }
 
 int oracle_blas_active(void) { return p_dsyrk != 0; }
+
+/* BLAS threads inside one call (default 1 = the reference's -lblas build).  The full-size parity
+ * tests give a single huge block (m ~ 10k) all host cores; NumPy shares this OpenBLAS, so the
+ * setting also governs NumPy's matmul / LAPACK in the same process. */
+int oracle_blas_threads(int n) {
+    if (!p_setthr) return -1;
+    p_setthr(n > 0 ? n : 1);
+    return 0;
+}
 
 /* C(m x m) = A^T A, A col-major n x m (both triangles filled). */
 static void gram_tt(const double* A, int64_t n, int64_t m, double* C) {
@@ -192,6 +202,22 @@ int oracle_bed_maf(const uint8_t* bed, int32_t n_ref, int64_t n_snp, double* maf
 #pragma omp for schedule(static)
         for (int64_t s = 0; s < n_snp; ++s) oracle_read_snp_im(bed, s, idv, n_ref, g, n_ref, &maf[s]);
         free(g);
+    }
+    free(idv);
+    return 0;
+}
+
+/* calcBlock's column loop (dbslmmfit.cpp:419-430) for one block: readSNPIm + nomalizeVec of
+ * bed rows rows[0..m) into out (n_ref x m col-major), columns in parallel. */
+int oracle_read_block_std(const uint8_t* bed, int32_t n_ref, const int32_t* rows, int64_t m,
+                          double* out, int threads) {
+    int32_t* idv = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_ref);
+    for (int i = 0; i < n_ref; ++i) idv[i] = 1;
+#pragma omp parallel for schedule(static) num_threads(threads > 0 ? threads : 1)
+    for (int64_t c = 0; c < m; ++c) {
+        double maf;
+        oracle_read_snp_im(bed, rows[c], idv, n_ref, out + c * (int64_t)n_ref, n_ref, &maf);
+        oracle_normalize(out + c * (int64_t)n_ref, n_ref);
     }
     free(idv);
     return 0;

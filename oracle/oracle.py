@@ -39,6 +39,8 @@ def lib():
         L.oracle_read_snp_im.argtypes = [P, C.c_int64, P, C.c_int64, P, C.c_int64, P]
         L.oracle_normalize.argtypes = [P, C.c_int64]
         L.oracle_bed_maf.argtypes = [P, C.c_int32, C.c_int64, P, C.c_int]
+        L.oracle_blas_threads.argtypes = [C.c_int]
+        L.oracle_read_block_std.argtypes = [P, C.c_int32, P, C.c_int64, P, C.c_int]
         L.oracle_est_block.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, P, C.c_int, P,
                                        C.c_int, P, P, P, P, C.c_int, P]
         L.oracle_est.argtypes = [P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, P, P, P,
@@ -53,6 +55,20 @@ def use_blas(enable: bool = True) -> bool:
         return False
     p = numpy_openblas_path()
     return bool(p) and lib().oracle_use_blas(p.encode()) == 0
+
+
+def blas_threads(n: int) -> bool:
+    """Threads of the shared OpenBLAS (oracle and NumPy) for the calls that follow."""
+    return lib().oracle_blas_threads(int(n)) == 0
+
+
+def read_block_std(bed: np.ndarray, n_ref: int, rows, threads: int = 8) -> np.ndarray:
+    """Standardised n_ref x m block matrix (calcBlock's readSNPIm + nomalizeVec loop)."""
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    out = np.zeros((n_ref, len(rows)), dtype=np.float64, order="F")
+    lib().oracle_read_block_std(_p(np.ascontiguousarray(bed, dtype=np.uint8)), n_ref, _p(rows),
+                                len(rows), _p(out), threads)
+    return out
 
 
 def _p(a):

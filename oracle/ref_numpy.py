@@ -159,19 +159,39 @@ def pcg_m(A, B, maxiter=1000, tol=1e-7):
 def _solve(A, B, method):
     if method == "pcg":
         return pcg_m(A, B) if B.ndim == 2 else pcg_v(A, B)[0]
+    if method == "chol":      # direct, SPD: one Cholesky (used by the full-size parity tests)
+        from scipy.linalg import cho_factor, cho_solve
+        return cho_solve(cho_factor(A, lower=True, check_finite=False), B, check_finite=False)
     return np.linalg.solve(A, B)
 
 
-def est_block_ls(n_ref, n_obs, sigma_s, Xs, Xl, z_s, z_l, tau=0.8, method="pcg"):
-    """estBlock, large + small (dbslmmfit.cpp:680-738). Returns (beta_s, beta_l, Sss, Ssl, Sll)."""
+def _solver(A, method):
+    """x = A^-1 B for repeated right-hand sides of one matrix (factor once when direct)."""
+    if method == "chol":
+        from scipy.linalg import cho_factor, cho_solve
+        cf = cho_factor(A, lower=True, check_finite=False)
+        return lambda B: cho_solve(cf, B, check_finite=False)
+    return lambda B: _solve(A, B, method)
+
+
+def block_sigmas_tau(Xs, Xl, n_ref, tau=0.8):
+    """Sigma_ss, Sigma_ls, Sigma_ll of estBlock (dbslmmfit.cpp:697-709); Xl may be None."""
+    Sss = (Xs.T @ Xs) * (tau / n_ref) + np.eye(Xs.shape[1]) * (1.0 - tau)   # :705-709
+    if Xl is None:
+        return Sss, None, None
     Sls = (Xl.T @ Xs) * (tau / n_ref)                                  # :698-699
     Sll = (Xl.T @ Xl) * (tau / n_ref) + np.eye(Xl.shape[1]) * (1.0 - tau)   # :700-704
-    Sss = (Xs.T @ Xs) * (tau / n_ref) + np.eye(Xs.shape[1]) * (1.0 - tau)   # :705-709
+    return Sss, Sls, Sll
+
+
+def est_block_ls_sigma(Sss, Sls, Sll, n_obs, sigma_s, z_s, z_l, method="pcg"):
+    """estBlock (large + small) from its Sigma blocks (dbslmmfit.cpp:711-729)."""
     d = 1.0 / (sigma_s * n_obs)
-    A = Sss + np.eye(Xs.shape[1]) * d                                  # :712
-    P = _solve(A, Sls.T, method)                                       # :713
+    A = Sss + np.eye(Sss.shape[0]) * d                                 # :712
+    solve_a = _solver(A, method)
+    P = solve_a(Sls.T)                                                 # :713
     S = Sll - Sls @ P                                                  # :714-715
-    q = _solve(A, z_s, method)                                         # :716
+    q = solve_a(z_s)                                                   # :716
     rhs = z_l - Sls @ q                                                # :717-718
     beta_l = _solve(S, rhs, method) / math.sqrt(n_obs)                 # :719-720
     # :723-729 verbatim order of operations
@@ -180,17 +200,28 @@ def est_block_ls(n_ref, n_obs, sigma_s, Xs, Xl, z_s, z_l, tau=0.8, method="pcg")
     w = qs - Pb
     beta_s = math.sqrt(n_obs) * z_s - n_obs * (Sls.T @ beta_l) - Sss @ w
     beta_s = beta_s * sigma_s
+    return beta_s, beta_l
+
+
+def est_block_s_sigma(Sss, n_obs, sigma_s, z_s, method="pcg"):
+    """estBlock (small only) from Sigma_ss (dbslmmfit.cpp:758-764)."""
+    d = 1.0 / (sigma_s * n_obs)
+    A = Sss + np.eye(Sss.shape[0]) * d                                 # :759
+    q = _solve(A, z_s, method)                                         # :760
+    return math.sqrt(n_obs) * sigma_s * (z_s - Sss @ q)                # :761-764
+
+
+def est_block_ls(n_ref, n_obs, sigma_s, Xs, Xl, z_s, z_l, tau=0.8, method="pcg"):
+    """estBlock, large + small (dbslmmfit.cpp:680-738). Returns (beta_s, beta_l, Sss, Ssl, Sll)."""
+    Sss, Sls, Sll = block_sigmas_tau(Xs, Xl, n_ref, tau)
+    beta_s, beta_l = est_block_ls_sigma(Sss, Sls, Sll, n_obs, sigma_s, z_s, z_l, method)
     return beta_s, beta_l, Sss, Sls.T, Sll
 
 
 def est_block_s(n_ref, n_obs, sigma_s, Xs, z_s, tau=0.8, method="pcg"):
     """estBlock, small only (dbslmmfit.cpp:740-770). Returns (beta_s, Sss)."""
-    Sss = (Xs.T @ Xs) * (tau / n_ref) + np.eye(Xs.shape[1]) * (1.0 - tau)
-    d = 1.0 / (sigma_s * n_obs)
-    A = Sss + np.eye(Xs.shape[1]) * d
-    q = _solve(A, z_s, method)
-    beta_s = math.sqrt(n_obs) * sigma_s * (z_s - Sss @ q)
-    return beta_s, Sss
+    Sss, _, _ = block_sigmas_tau(Xs, None, n_ref, tau)
+    return est_block_s_sigma(Sss, n_obs, sigma_s, z_s, method), Sss
 
 
 # ----------------------------------------------------------------------------- host parsing
