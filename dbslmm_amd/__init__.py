@@ -14,7 +14,7 @@ All compute runs on the GPU through the HIP library; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -74,6 +74,9 @@ class BlockProblem:
     l_pos: np.ndarray | None = None
     z_l: np.ndarray | None = None
     tau: float = 0.8
+    # dbslmm_options (path-selection thresholds; missing keys = the library defaults):
+    # tiled_min, gram_big_min, gram_huge_min, h2f_mode (0 auto / 1 merged), cheb_tol
+    opts: dict = field(default_factory=dict)
 
     def __post_init__(self):
         self.bed = np.ascontiguousarray(self.bed, dtype=np.uint8)
@@ -101,10 +104,14 @@ class BlockProblem:
         return 0 if self.l_ptr is None else int(self.l_ptr[-1])
 
     def c_struct(self) -> _lib.Problem:
+        unknown = set(self.opts) - {f[0] for f in _lib.Options._fields_}
+        if unknown:
+            raise ValueError(f"unknown dbslmm_options fields: {sorted(unknown)}")
+        self._opts = _lib.Options(**self.opts)     # kept alive with the problem
         return _lib.Problem(
             _ptr(self.bed), self.bed.size, self.n_ref, self.n_obs, self.sigma_s, self.tau,
             self.num_block, _ptr(self.s_ptr), _ptr(self.s_pos), _ptr(self.z_s),
-            _ptr(self.l_ptr), _ptr(self.l_pos), _ptr(self.z_l))
+            _ptr(self.l_ptr), _ptr(self.l_pos), _ptr(self.z_l), C.pointer(self._opts))
 
 
 class Plan:

@@ -20,12 +20,20 @@ EXPORTS = (
     "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
 )
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv")
 WORKLOAD_LEN = 16
 BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC = 0, 1, 2, 3
+
+
+class Options(C.Structure):
+    """dbslmm_options: path-selection thresholds (0 = default)."""
+    _fields_ = [
+        ("tiled_min", C.c_int32), ("gram_big_min", C.c_int32), ("gram_huge_min", C.c_int32),
+        ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double),
+    ]
 
 
 class Problem(C.Structure):
@@ -34,6 +42,7 @@ class Problem(C.Structure):
         ("sigma_s", C.c_double), ("tau", C.c_double), ("num_block", C.c_int32),
         ("s_ptr", C.c_void_p), ("s_pos", C.c_void_p), ("z_s", C.c_void_p),
         ("l_ptr", C.c_void_p), ("l_pos", C.c_void_p), ("z_l", C.c_void_p),
+        ("opts", C.POINTER(Options)),
     ]
 
 

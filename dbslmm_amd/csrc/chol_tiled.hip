@@ -5,9 +5,9 @@
 //
 //   tchol_region        factor + invert a 128 x 128 diagonal region in LDS (+ pending updates)
 //   tchol_panel         L_i = A_i L_RR^{-T} per 64-row tile below the region (+ pending update)
-//   tchol_trailing2/3   C_IJ -= L_I L_J^T on 128 x 128 tiles, K = 128 x regions per super step
-//   tchol_backward(J)   x_J = X_JJ^T v_J, v_{<J} -= L_{J,<J}^T x_J        (one workgroup per
-//                       256 columns; x_J recomputed per workgroup, v_J is read-only in a launch)
+//   tchol_trailing3     C_IJ -= L_I L_J^T on 128 x 128 tiles, K = 128 x regions per super step
+// followed by one persistent backward substitution over all tiled blocks (trsv.hip,
+// dbslmm_trsv_bwd, plain mode).
 //
 // A 64 x 64 diagonal tile is factored as 2 x 2 tiles of 32 by chol::factor_diag:
 //   L00, X00 = L00^{-1};  L10 = A10 X00^T;  A11 -= L10 L10^T;  L11, X11;  X10 = -X11 L10 X00
@@ -59,17 +59,6 @@ struct TiledArgs {
         return v;
     }
 };
-
-// work list of one launch: act[0..n) = plan block indices, pfx[0..n] = prefix of item counts
-__device__ __forceinline__ int find_item(const int32_t* pfx, int n, int item) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pfx[mid] <= item) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
 
 __device__ __forceinline__ void acc_to_lds_t(const v4d (&acc)[2][2], double* W, int lane) {
 #pragma unroll
@@ -549,128 +538,17 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
 // C(I, J) -= L_I L_J^T on 128 x 128 tiles (I, J in units of 128 rows), K = 128 nk from column
 // c0, one 512-thread workgroup per run of tiles J0..J1 of tile row I.  A 64 x 64 tile does 8 flops
 // per operand byte loaded, which at the f64 MFMA rate needs ~10 TB/s of L2/HBM operand traffic;
-// a 128 x 128 tile halves that (the bulk of the factorisation is bound by it), and reads its MFMA
-// operands from LDS as conflict-free ds_read_b128 pairs:
-//   * K is staged 32 columns at a time: A = -L_I (128 x 32), B = L_J (128 x 32), row-major in LDS
-//     with a 36-double row stride, double-buffered (one barrier per stage); the next stage is
-//     loaded into registers (16-B global loads) while the current one is multiplied;
-//   * wave w (8 waves) owns rows 64 (w >> 2) .., columns 32 (w & 3) .. of the tile: 4 x 2
-//     accumulators of v_mfma_f64_16x16x4_f64.  The MFMA pair (k, k+1) of lane group q takes
-//     k = 8 j + 2 q (+1): one 16-B read per operand row feeds two MFMAs;
-//   * on a diagonal tile (I == J) the two waves wholly above the diagonal skip their MFMAs and
-//     stores; the next tile's C is prefetched during the last stage of the current one.
+// a 128 x 128 tile halves that (the bulk of the factorisation is bound by it).  Wave w (8 waves)
+// owns rows 64 (w >> 2) .., columns 32 (w & 3) .. of the tile: 4 x 2 accumulators of
+// v_mfma_f64_16x16x4_f64; on a diagonal tile (I == J) the two waves wholly above the diagonal
+// skip their MFMAs and stores; the next tile's C is prefetched during the last stage of the
+// current one.  (A register-staged twin and a 64 x 64-tile version were measured slower in
+// round 1 and dropped.)
 namespace chol {
 constexpr int kT2 = 128;                 // tile edge
 constexpr int kK2 = 32;                  // K per stage
-constexpr int kS2 = 36;                  // LDS row stride (doubles)
-constexpr int kOp2 = kT2 * kS2;          // one operand stage buffer
-constexpr int kTrail2Doubles = 4 * kOp2; // A, B x 2 buffers
 constexpr int kRun2 = 2;                 // tiles per run (when a step has plenty of tiles)
-
-__device__ __forceinline__ void t2_load_stage(v2d (&r)[8], const double* A, int ld, int I, int J, int col, int tid) {
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int op = it >> 2, e = (it & 3) * 512 + tid;     // 2048 16-B chunks per operand
-        const int row = e >> 4, kc = (e & 15) * 2;
-        const int rb = kT2 * (op ? J : I);
-        r[it] = *reinterpret_cast<const v2d*>(A + static_cast<int64_t>(rb + row) * ld + col + kc);
-    }
-}
-__device__ __forceinline__ void t2_store_stage(const v2d (&r)[8], double* S, int tid) {
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int op = it >> 2, e = (it & 3) * 512 + tid;
-        const int row = e >> 4, kc = (e & 15) * 2;
-        v2d v = r[it];
-        if (op == 0) v = -v;                                   // A = -L_I: the MFMA subtracts
-        *reinterpret_cast<v2d*>(S + op * kOp2 + row * kS2 + kc) = v;
-    }
-}
-__device__ __forceinline__ void t2_load_c(v4d (&c)[4][2], const double* A, int ld, int r0, int c0, int lane) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                c[i][j][q] = A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)];
-}
-__device__ __forceinline__ void t2_store_c(const v4d (&c)[4][2], double* A, int ld, int r0, int c0, int lane) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)] = c[i][j][q];
-}
-// acc += A_w B_w^T over one 32-deep stage (A already negated)
-__device__ __forceinline__ void t2_mfma_stage(v4d (&acc)[4][2], const double* S, int wr, int wc, int lane) {
-    const double* SA = S + (64 * wr + (lane & 15)) * kS2 + 2 * (lane >> 4);
-    const double* SB = S + kOp2 + (32 * wc + (lane & 15)) * kS2 + 2 * (lane >> 4);
-#pragma unroll
-    for (int j8 = 0; j8 < kK2 / 8; ++j8) {
-        v2d a[4], b[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v2d*>(SA + 16 * i * kS2 + 8 * j8);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const v2d*>(SB + 16 * j * kS2 + 8 * j8);
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][h], b[j][h], acc[i][j], 0, 0, 0);
-    }
-}
 }  // namespace chol
-
-extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing2(
-    chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
-    using namespace chol;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    if (static_cast<int>(blockIdx.x) >= n_items) return;
-    const int32_t it = items[2 * blockIdx.x];
-    if (it < 0) return;
-    const int32_t meta = items[2 * blockIdx.x + 1];
-    const int s = meta >> 8, nk = meta & 255;
-    const int I = (it >> 8) & 255, J0 = it & 255;
-    int b;
-    const TiledArgs a = a0.view(it >> 16, b);
-    const int m = a.blk_m[b], ld = a.blk_ld[b];
-    const int T2 = (m + kT2 - 1) / kT2;
-    const int J1 = min(J0 + run - 1, min(I, T2 - 1));
-    double* A = a.M + a.blk_matoff[b];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
-    const int c0 = 2 * kBT * s;
-    const int nst = 4 * nk;                        // stages per tile
-    const int total = nst * (J1 - J0 + 1);
-    v2d st[8];
-    v4d acc[4][2], nxt[4][2];
-    t2_load_stage(st, A, ld, I, J0, c0, tid);
-    t2_load_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J0 + 32 * wc, lane);
-    for (int g = 0; g < total; ++g) {
-        const int J = J0 + g / nst, t = g % nst;
-        double* S = lds + (g & 1) * 2 * kOp2;
-        t2_store_stage(st, S, tid);
-        __syncthreads();
-        if (g + 1 < total) {
-            const int Jn = J0 + (g + 1) / nst, tn = (g + 1) % nst;
-            t2_load_stage(st, A, ld, I, Jn, c0 + kK2 * tn, tid);
-            if (tn == 0) t2_load_c(nxt, A, ld, kT2 * I + 64 * wr, kT2 * Jn + 32 * wc, lane);
-        }
-        const bool skip = I == J && 32 * wc > 64 * wr + 63;
-        if (!skip) t2_mfma_stage(acc, S, wr, wc, lane);
-        if (t == nst - 1) {
-            if (!skip) t2_store_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J + 32 * wc, lane);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = nxt[i][j];
-        }
-    }
-}
 
 // The same update fed by LDS-DMA (global_load_lds_dwordx4): no staging registers, no LDS store
 // instructions.  Operand rows are unpadded in LDS (32 doubles = 16 chunks of 16 B); the DMA image
@@ -809,94 +687,3 @@ extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
     }
 }
 
-// backward step J (launches J = Kmax-1 .. 0).  v lives in y[row0 ..]; x_J overwrites v_J once
-// it is known.  Workgroup = (block, 256 columns of [0, 64 J)):
-//   x_J: read from y (written by the previous launch) -- or, at a block's first backward step
-//        (J = T-1), computed by every workgroup from the z row;
-//   v[c] -= sum_r L[64 J + r][c] x_J[r]   (column per thread, 64 independent loads);
-//   the workgroup holding tile J-1 then has the final v_{J-1}: it forms x_{J-1} = X^T v_{J-1}
-//   from the stored inverse, writes it over v_{J-1} and scatters beta for tile J-1.
-namespace chol {
-__device__ __forceinline__ void tile_x(const double* A, int ld, int c1, int jmax, const double* vsrc,
-                                       double* D, double* vl, double* red, double* xs, int tid) {
-    // D = stored rows c1.. of the diagonal tile (diagonal + upper = X^T), vl = v_J
-    for (int e = tid; e < kBT * kBT; e += kLargeThreads) {
-        const int r = e >> 6, c = e & 63;
-        D[r * (kBT + 1) + c] = (r < jmax && c < jmax) ? A[static_cast<int64_t>(c1 + r) * ld + c1 + c] : 0.0;
-    }
-    if (tid < kBT) vl[tid] = tid < jmax ? vsrc[c1 + tid] : 0.0;
-    __syncthreads();
-    const int r = tid & 63, g = tid >> 6;
-    double acc = 0.0;
-    for (int c = r + g; c < kBT; c += 4) acc += D[r * (kBT + 1) + c] * vl[c];
-    red[g * kBT + r] = acc;
-    __syncthreads();
-    if (tid < kBT) xs[tid] = (red[tid] + red[kBT + tid]) + (red[2 * kBT + tid] + red[3 * kBT + tid]);
-    __syncthreads();
-}
-}  // namespace chol
-
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_backward(
-    chol::TiledArgs a0, int32_t J, const int32_t* __restrict__ act, const int32_t* __restrict__ pfx,
-    int32_t n) {
-    using namespace chol;
-    __shared__ double D[kBT * (kBT + 1)];
-    __shared__ double vl[kBT];
-    __shared__ double red[4 * kBT];
-    __shared__ double xs[kBT];
-    const int item = blockIdx.x;
-    if (item >= pfx[n]) return;
-    const int s = find_item(pfx, n, item);
-    int b;
-    const TiledArgs a = a0.view(act[s], b);
-    const int chunk = item - pfx[s];
-    const int tid = threadIdx.x;
-    const int row0 = a.blk_row0[b], m = a.blk_m[b], ld = a.blk_ld[b];
-    const double* A = a.M + a.blk_matoff[b];
-    const int T = (m + kBT - 1) / kBT;
-    const bool first = J == T - 1;
-    const double* zrow = A + static_cast<int64_t>(m) * ld;
-    double* v = a.y + row0;
-    const int c1 = kBT * J, jmax = min(kBT, m - c1);
-    const bool fail = a.status[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
-    auto put_beta = [&](int c0, int i, double x) {
-        const double val = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
-        const int o = a.slot_out[row0 + c0 + i];
-        if (o >= 0) a.beta_s[o] = val;
-        else a.beta_l[-1 - o] = val;
-    };
-    if (first) {
-        tile_x(A, ld, c1, jmax, zrow, D, vl, red, xs, tid);
-        if (chunk == 0 && tid < jmax) {
-            v[c1 + tid] = xs[tid];      // x complete in y (the h2f iteration starts from it)
-            put_beta(c1, tid, xs[tid]);
-        }
-    } else {
-        if (tid < kBT) xs[tid] = tid < jmax ? v[c1 + tid] : 0.0;
-        __syncthreads();
-    }
-    const int c = chunk * kLargeThreads + tid;
-    if (c < c1) {
-        const double* Lc = A + static_cast<int64_t>(c1) * ld + c;
-        double part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (jmax == kBT) {
-#pragma unroll
-            for (int r = 0; r < kBT; ++r) part[r & 7] += Lc[static_cast<int64_t>(r) * ld] * xs[r];
-        } else {
-            for (int r = 0; r < jmax; ++r) part[r & 7] += Lc[static_cast<int64_t>(r) * ld] * xs[r];
-        }
-        const double sum = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
-        v[c] = (first ? zrow[c] : v[c]) - sum;
-    }
-    // the workgroup holding tile J-1 finishes it: x_{J-1} over v_{J-1}, beta
-    if (J >= 1 && (c1 - 1) / kLargeThreads == chunk) {
-        __syncthreads();
-        __threadfence_block();
-        const int c0 = c1 - kBT;
-        tile_x(A, ld, c0, kBT, v, D, vl, red, xs, tid);
-        if (tid < kBT) {
-            v[c0 + tid] = xs[tid];
-            put_beta(c0, tid, xs[tid]);
-        }
-    }
-}

@@ -47,7 +47,7 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     // extensions
     int gpu = 0;
     double tau = 0.8;
-    bool precise = false, dry_run = false;
+    bool precise = false, dry_run = false, h2f_merged = false;
     string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
 };
 
@@ -85,7 +85,9 @@ void print_help() {
               << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
               << " --precise-out          17 significant digits in <eff>.txt (extension)\n"
               << " -h2f      [list]       h2 factors, e.g. 0.8,1,1.2: one Gram, one solve per factor,\n"
-              << "                        <eff>_h2f<f>.txt each (software/DBSLMM.R tuning, extension)\n";
+              << "                        <eff>_h2f<f>.txt each (software/DBSLMM.R tuning, extension)\n"
+              << " --h2f-merged           -h2f: one factorisation per factor instead of one factor +\n"
+              << "                        Chebyshev iteration for the big blocks (extension)\n";
 }
 
 // DBSLMM::Assign (scr/dbslmm.cpp:67-172): a flag's value is skipped when it starts with '-'.
@@ -114,6 +116,7 @@ void assign(int argc, char** argv, Param& p) {
         else if (!strcmp(a, "--tau")) { if ((v = take(i))) p.tau = atof(v); }
         else if (!strcmp(a, "--precise-out")) p.precise = true;
         else if (is("--h2f", "-h2f")) { if ((v = take(i))) p.h2f = v; }
+        else if (!strcmp(a, "--h2f-merged")) p.h2f_merged = true;
         else if (!strcmp(a, "--dry-run")) p.dry_run = true;
     }
 }
@@ -436,6 +439,9 @@ int main(int argc, char** argv) {
         prob.l_pos = l_pos.data();
         prob.z_l = z_l.data();
     }
+    dbslmm_options opts{};
+    opts.h2f_mode = p.h2f_merged ? 1 : 0;
+    prob.opts = &opts;
     // h2 factors (software/DBSLMM.R:204-219 runs dbslmm with -h h2 * hh for each hh); without
     // -h2f a single run with factor 1 and the plain <eff>.txt name
     vector<double> factors;

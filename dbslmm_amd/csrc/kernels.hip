@@ -1,27 +1,27 @@
 // kernels.hip -- gfx950 (CDNA4) kernels of the per-LD-block effect-size solver.
 //
-// The hot path of DBSLMMFIT::est (reference scr/dbslmmfit.cpp:56-363) as three launches:
+// The front of the hot path of DBSLMMFIT::est (reference scr/dbslmmfit.cpp:56-363):
 //
 //   dbslmm_unpack_stats  IO::readSNPIm + nomalizeVec statistics (scr/dtpr.cpp:285-380):
-//                        2-bit PLINK rows -> int8 dosages {0,1,2, 0x80 = missing} in a
-//                        block-ordered slot matrix G[slot][individual], plus exact integer
-//                        per-SNP count / sum / sum-of-squares and the fp64 mean, 1/sd (N-1).
-//                        HBM-bound streaming kernel, one wave per SNP row.
-//   dbslmm_gram_i8       estBlock's LD matrices (scr/dbslmmfit.cpp:697-709, 751-756) as ONE
-//                        joint Gram per block over [small | large] SNPs on i8 MFMA
-//                        (v_mfma_i32_32x32x32_i8, exact int32 accumulation) with an fp64
-//                        epilogue that centres, standardises and applies tau:
+//                        2-bit PLINK rows -> the 2-bit DOSAGE operand Gp (codes 0/1/2, 3 =
+//                        missing, padding individuals 0; kpad / 16 dwords per slot, slots in
+//                        block order) plus exact integer per-SNP count / sum / sum-of-squares
+//                        (popcounts) and the fp64 mean and 1/sd (N-1).  HBM-bound, one wave per
+//                        slot.
+//   dbslmm_gram_i8 /     estBlock's LD matrices (scr/dbslmmfit.cpp:697-709, 751-756) as ONE
+//   dbslmm_gram_big /    joint Gram per block over [small | large] SNPs on i8 MFMA
+//   dbslmm_gram_huge     (v_mfma_i32_32x32x32_i8, exact int32 accumulation; each Gp dword is
+//                        expanded to 16 int8 codes in registers / LDS) with an fp64 epilogue that
+//                        centres, standardises and applies tau:
 //                          Sigma_ij = tau/n_ref * C_ij /(s_i s_j) + (1-tau) delta_ij,
 //                          C_ij = G_ij - S_i S_j / n   (no missing calls in the block)
 //                        Blocks with missing calls add the observed-mask Grams (4 MFMAs/step).
-//   dbslmm_chol_solve    the whole per-block solve (PCGm/PCGv at :713-729, :758-764) as one
-//                        SPD solve of the joint matrix
-//                          M = [[Sigma_ss + I/(sigma_s n), Sigma_sl], [Sigma_ls, Sigma_ll]],
-//                          beta = M^{-1} [z_s; z_l] / sqrt(n)
-//                        (block elimination of M reproduces beta_l = S^{-1}(z_l - Sigma_ls q)/sqrt n
-//                        and beta_s = (q - P beta_l sqrt n)/sqrt n of :714-729 exactly; see
-//                        DESIGN.md).  fp64 blocked right-looking Cholesky, one workgroup per
-//                        block, 32x32 tiles staged in LDS.
+//                        32 x 32 tiles per wave (m < 96), 128 x 128 per workgroup, 256 x 256 per
+//                        workgroup (the big blocks).
+//
+// The solve of the joint matrix M = [[Sigma_ss + I/(sigma_s n), Sigma_sl], [Sigma_ls, Sigma_ll]],
+// beta = M^{-1} [z_s; z_l] / sqrt(n) (PCGm/PCGv at :713-729, :758-764) is
+// in chol.hip (dbslmm_chol_small / _large), chol_tiled.hip (dbslmm_tchol_*) and trsv.hip.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

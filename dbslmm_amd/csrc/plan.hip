@@ -40,7 +40,6 @@ constexpr int kEvPerRun = 9;
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
-constexpr size_t kTrail2Lds = sizeof(double) * chol::kTrail2Doubles;
 constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3Doubles;
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
 constexpr int kTiledMinSmall = 256;     // the same when no block reaches kTiledMinDefault
@@ -50,8 +49,8 @@ constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
-    int kind;         // 1 panel, 3 backward, 4 region, 5 trailing (128 x 128 tiles); items of
-                      // kinds 1/4/5 are int32 pairs carrying each block's own step
+    int kind;         // 1 panel, 4 region, 5 trailing (128 x 128 tiles); items are int32 pairs
+                      // carrying each block's own step
     int step;
     int32_t off;      // into d_tlist: act[n] then pfx[n + 1]
     int32_t n;
@@ -62,6 +61,8 @@ struct TLaunch {
 // sync entries of a launch list (lookahead): kind 6 records tiled event `step` on stream `strm`,
 // kind 7 makes stream `strm` wait for it
 constexpr int kTlRecord = 6, kTlWait = 7;
+constexpr int kSuper = 2;               // regions (128 columns) per super step
+constexpr int kGramSq = 4;              // 2D tile squares per XCD of the 256-tile Gram
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 }  // namespace
@@ -114,7 +115,6 @@ struct dbslmm_plan {
     int32_t multi_n = 0;
     hipGraphExec_t graph_multi = nullptr;
     int32_t var_copy = 0;              // copy holding the latest factorisation (variance)
-    bool trail_dma = true;             // 128-tile trailing fed by LDS-DMA (env DBSLMM_TRAIL_DMA=0: registers)
     std::vector<int32_t> h_ld;  // per non-empty block
     std::vector<int32_t> h_m;   // per non-empty block
     std::vector<int32_t> h_tb;  // blocks on the tiled path
@@ -132,14 +132,13 @@ struct dbslmm_plan {
     // iteration vectors [Y, Z, X, R, D, S] x kMaxR x n_slots
     int32_t *d_tri_f = nullptr, *d_tri_b = nullptr, *d_foff = nullptr, *d_tflags = nullptr, *d_tb = nullptr;
     int32_t n_titems = 0, n_tflags = 0;
-    // h2f split: the tiled blocks whose factorisation ends in the first part of the sequence
-    // ("early": their items first in d_tri_f / d_tri_b, their blocks first in d_tb) run their
-    // backward solve and Chebyshev iterations on the main stream as soon as the sequence has
-    // recorded tev[early_ev], overlapping the chain-bound rest of the big blocks' factorisation
-    int32_t n_titems_early = 0, n_tb_early = 0, early_ev = -1;
     int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
-    unsigned long long* d_stamps = nullptr;  // diagnostics only (DBSLMM_TRSV_STAMPS; not owned)
+    int32_t h2f_mode = 0;                    // dbslmm_options.h2f_mode
+    double cheb_tol = 1e-13;                 // dbslmm_options.cheb_tol
+    bool trsv_pending = false;               // a persistent substitution ran since the last error check
+    bool trsv_failed = false;                // ... and one of its hand-off waits gave up (sticky until the next run)
+    unsigned long long* d_stamps = nullptr;  // diagnostic builds (DBSLMM_DIAG) only
     double* d_cheb = nullptr;
     double* d_coef = nullptr;
     int32_t coef_cap = 0;
@@ -191,42 +190,11 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 // super steps starts later, so its heavy first steps overlap the largest block's latency-bound
 // last steps -- no gain measured at configs 3-5).  Each work item is two int32:
 // [block / tile, (local step << 8) | pending panels or K multiple].
-// env DBSLMM_CHEB_SPLIT=1: the early group's substitutions overlap the factorisation's tail.
-// Off by default -- measured at config 4 (56.7 ms/step without): the persistent substitution
-// workgroups hold whole CUs (96 KiB LDS each) for the length of a launch, the chain kernels of
-// the big blocks wait for CUs, and the factorisation grows from 29 to 34-43 ms (n_cu / 2 .. n_cu
-// substitution workgroups), more than the 5.5 ms the later substitutions save.
-// DBSLMM_CHEB_SPLIT=2: both groups after the factorisation, concurrently on two streams with
-// disjoint workgroup budgets: the big blocks' chains (DBSLMM_LATE_GRID workgroups, default 96)
-// and the bandwidth-bound rest (the other CUs).
-static int cheb_split_mode() {
-    const char* e = getenv("DBSLMM_CHEB_SPLIT");
-    return e ? atoi(e) : 0;
-}
-static bool cheb_split() { return cheb_split_mode() != 0; }
-
-// regions (128 columns) per super step (env DBSLMM_SUPER)
-static int tiled_R() {
-    int R = 2;
-    if (const char* e = getenv("DBSLMM_SUPER")) R = std::max(1, std::min(8, atoi(e)));
-    return R;
-}
-
-// g_early >= 0: record event 2 G + 2 on the chain stream after super step g_early's regions and
-// panels (every block whose last super step is <= g_early is then fully factored); *ev_out = its
-// index, or -1
 static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
-                        int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist, int g_early = -1,
-                        int* ev_out = nullptr) {
+                        int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
     struct Blk { int32_t bq; int T64, Tz64, T2, Tz2, nr, S, off; };
-    const int R = tiled_R();
-    if (ev_out) *ev_out = -1;
-    bool right = false;     // measured: no gain at configs 3-5 (the sequence is throughput-bound)
-    if (const char* e = getenv("DBSLMM_ALIGN")) right = atoi(e) != 0;
-    int run2 = chol::kRun2;
-    if (const char* e = getenv("DBSLMM_RUN2")) run2 = std::max(1, atoi(e));
-    bool lookahead = true;  // env DBSLMM_LOOKAHEAD=0: one trailing launch per super step, one stream
-    if (const char* e = getenv("DBSLMM_LOOKAHEAD")) lookahead = atoi(e) != 0;
+    constexpr int R = kSuper;
+    const int run2 = chol::kRun2;
     std::vector<Blk> bl;
     int G = 0, Kmax = 0;
     for (int c = 0; c < copies; ++c)
@@ -243,7 +211,7 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             Kmax = std::max(Kmax, k.T64);
             bl.push_back(k);
         }
-    for (auto& k : bl) k.off = right ? G - k.S : 0;
+    for (auto& k : bl) k.off = 0;   // left-aligned (right alignment measured: no gain at configs 3-5)
     auto push_pairs = [&](int kind, const std::vector<int32_t>& v) {   // plain pair list
         if (v.empty()) return;
         TLaunch L{kind, 0, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(v.size() / 2),
@@ -305,10 +273,6 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             region_launch(rv);
             panel_launch(pv);
         }
-        if (g == g_early && !right) {
-            sync(kTlRecord, 2 * G + 2, 0);
-            if (ev_out) *ev_out = 2 * G + 2;
-        }
         // trailing: 128 x 128 tiles (I, J) right of the super step, rl + jlo <= J <= rl + jhi, LPT
         // over per-XCD queues by tile row
         auto trailing = [&](int jlo, int jhi, int strm, int run_force) {
@@ -343,19 +307,15 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
                 }
             trailing_launch(q, run, strm);
         };
-        if (lookahead) {
-            // the next super step's R tile columns ("near": chain stream, one tile per work item)
-            // are updated first; the rest ("far": stream 1) overlaps the next super step's
-            // regions and panels.  Tiles of near(g) were far(g-1)'s.
-            sync(kTlRecord, 2 * g, 0);
-            if (g > 0) sync(kTlWait, 2 * g - 1, 0);
-            trailing(1, R, 0, 1);
-            sync(kTlWait, 2 * g, 1);
-            trailing(R + 1, 1 << 20, 1, 0);
-            sync(kTlRecord, 2 * g + 1, 1);
-        } else {
-            trailing(1, 1 << 20, 0, 0);
-        }
+        // lookahead: the next super step's R tile columns ("near": chain stream, one tile per
+        // work item) are updated first; the rest ("far": stream 1) overlaps the next super step's
+        // regions and panels.  Tiles of near(g) were far(g-1)'s.
+        sync(kTlRecord, 2 * g, 0);
+        if (g > 0) sync(kTlWait, 2 * g - 1, 0);
+        trailing(1, R, 0, 1);
+        sync(kTlWait, 2 * g, 1);
+        trailing(R + 1, 1 << 20, 1, 0);
+        sync(kTlRecord, 2 * g + 1, 1);
         {   // next super step's first region; region 0 of the blocks that start at g + 1
             std::vector<int32_t> v;
             for (const auto& k : bl) {
@@ -370,26 +330,8 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             region_launch(v);
         }
     }
-    auto add = [&](int kind, int step, const std::vector<int32_t>& act, const std::vector<int32_t>& cnt) {
-        if (act.empty()) return;
-        TLaunch L{kind, step, static_cast<int32_t>(tlist.size()), static_cast<int32_t>(act.size()), 0};
-        tlist.insert(tlist.end(), act.begin(), act.end());
-        int32_t acc = 0;
-        tlist.push_back(0);
-        for (int32_t c : cnt) tlist.push_back(acc += c);
-        L.items = acc;
-        tl.push_back(L);
-    };
-    if (lookahead && G > 0) sync(kTlWait, 2 * G - 1, 0);   // the last far update
-    for (int J = Kmax - 1; J >= 0; --J) {
-        std::vector<int32_t> ba, bc;
-        for (const auto& k : bl)
-            if (k.T64 > J) {
-                ba.push_back(k.bq);
-                bc.push_back(std::max(1, (chol::kBT * J + chol::kLargeThreads - 1) / chol::kLargeThreads));
-            }
-        add(3, J, ba, bc);
-    }
+    if (G > 0) sync(kTlWait, 2 * G - 1, 0);   // the last far update
+    // (the backward substitution is one persistent launch after the sequence: run_pbwd)
 }
 
 template <int NR>
@@ -400,23 +342,6 @@ static hipError_t set_trsv_lds() {
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_bwd<NR>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
-}
-
-// The lookahead's bulk-trailing stream.  Env DBSLMM_CHAIN_CUS=k (diagnostic): a CU mask keeps
-// k CUs (spread over the XCDs) free of the bulk so the latency-bound chain kernels of the other
-// stream find them idle.
-static hipError_t create_far_stream(int device, hipStream_t* st) {
-    int k = 0;
-    if (const char* e = getenv("DBSLMM_CHAIN_CUS")) k = atoi(e);
-    int ncu = 0;
-    if (k <= 0 || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-        ncu <= k)
-        return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    const int stride = ncu / k;
-    for (int i = 0; i < ncu; ++i)
-        if (!(i % stride == stride - 1 && i / stride < k)) mask[i / 32] |= 1u << (i % 32);
-    return hipExtStreamCreateWithCUMask(st, static_cast<uint32_t>(mask.size()), mask.data());
 }
 
 extern "C" {
@@ -436,7 +361,7 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        create_far_stream(device, &c->stream3) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
@@ -456,9 +381,6 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kTrail3Lds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing2),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTrail2Lds)) != hipSuccess ||
         set_trsv_lds<1>() != hipSuccess || set_trsv_lds<2>() != hipSuccess ||
         hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         dbslmm_ctx_destroy(c);
@@ -490,7 +412,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
-                    p->d_cheb, p->d_coef};
+                    p->d_cheb, p->d_coef, p->d_stamps};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -525,7 +447,11 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->bytes_per_snp = bps;
     p->kpad = round_up(pr->n_ref, gram::kKS);
     p->bed_len = pr->bed_len;
-    if (const char* e = getenv("DBSLMM_TRAIL_DMA")) p->trail_dma = atoi(e) != 0;
+    const dbslmm_options op = pr->opts ? *pr->opts : dbslmm_options{};
+    ARG_CHECK(ctx, op.tiled_min >= 0 && op.gram_big_min >= 0 && op.gram_huge_min >= 0 &&
+                   (op.h2f_mode == 0 || op.h2f_mode == 1) && op.cheb_tol >= 0.0, "bad dbslmm_options");
+    p->h2f_mode = op.h2f_mode;
+    if (op.cheb_tol > 0.0) p->cheb_tol = std::max(1e-16, op.cheb_tol);
     p->n_s = pr->s_ptr[pr->num_block];
     p->n_l = has_l ? pr->l_ptr[pr->num_block] : 0;
 
@@ -534,20 +460,17 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::vector<double> z;
     std::vector<int64_t> matoff;
     std::vector<GramTile> tiles;
-    int64_t gram_big_min = kGramBigMinDefault;
-    if (const char* env = getenv("DBSLMM_GRAM_BIG_MIN")) gram_big_min = std::max<int64_t>(1, atoll(env));
+    const int64_t gram_big_min = op.gram_big_min > 0 ? op.gram_big_min : kGramBigMinDefault;
     // the 256-tile kernel pays once its K loop outweighs its 512 KB fp64 epilogue per tile
-    int64_t gram_huge_min = p->kpad >= 4096 ? kGramHugeMinDefault : 2 * kGramHugeMinDefault;
-    if (const char* env = getenv("DBSLMM_GRAM_HUGE_MIN")) gram_huge_min = std::max<int64_t>(1, atoll(env));
-    int gram_sq = 4;                   // 2D tile squares per XCD for the 256-tile Gram (env)
-    if (const char* env = getenv("DBSLMM_GRAM_SQ")) gram_sq = std::max(1, atoi(env));
+    const int64_t gram_huge_min = op.gram_huge_min > 0 ? op.gram_huge_min
+                                  : p->kpad >= 4096 ? kGramHugeMinDefault : 2 * kGramHugeMinDefault;
     std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd);
     std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0);
     int64_t moff = 0;
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
-    if (const char* env = getenv("DBSLMM_TILED_MIN")) {
-        tiled_min = std::max<int64_t>(64, atoll(env));
+    if (op.tiled_min > 0) {
+        tiled_min = std::max<int64_t>(64, op.tiled_min);
     } else {
         // no block reaches the default: the single-workgroup solve of the largest blocks is then
         // the critical path itself, and spreading the blocks of >= kTiledMinSmall SNPs over many
@@ -608,25 +531,17 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         }
         if (m >= gram_huge_min) {   // 256 x 256 tiles
             const int T = static_cast<int>((m + gram::kHT - 1) / gram::kHT);
-            if (gram_sq > 1) {
-                // squares of gram_sq x gram_sq tiles (lower triangle), each on the least-loaded
-                // XCD: the workgroups in flight on an XCD share gram_sq row panels of each operand
-                for (int si = 0; si < T; si += gram_sq)
-                    for (int sj = 0; sj <= si; sj += gram_sq) {
-                        const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
-                        for (int ti = si; ti < std::min(T, si + gram_sq); ++ti)
-                            for (int tj = sj; tj < std::min(ti + 1, sj + gram_sq); ++tj) {
-                                hq[x].push_back({nb, ti, tj, 0});
-                                hload[x] += 1;
-                            }
-                    }
-            } else {                 // each tile row on the least-loaded XCD
-                for (int ti = 0; ti < T; ++ti) {
+            // squares of kGramSq x kGramSq tiles (lower triangle), each on the least-loaded XCD:
+            // the workgroups in flight on an XCD share kGramSq row panels of each operand
+            for (int si = 0; si < T; si += kGramSq)
+                for (int sj = 0; sj <= si; sj += kGramSq) {
                     const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
-                    for (int tj = 0; tj <= ti; ++tj) hq[x].push_back({nb, ti, tj, 0});
-                    hload[x] += ti + 1;
+                    for (int ti = si; ti < std::min(T, si + kGramSq); ++ti)
+                        for (int tj = sj; tj < std::min(ti + 1, sj + kGramSq); ++tj) {
+                            hq[x].push_back({nb, ti, tj, 0});
+                            hload[x] += 1;
+                        }
                 }
-            }
             ops_exec += 2.0 * p->kpad * gram::kHT * gram::kHT * (T * (T + 1) / 2);
         } else if (m >= gram_big_min) {   // 128 x 128 tiles, the block's queue on the least-loaded XCD
             const int T = static_cast<int>((m + gram::kGT - 1) / gram::kGT);
@@ -678,7 +593,6 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                 order.end());
     for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
     std::vector<int32_t> tlist;
-    std::vector<char> is_early(std::max(1, p->n_nonempty), 0);
     {
         std::vector<int32_t> tb;
         for (int b = 0; b < p->n_nonempty; ++b)
@@ -686,26 +600,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         p->n_tiled = static_cast<int32_t>(tb.size());
         p->h_m = mv;
         p->h_tb = tb;
-        // h2f split (env DBSLMM_CHEB_SPLIT=1, see cheb_split): blocks whose last super step is at
-        // most g_early = DBSLMM_SPLIT_FRAC (0.5) of the sequence form the early group
-        const int R = tiled_R();
-        auto last_step = [&](int32_t b) {
-            const int T64 = (mv[b] + chol::kBT - 1) / chol::kBT;
-            return ((T64 + 1) / 2 + R - 1) / R - 1;
-        };
-        int G = 0;
-        for (int32_t b : tb) G = std::max(G, last_step(b) + 1);
-        int g_early = -1;
-        if (cheb_split() && G > 1) {
-            double frac = 0.5;
-            if (const char* e = getenv("DBSLMM_SPLIT_FRAC")) frac = atof(e);
-            g_early = static_cast<int>(frac * (G - 1));
-            int ne = 0;
-            for (int32_t b : tb) ne += last_step(b) <= g_early;
-            if (ne == 0 || ne == static_cast<int>(tb.size())) g_early = -1;
-        }
-        for (int32_t b : tb) is_early[b] = g_early >= 0 && last_step(b) <= g_early;
-        build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist, g_early, &p->early_ev);
+        build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist);
     }
     // substitution work lists (trsv.hip): 64-row tiles of the tiled blocks; forward in order of
     // (tile, block), backward in order of (tiles from the end, block) -- every dependency of an
@@ -721,36 +616,21 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         }
         p->n_tflags = nf;
         (void)tmax;
-        // ticket order: tile position relative to the block's length (ties: longer block first),
+        // ticket order: tile position relative to the block's length minus alpha T / Tmax (bigger
+        // blocks' tiles are claimed earlier: their chains are longer; ties: longer block first),
         // monotone in the position within each block, so every dependency comes earlier
         struct It { double key; int T; int32_t b, I; };
         std::vector<It> v;
-        int32_t only = -1;   // diagnostics: DBSLMM_TRSV_ONLY_BIGGEST=1 keeps the largest block alone
-        if (getenv("DBSLMM_TRSV_ONLY_BIGGEST") && !p->h_tb.empty()) {
-            only = p->h_tb[0];
-            for (int32_t b : p->h_tb) if (mv[b] > mv[only]) only = b;
-        }
-        int order = 0;   // 0: I / T - alpha T / Tmax, 1: I - T, 2: I, 3: I - T / 2
-        if (const char* e = getenv("DBSLMM_TRSV_ORDER")) order = atoi(e);
-        double alpha = 0.25; // bigger blocks' tiles are claimed earlier (their chains are longer)
-        if (const char* e = getenv("DBSLMM_TRSV_ALPHA")) alpha = atof(e);
+        constexpr double alpha = 0.25;
         int tmx = 1;
         for (int32_t b : p->h_tb) tmx = std::max(tmx, (mv[b] + trsv::kT - 1) / trsv::kT);
         for (int32_t b : p->h_tb) {
-            if (only >= 0 && b != only) continue;
             const int T = (mv[b] + trsv::kT - 1) / trsv::kT;
-            for (int I = 0; I < T; ++I) {
-                const double key = order == 1 ? I - T : order == 2 ? I : order == 3 ? I - 0.5 * T
-                                   : static_cast<double>(I) / T - alpha * T / tmx;
-                v.push_back({key, T, b, I});
-            }
+            for (int I = 0; I < T; ++I) v.push_back({static_cast<double>(I) / T - alpha * T / tmx, T, b, I});
         }
-        // early group first (its launches take the prefix of the lists)
         std::stable_sort(v.begin(), v.end(), [&](const It& x, const It& y) {
-            if (is_early[x.b] != is_early[y.b]) return is_early[x.b] > is_early[y.b];
             return x.key != y.key ? x.key < y.key : x.T > y.T;
         });
-        for (const It& x : v) p->n_titems_early += is_early[x.b] ? 1 : 0;
         for (const It& x : v) {
             tri_f.push_back(x.b);
             tri_f.push_back(x.I);
@@ -816,14 +696,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_tri_f, tri_f)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_tri_b, tri_b)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_foff, foff)) != hipSuccess) return fail("upload trsv lists");
-    {
-        std::vector<int32_t> tbg;
-        for (int32_t b : p->h_tb) if (is_early[b]) tbg.push_back(b);
-        p->n_tb_early = static_cast<int32_t>(tbg.size());
-        for (int32_t b : p->h_tb) if (!is_early[b]) tbg.push_back(b);
-        if ((e = dev_upload(&p->d_tb, tbg)) != hipSuccess) return fail("upload trsv lists");
-    }
-    // [tile flags | ticket counter | error word | ticket counter of the early group's launches]
+    if ((e = dev_upload(&p->d_tb, p->h_tb)) != hipSuccess) return fail("upload trsv lists");
+    // [tile flags | ticket counter | error word | spare]
     if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
     if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
     const size_t ns = std::max<size_t>(1, p->n_slots);
@@ -879,7 +753,7 @@ static int collect_timing(dbslmm_plan* p) {
 // copy: the list is a single-copy list applied to factorisation copy `copy` (its matrix, sigma
 // scalar, scratch, betas and status); multi-copy lists address the copies themselves (copy 0).
 static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist,
-                         int copy = 0, bool skip_bwd = false) {
+                         int copy = 0) {
     dbslmm_ctx* ctx = p->ctx;
     const int64_t c = copy;
     const chol::TiledArgs ta{p->d_M + c * p->M_elems, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
@@ -899,20 +773,13 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
         hipStream_t st = L.strm ? ctx->stream3 : ctx->stream2;
         if (L.kind == kTlRecord) { HIP_TRY(ctx, hipEventRecord(p->tev[L.step], st)); continue; }
         if (L.kind == kTlWait) { HIP_TRY(ctx, hipStreamWaitEvent(st, p->tev[L.step], 0)); continue; }
-        if (L.items == 0 || (skip_bwd && L.kind == 3)) continue;
+        if (L.items == 0) continue;
         const int32_t* act = d_tlist + L.off;
-        const int32_t* pfx = act + L.n;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
         switch (L.kind) {
         case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, act, L.items); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, act, L.items); break;
-        case 5:
-            if (p->trail_dma)
-                hipLaunchKernelGGL(dbslmm_tchol_trailing3, g, dim3(512), kTrail3Lds, st, ta, L.n, act, L.items);
-            else
-                hipLaunchKernelGGL(dbslmm_tchol_trailing2, g, dim3(512), kTrail2Lds, st, ta, L.n, act, L.items);
-            break;
-        default: hipLaunchKernelGGL(dbslmm_tchol_backward, g, blk, 0, st, ta, L.step, act, pfx, L.n); break;
+        default: hipLaunchKernelGGL(dbslmm_tchol_trailing3, g, dim3(512), kTrail3Lds, st, ta, L.n, act, L.items); break;
         }
     }
     HIP_TRY(ctx, hipGetLastError());
@@ -947,25 +814,12 @@ static int ensure_copies(dbslmm_plan* p, int n) {
     return DBSLMM_OK;
 }
 
-static bool tiled_use_graph() {
-    static const bool v = [] {
-        const char* e = getenv("DBSLMM_TGRAPH");
-        return !e || atoi(e) != 0;
-    }();
-    return v;
-}
-
 extern "C++" {
 template <int NR>
 static void launch_trsv(bool fwd, int grid, hipStream_t st, const trsv::Args& a) {
     if (fwd) hipLaunchKernelGGL(dbslmm_trsv_fwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
     else hipLaunchKernelGGL(dbslmm_trsv_bwd<NR>, dim3(grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
 }
-}
-
-static bool persistent_bwd() {   // env DBSLMM_PBWD=0: the per-tile backward launches instead
-    const char* e = getenv("DBSLMM_PBWD");
-    return !e || atoi(e) != 0;
 }
 
 // Backward substitution of factorisation copy `copy`'s tiled blocks in one persistent launch
@@ -979,30 +833,9 @@ struct TGroup {
     int32_t* ctr;
     int grid;
 };
-static int late_grid(const dbslmm_plan* p) {
-    int g = 96;
-    if (const char* e = getenv("DBSLMM_LATE_GRID")) g = atoi(e);
-    return std::max(8, std::min(p->ctx->n_cu - 8, g));
-}
 static TGroup tgroup_all(const dbslmm_plan* p) {
-    int cap = p->ctx->n_cu;   // env DBSLMM_TRSV_GRID (diagnostic): fewer substitution workgroups
-    if (const char* e = getenv("DBSLMM_TRSV_GRID")) cap = std::max(1, atoi(e));
     return TGroup{0, p->n_titems, 0, p->n_tiled, p->ctx->stream2, p->d_tflags + p->n_tflags,
-                  std::max(1, std::min(cap, p->n_titems))};
-}
-static TGroup tgroup_late(const dbslmm_plan* p) {
-    const int32_t n = p->n_titems - p->n_titems_early;
-    const int cap = cheb_split_mode() == 2 ? late_grid(p) : p->ctx->n_cu;
-    return TGroup{p->n_titems_early, n, p->n_tb_early, p->n_tiled - p->n_tb_early, p->ctx->stream2,
-                  p->d_tflags + p->n_tflags, std::max(1, std::min(cap, n))};
-}
-// the early group shares the GPU with the rest of the tiled sequence: at most DBSLMM_SPLIT_GRID
-// (default n_cu / 2) workgroups, so the chain kernels of the big blocks keep CUs
-static TGroup tgroup_early(const dbslmm_plan* p) {
-    int cap = cheb_split_mode() == 2 ? p->ctx->n_cu - late_grid(p) : p->ctx->n_cu / 2;
-    if (const char* e = getenv("DBSLMM_SPLIT_GRID")) cap = std::max(1, atoi(e));
-    return TGroup{0, p->n_titems_early, 0, p->n_tb_early, p->ctx->stream, p->d_tflags + p->n_tflags + 2,
-                  std::max(1, std::min(cap, p->n_titems_early))};
+                  std::max(1, std::min(p->ctx->n_cu, p->n_titems))};
 }
 
 static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
@@ -1043,27 +876,23 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
         p->trsv_epoch = 1;
     }
     a.epoch = p->trsv_epoch;
-    if (a.n_items > 0) launch_trsv<1>(false, a.grid, st, a);
+    if (a.n_items > 0) {
+        launch_trsv<1>(false, a.grid, st, a);
+        p->trsv_pending = true;
+    }
     HIP_TRY(ctx, hipGetLastError());
     return DBSLMM_OK;
 }
 
-// The single-copy tiled sequence on factorisation copy `copy` (stream2), replayed from a graph
-// captured per copy; its backward substitution is one persistent launch (run_pbwd) unless
-// DBSLMM_PBWD=0.
-static int run_tiled_copy(dbslmm_plan* p, double isn, int copy, bool with_pbwd = true) {
+// Capture a launch list into a graph on stream2 (once; sigma is read from device scalars, so the
+// graph stays valid) and replay it.
+static int launch_graph(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist,
+                        int copy, hipGraphExec_t& gx) {
     dbslmm_ctx* ctx = p->ctx;
-    const bool pb = persistent_bwd();
-    if (!tiled_use_graph()) {
-        const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy, pb);
-        return rc != DBSLMM_OK || !pb || !with_pbwd ? rc : run_pbwd(p, isn, copy, tgroup_all(p));
-    }
-    if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
-    hipGraphExec_t& gx = p->graph_copy[copy];
     if (!gx) {
         hipGraph_t gr = nullptr;
         HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-        const int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, copy, pb);
+        const int rc = enqueue_tiled(p, isn, tl, d_tlist, copy);
         hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
         if (rc != DBSLMM_OK) {
             if (gr) (void)hipGraphDestroy(gr);
@@ -1075,7 +904,15 @@ static int run_tiled_copy(dbslmm_plan* p, double isn, int copy, bool with_pbwd =
         HIP_TRY(ctx, ie);
     }
     HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
-    return pb && with_pbwd ? run_pbwd(p, isn, copy, tgroup_all(p)) : DBSLMM_OK;
+    return DBSLMM_OK;
+}
+
+// The single-copy tiled sequence on factorisation copy `copy` (stream2, one graph per copy),
+// then its backward substitution as one persistent launch (run_pbwd).
+static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
+    if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
+    const int rc = launch_graph(p, isn, p->tl, p->d_tlist, copy, p->graph_copy[copy]);
+    return rc != DBSLMM_OK ? rc : run_pbwd(p, isn, copy, tgroup_all(p));
 }
 
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
@@ -1091,9 +928,7 @@ struct ChebPlan {
 // M_b^{-1} M_c lies in [1, 1 + delta / (d_b + 1 - tau)] (delta > 0) or its mirror (delta < 0).
 // Not applicable (false): tau outside (0, 1], or more than 60 iterations needed.
 static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPlan& cp) {
-    const char* env = getenv("DBSLMM_H2F_CHEB");
-    const bool enabled = !env || atoi(env) != 0;
-    if (!enabled || n < 2 || p->n_tiled == 0 || !(p->tau > 0.0 && p->tau <= 1.0)) return false;
+    if (p->h2f_mode != 0 || n < 2 || p->n_tiled == 0 || !(p->tau > 0.0 && p->tau <= 1.0)) return false;
     std::vector<int> idx(n);
     std::iota(idx.begin(), idx.end(), 0);
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return sigmas[a] < sigmas[b]; });
@@ -1101,8 +936,7 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
     const double nobs = static_cast<double>(p->n_obs);
     const double db = 1.0 / (sigmas[cp.base] * nobs);
     const double floor_ = db + 1.0 - p->tau;
-    double tol = 1e-13;
-    if (const char* e = getenv("DBSLMM_CHEB_TOL")) tol = std::max(1e-16, atof(e));
+    const double tol = p->cheb_tol;
     for (int c = 0; c < n; ++c)
         if (c != cp.base) cp.others.push_back(c);
     for (size_t g0 = 0; g0 < cp.others.size(); g0 += trsv::kMaxR) {
@@ -1118,7 +952,7 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
             if (!(lo[j] > 0.0)) return false;
             // Chebyshev: error <= 2 q^K x the initial error x_c - x_b, itself <= |ext| relative
             // (the same bound); K so that the final error is 1e-13 of the solution (below the
-            // forward error of the fp64 Cholesky solve itself; env DBSLMM_CHEB_TOL overrides)
+            // forward error of the fp64 Cholesky solve itself; dbslmm_options.cheb_tol)
             const double kap = hi[j] / lo[j], q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
             const double e0 = std::max(std::fabs(ext), 1e-300);
             const int k = q < 1e-300 ? 1 : std::max(1, static_cast<int>(std::ceil(std::log(tol / e0) / std::log(q))));
@@ -1217,15 +1051,15 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
         a.nl_stride = p->n_l;
         for (int j = 0; j < trsv::kMaxR; ++j) a.cix[j] = cix[j];
         a.status = p->d_status + cp.base * p->nbk;
-        static unsigned long long* d_stamps = nullptr;   // diagnostics: the largest tiled block
+#ifdef DBSLMM_DIAG   // diagnostic build: per-tile stamps of the largest tiled block
         if (getenv("DBSLMM_TRSV_STAMPS")) {
             int bmax = p->h_tb[0];
             for (int32_t b : p->h_tb) if (p->h_m[b] > p->h_m[bmax]) bmax = b;
-            if (!d_stamps) HIP_TRY(ctx, hipMalloc(&d_stamps, 8 * 4096 * sizeof(unsigned long long)));
-            a.stamps = d_stamps;
+            if (!p->d_stamps) HIP_TRY(ctx, hipMalloc(&p->d_stamps, 8 * 4096 * sizeof(unsigned long long)));
+            a.stamps = p->d_stamps;
             a.stamp_b = bmax;
-            p->d_stamps = d_stamps;
         }
+#endif
         const int K = cp.iters[g];
         a.grid = grid;
         for (int k = 0; k < K; ++k) {
@@ -1244,12 +1078,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
                 if (nr == 1) launch_trsv<1>(fwd, grid, st, a);
                 else launch_trsv<2>(fwd, grid, st, a);
                 HIP_TRY(ctx, hipGetLastError());
-                if (getenv("DBSLMM_TRSV_SYNC")) {   // diagnostics: one launch at a time
-                    fprintf(stderr, "trsv g%zu k%d pass%d nr%d n_items %d grid %d ...", g, k, pass, nr,
-                            a.n_items, grid);
-                    HIP_TRY(ctx, hipStreamSynchronize(st));
-                    fprintf(stderr, " done\n");
-                }
+                p->trsv_pending = true;
             }
         }
     }
@@ -1278,6 +1107,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         }
     }
     // h2f: the tiled blocks are factored once (copy cp.base) and the other copies iterate on it
+    p->trsv_failed = false;
     ChebPlan cp;
     const bool cheb = front && p->n_nonempty > 0 && cheb_plan(p, sigmas, n, cp);
     const int32_t tcopy = cheb ? cp.base : -1;   // Gram epilogues: tiled blocks write this copy only
@@ -1379,38 +1209,9 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         if (!tl.empty()) {
             // the tiled sequence (~2.5 launches per 128 columns) is replayed from a graph
             // captured on first use (sigma is read from device scalars, so it stays valid)
-            hipGraphExec_t& gx = n > 1 ? p->graph_multi : p->graph_exec;
-            const bool single = n == 1 && persistent_bwd();   // one copy: run_tiled_copy's path
-            const bool use_graph = tiled_use_graph() && !cheb && !single;
-            if (single) {
+            if (n == 1) {
                 const int rc = run_tiled_copy(p, isn, 0);
                 if (rc != DBSLMM_OK) return rc;
-            } else if (cheb && p->n_titems_early > 0 && persistent_bwd() && cheb_split_mode() == 2) {
-                // h2f, split after the factorisation: the two groups' backward solves and
-                // iterations concurrently, the rest on the main stream
-                int rc = run_tiled_copy(p, isn, cp.base, false);
-                if (rc != DBSLMM_OK) return rc;
-                HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
-                HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join3, 0));
-                const TGroup ge = tgroup_early(p), gl = tgroup_late(p);
-                if ((rc = run_pbwd(p, isn, cp.base, ge)) != DBSLMM_OK) return rc;
-                if ((rc = run_cheb(p, isn, cp, ge)) != DBSLMM_OK) return rc;
-                if ((rc = run_pbwd(p, isn, cp.base, gl)) != DBSLMM_OK) return rc;
-                if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
-                if ((rc = run_cheb(p, isn, cp, gl)) != DBSLMM_OK) return rc;
-            } else if (cheb && p->early_ev >= 0 && p->n_titems_early > 0 && persistent_bwd() && cheb_split()) {
-                // h2f, split: the sequence by direct launches (its early-group event is waited on
-                // by the main stream), the early group's backward solve + iterations on the main
-                // stream as soon as its blocks are factored, the rest after the sequence
-                int rc = enqueue_tiled(p, isn, p->tl, p->d_tlist, cp.base, true);
-                if (rc != DBSLMM_OK) return rc;
-                HIP_TRY(ctx, hipStreamWaitEvent(s, p->tev[p->early_ev], 0));
-                const TGroup ge = tgroup_early(p), gl = tgroup_late(p);
-                if ((rc = run_pbwd(p, isn, cp.base, ge)) != DBSLMM_OK) return rc;
-                if ((rc = run_cheb(p, isn, cp, ge)) != DBSLMM_OK) return rc;
-                if ((rc = run_pbwd(p, isn, cp.base, gl)) != DBSLMM_OK) return rc;
-                if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
-                if ((rc = run_cheb(p, isn, cp, gl)) != DBSLMM_OK) return rc;
             } else if (cheb) {
                 // h2f: factor only the base copy, iterate the others on its factor
                 int rc = run_tiled_copy(p, isn, cp.base);
@@ -1418,31 +1219,12 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                 if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
                 rc = run_cheb(p, isn, cp, tgroup_all(p));
                 if (rc != DBSLMM_OK) return rc;
-            } else if (!use_graph) {
-                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist, 0,
-                                             persistent_bwd());
+            } else {
+                // merged copies: one sequence factors every copy, then one backward launch each
+                int rc = launch_graph(p, isn, tl, p->d_tlist_multi, 0, p->graph_multi);
+                for (int c = 0; c < n && rc == DBSLMM_OK; ++c) rc = run_pbwd(p, isn, c, tgroup_all(p));
                 if (rc != DBSLMM_OK) return rc;
-            } else if (!gx) {
-                hipGraph_t gr = nullptr;
-                HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-                const int rc = enqueue_tiled(p, isn, tl, n > 1 ? p->d_tlist_multi : p->d_tlist, 0,
-                                             persistent_bwd());
-                hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
-                if (rc != DBSLMM_OK) {
-                    if (gr) (void)hipGraphDestroy(gr);
-                    return rc;
-                }
-                HIP_TRY(ctx, ce);
-                hipError_t ie = hipGraphInstantiate(&gx, gr, nullptr, nullptr, 0);
-                (void)hipGraphDestroy(gr);
-                HIP_TRY(ctx, ie);
             }
-            if (use_graph) HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
-            if (!single && !cheb && persistent_bwd())   // merged copies: one backward launch each
-                for (int c = 0; c < n; ++c) {
-                    const int rc = run_pbwd(p, isn, c, tgroup_all(p));
-                    if (rc != DBSLMM_OK) return rc;
-                }
         }
         if (ev && !cheb) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));
@@ -1472,20 +1254,31 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     return DBSLMM_OK;
 }
 
+// After the main stream has drained: the error word of the persistent substitutions (trsv.hip:
+// a bounded hand-off wait that gave up means the tiled blocks' betas of that run are invalid).
+// Read and cleared after every run that launched one; the failure stays reported until the next run.
+static int check_trsv(dbslmm_plan* p) {
+    dbslmm_ctx* ctx = p->ctx;
+    if (p->trsv_pending) {
+        int32_t werr = 0;
+        HIP_TRY(ctx, hipMemcpy(&werr, p->d_tflags + p->n_tflags + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (werr) HIP_TRY(ctx, hipMemset(p->d_tflags + p->n_tflags + 1, 0, sizeof(int32_t)));
+        p->trsv_pending = false;
+        p->trsv_failed = p->trsv_failed || werr != 0;
+    }
+    if (p->trsv_failed) {
+        ctx->err = "substitution hand-off wait gave up (trsv): the tiled blocks' betas of this run are invalid";
+        return DBSLMM_E_HIP;
+    }
+    return DBSLMM_OK;
+}
+
 static int download_copy(dbslmm_plan* p, int c, double* beta_s, double* beta_l, int32_t* block_status) {
     dbslmm_ctx* ctx = p->ctx;
     if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (p->d_tflags && p->cheb_base >= 0) {
-        int32_t werr = 0;
-        HIP_TRY(ctx, hipMemcpy(&werr, p->d_tflags + p->n_tflags + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
-        if (werr) {
-            (void)hipMemset(p->d_tflags + p->n_tflags + 1, 0, sizeof(int32_t));
-            ctx->err = "substitution hand-off wait gave up (trsv)";
-            return DBSLMM_E_HIP;
-        }
-    }
+    if (const int rc = check_trsv(p)) return rc;
     if (beta_s && p->n_s)
         HIP_TRY(ctx, hipMemcpy(beta_s, p->d_beta_s + c * p->n_s, p->n_s * sizeof(double), hipMemcpyDeviceToHost));
     if (beta_l && p->n_l)
@@ -1527,6 +1320,7 @@ int dbslmm_plan_sync(dbslmm_plan* p) {
     if (!p) return DBSLMM_E_ARG;
     HIP_TRY(p->ctx, hipSetDevice(p->ctx->device));
     HIP_TRY(p->ctx, hipStreamSynchronize(p->ctx->stream));
+    if (const int rc = check_trsv(p)) return rc;
     if (p->timing) return collect_timing(p);
     p->runs_pending = 0;
     return DBSLMM_OK;
@@ -1539,13 +1333,15 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* p, double* ms_out, int32_t* launches_out)
     return DBSLMM_OK;
 }
 
-// diagnostics (not in the public header): the substitution stamps of the last forward launch
+#ifdef DBSLMM_DIAG
+// diagnostic build only (not in the public header): the substitution stamps of the last forward launch
 extern "C" int dbslmm_diag_trsv_stamps(dbslmm_plan* p, unsigned long long* out, int n) {
     if (!p || !p->d_stamps) return DBSLMM_E_STATE;
     if (hipDeviceSynchronize() != hipSuccess) return DBSLMM_E_HIP;
     return hipMemcpy(out, p->d_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess
                ? DBSLMM_OK : DBSLMM_E_HIP;
 }
+#endif
 
 int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     if (!p || !out) return DBSLMM_E_ARG;

@@ -88,11 +88,13 @@ struct Args {
     const int32_t* status;       // the base copy's block status
     int32_t mode;                // backward: 0 Chebyshev epilogue; 1 plain solve of the factored
                                  // system (y = the matrix's z row, x -> X, beta of copy cix[0])
-    unsigned long long* stamps;  // diagnostics (env DBSLMM_TRSV_STAMPS): per tile of block stamp_b,
+    unsigned long long* stamps;  // diagnostic build (DBSLMM_DIAG, env DBSLMM_TRSV_STAMPS): per tile of block stamp_b,
     int32_t stamp_b;             // 100 MHz times [claim, last hand-off staged, stream done, publish]
 };
 __device__ __forceinline__ void stamp(const Args& a, int b, int I, int k) {
+#ifdef DBSLMM_DIAG
     if (a.stamps && b == a.stamp_b) a.stamps[8 * I + k] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // LDS control words of the ring

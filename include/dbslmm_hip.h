@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 4
+#define DBSLMM_ABI_VERSION 5
 
 enum {
     DBSLMM_OK = 0,
@@ -51,6 +51,27 @@ enum {
 typedef struct dbslmm_ctx dbslmm_ctx;
 typedef struct dbslmm_plan dbslmm_plan;
 
+/* Path selection of a plan (the product has ONE numerical path per block size class; these
+ * fields only move the size thresholds, e.g. so tests can drive every kernel class at small
+ * sizes).  Zero-initialise for the defaults; every field's 0 means "default".
+ *
+ * tiled_min      blocks with m >= tiled_min take the multi-workgroup tiled factorisation
+ *                (default 512, or 256 when no block reaches 512; minimum 64)
+ * gram_big_min   blocks with m >= this use the 128 x 128-tile Gram kernel (default 96)
+ * gram_huge_min  ... and the 256 x 256-tile one from here (default 384, 768 when n_ref < 4096)
+ * h2f_mode       plan_run_multi: 0 = tiled blocks factored once, the other sigmas solved by
+ *                Chebyshev iteration on that factor when the bound allows (tau in (0, 1],
+ *                <= 60 iterations); 1 = one factorisation per sigma (the merged sequence)
+ * cheb_tol       relative error target of the Chebyshev iteration (default 1e-13)
+ */
+typedef struct dbslmm_options {
+    int32_t tiled_min;
+    int32_t gram_big_min;
+    int32_t gram_huge_min;
+    int32_t h2f_mode;
+    double cheb_tol;
+} dbslmm_options;
+
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.
  *
  * bed       the whole PLINK .bed image INCLUDING its 3 magic bytes (host memory); row r of
@@ -64,6 +85,7 @@ typedef struct dbslmm_plan dbslmm_plan;
  *           rows, INFO::pos) with z-scores z_s[...] (INFO::z); order = the reference's
  *           info_s order.
  * l_ptr     same for large SNPs, or NULL for the LMM-only path.
+ * opts      path-selection thresholds (dbslmm_options), or NULL for the defaults.
  */
 typedef struct dbslmm_problem {
     const uint8_t* bed;
@@ -79,6 +101,7 @@ typedef struct dbslmm_problem {
     const int64_t* l_ptr;
     const int32_t* l_pos;
     const double* z_l;
+    const dbslmm_options* opts;
 } dbslmm_problem;
 
 /* Kernel timing slots reported by dbslmm_plan_kernel_ms. */
@@ -90,9 +113,9 @@ enum {
                                  threshold, one workgroup each */
     DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
                                  (concurrent with CHOL_LARGE when there are no tiled blocks) */
-    DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold (env
-                                 DBSLMM_TILED_MIN; default 512, or 256 when no block reaches
-                                 512), many workgroups per block,
+    DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold
+                                 (dbslmm_options.tiled_min; default 512, or 256 when no block
+                                 reaches 512), many workgroups per block,
                                  one launch per panel phase (third stream); the whole sequence */
     DBSLMM_K_TRSV = 5,        /* dbslmm_trsv_fwd/bwd: h2f tuning's Chebyshev iterations of the
                                  tiled blocks on the base copy's factor (run_multi; 0 otherwise) */

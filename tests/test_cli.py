@@ -124,15 +124,15 @@ def _eff_rows(text):
 def test_cli_h2f_tuning_matches_separate_runs(tmp_path, monkeypatch, cheb):
     """-h2f 0.8,1,1.2 (one Gram, three solves) writes the R driver's file names
     (<prefix>_h2f<hh>.dbslmm.txt, software/DBSLMM.R:204-219) with the same rows as three runs
-    with -h 0.5*hh: identical with the merged factorisations (DBSLMM_H2F_CHEB=0); with the
+    with -h 0.5*hh: identical with the merged factorisations (--h2f-merged); with the
     Chebyshev path (one factor, the other factors iterated) the same rows and values within
     1e-12 of the largest |beta| (the base factor's file stays identical)."""
-    monkeypatch.setenv("DBSLMM_H2F_CHEB", cheb)
     s, l = split_summary(tmp_path)
     base = ["-s", s, "-l", l, "-r", REF, "-b", BLOCKS_EUR1, "-n", "2400", "-nsnp", "996",
             "-mafMax", "0.2", "--precise-out"]
     prefix = str(tmp_path / "chr1")
-    r = run(base + ["-h", "0.5", "-h2f", "0.8,1,1.2", "-eff", prefix + ".dbslmm"])
+    merged = ["--h2f-merged"] if cheb == "0" else []
+    r = run(base + merged + ["-h", "0.5", "-h2f", "0.8,1,1.2", "-eff", prefix + ".dbslmm"])
     assert r.returncode == 0, r.stderr
     for hh in ("0.8", "1", "1.2"):
         tuned = open(f"{prefix}_h2f{hh}.dbslmm.txt").read()

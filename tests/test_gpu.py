@@ -207,10 +207,10 @@ def test_bench_config_vs_oracle(fit):
 def test_run_multi_sigma_matches_separate_solves(fit, monkeypatch):
     """h2f tuning: one Gram, three solves == three fresh plans (bit-identical), any block path
     (the merged-factorisation path; tests/test_h2f_cheb.py covers the Chebyshev one)."""
-    monkeypatch.setenv("DBSLMM_H2F_CHEB", "0")
     from dbslmm_amd import Plan, synth
     p = synth.simulate(20000, 600, seed=3, chroms=[1, 2, 3], miss_rate=0.001)
     prob = synth.make_problem(p)
+    prob.opts["h2f_mode"] = 1
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     plan = Plan(fit.ctx, prob)
     multi = plan.run_multi(sig)

@@ -2,7 +2,7 @@
 copy (median sigma) is factored; the other copies iterate M_b x = z - delta P_s x with the
 persistent forward / backward substitution kernels.  Every copy must match a fresh single-sigma
 solve to fp64 accuracy (normwise 1e-12), the base copy bit for bit; statuses and the NaN of a
-monomorphic block carry over; the merged-factorisation path (DBSLMM_H2F_CHEB=0) stays
+monomorphic block carry over; the merged-factorisation path (h2f_mode = 1) stays
 bit-identical."""
 import numpy as np
 import pytest
@@ -37,8 +37,8 @@ def _finite_normwise(a, b):
 @pytest.mark.parametrize("factors", [(0.8, 1.0, 1.2), (1.2, 0.8), (0.5, 0.7, 1.0, 1.3, 1.6, 2.0)])
 def test_cheb_copies_match_fresh_solves(monkeypatch, tiled_min, factors):
     from dbslmm_amd import Context, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", tiled_min)
     prob = _problem(seed=5, mono_block=3)
+    prob.opts["tiled_min"] = int(tiled_min)
     s0 = prob.sigma_s
     sig = [s0 * f for f in factors]
     plan = Plan(Context(0), prob)
@@ -61,9 +61,8 @@ def test_cheb_copies_match_fresh_solves(monkeypatch, tiled_min, factors):
 
 def test_cheb_off_is_bit_identical(monkeypatch):
     from dbslmm_amd import Context, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", "64")
-    monkeypatch.setenv("DBSLMM_H2F_CHEB", "0")
     prob = _problem(seed=6)
+    prob.opts.update(tiled_min=64, h2f_mode=1)
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     multi = Plan(Context(0), prob).run_multi(sig)
     for got, ref in zip(multi, _fresh(prob, sig)):
@@ -74,8 +73,8 @@ def test_cheb_repeatable_and_followed_by_plain_run(monkeypatch):
     """Two h2f runs give identical betas (fixed iteration count, fixed reduction order), and a
     plain run afterwards equals a fresh single-sigma plan."""
     from dbslmm_amd import Context, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", "64")
     prob = _problem(seed=8)
+    prob.opts["tiled_min"] = 64
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     plan = Plan(Context(0), prob)
     a = plan.run_multi(sig)
@@ -87,23 +86,3 @@ def test_cheb_repeatable_and_followed_by_plain_run(monkeypatch):
     got = plan.download()
     ref = _fresh(prob, sig[:1])[0]
     np.testing.assert_array_equal(_cat(got), _cat(ref))
-
-
-@pytest.mark.parametrize("split", ["1", "2"])
-def test_cheb_split_groups_match_joint(monkeypatch, split):
-    """The opt-in block-group split of the substitutions (DBSLMM_CHEB_SPLIT 1: the early group
-    overlapping the factorisation, 2: both groups after it on two streams) gives the joint
-    launches' betas bit for bit: the same per-block arithmetic in the same order."""
-    from dbslmm_amd import Context, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", "64")
-    prob = _problem(seed=9, mono_block=3)
-    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
-    joint = Plan(Context(0), prob).run_multi(sig)
-    monkeypatch.setenv("DBSLMM_CHEB_SPLIT", split)
-    monkeypatch.setenv("DBSLMM_SPLIT_FRAC", "0.3")
-    plan = Plan(Context(0), prob)
-    for _ in range(2):                       # twice: the second ticket counter resets itself
-        got = plan.run_multi(sig)
-        for x, y in zip(got, joint):
-            np.testing.assert_array_equal(_cat(x), _cat(y))
-            np.testing.assert_array_equal(x[2], y[2])

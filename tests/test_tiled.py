@@ -1,5 +1,5 @@
 """GPU parity of the multi-workgroup ("tiled") Cholesky path against the oracle's direct solve
-and against the single-workgroup path (the path is chosen per block by m >= DBSLMM_TILED_MIN).
+and against the single-workgroup path (the path is chosen per block by m >= dbslmm_options.tiled_min).
 
 Block sizes put the z row (row m of the bordered matrix) at every position that matters inside
 its 64-row tile: m % 64 in {0, 1, 31, 32, 33, 63}, alone in its own tile (m % 64 == 0), plus
@@ -51,9 +51,9 @@ def _problem(seed=11, n_ref=256, with_large=True, mono_block=None):
                         s_pos=s_pos, z_s=z_s, **kw)
 
 
-def _solve(prob, tiled_min, monkeypatch):
+def _solve(prob, tiled_min, monkeypatch=None):
     from dbslmm_amd import DBSLMMFIT
-    monkeypatch.setenv("DBSLMM_TILED_MIN", str(tiled_min))
+    prob.opts["tiled_min"] = int(tiled_min)
     bs, bl, st = DBSLMMFIT(0).est(prob)
     return np.concatenate([bs, bl]), st
 
@@ -102,8 +102,8 @@ def test_tiled_monomorphic_block_is_nan(monkeypatch):
 
 def test_tiled_plan_rerun_bit_identical(monkeypatch):
     from dbslmm_amd import Context, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", "128")
     prob = _problem(seed=3)
+    prob.opts["tiled_min"] = 128
     plan = Plan(Context(0), prob)
     wl = plan.workload()
     assert wl["blocks_tiled"] == len(SIZES) and wl["tiled_launches"] > 0
@@ -119,7 +119,7 @@ def test_tiled_plan_rerun_bit_identical(monkeypatch):
 @pytest.mark.parametrize("miss", [0.0, 0.01])
 @pytest.mark.parametrize("n_ref", [200, 333])
 def test_gram_kernels_bit_identical(monkeypatch, miss, n_ref):
-    """The 256x256 (m >= DBSLMM_GRAM_HUGE_MIN), 128x128 (m >= DBSLMM_GRAM_BIG_MIN) and per-wave
+    """The 256x256 (m >= gram_huge_min), 128x128 (m >= gram_big_min) and per-wave
     32x32 Gram kernels compute the same exact integers and the same fp64 epilogue: beta must
     agree bit for bit whichever kernel handles every block."""
     from dbslmm_amd import DBSLMMFIT, synth
@@ -127,8 +127,7 @@ def test_gram_kernels_bit_identical(monkeypatch, miss, n_ref):
     prob = synth.make_problem(p)
     out = []
     for big, huge in ((1, 1), (1, 10 ** 9), (10 ** 9, 10 ** 9)):
-        monkeypatch.setenv("DBSLMM_GRAM_BIG_MIN", str(big))
-        monkeypatch.setenv("DBSLMM_GRAM_HUGE_MIN", str(huge))
+        prob.opts.update(gram_big_min=big, gram_huge_min=min(huge, 2 ** 31 - 1))
         out.append(DBSLMMFIT(0).est(prob))
     for other in out[1:]:
         for x, y in zip(out[0], other):
@@ -144,9 +143,8 @@ def test_run_multi_merged_copies_bit_identical(monkeypatch, tiled_min):
     block NaN in every copy; a plain run afterwards (copy 0 again) and the variance-holding copy
     (the last sigma) stay consistent."""
     from dbslmm_amd import Context, DBSLMMFIT, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", tiled_min)
-    monkeypatch.setenv("DBSLMM_H2F_CHEB", "0")   # the merged path (tests/test_h2f_cheb.py: the other)
     prob = _problem(seed=5, mono_block=3)
+    prob.opts.update(tiled_min=int(tiled_min), h2f_mode=1)   # the merged path (test_h2f_cheb.py: the other)
     plan = Plan(Context(0), prob)
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     multi = plan.run_multi(sig)
@@ -164,18 +162,3 @@ def test_run_multi_merged_copies_bit_identical(monkeypatch, tiled_min):
     plan.set_sigma(sig[0])
     plan.run()
     np.testing.assert_array_equal(plan.download()[0], multi[0][0])
-
-
-@pytest.mark.parametrize("R", ["1", "3", "4"])
-def test_super_step_sizes_match_oracle(monkeypatch, R):
-    """Super steps of R regions (K = 128 R trailing updates, pending updates of up to R-1 panels
-    inside the region and panel kernels) give the same beta as the oracle and as R = 2."""
-    monkeypatch.setenv("DBSLMM_SUPER", R)
-    prob = _problem(seed=9)
-    ref, _ = _oracle(prob)
-    got, st = _solve(prob, 64, monkeypatch)
-    monkeypatch.setenv("DBSLMM_SUPER", "2")
-    two, _ = _solve(prob, 64, monkeypatch)
-    assert np.all(st == 0)
-    assert normwise(got, ref) < 1e-10
-    assert normwise(got, two) < 1e-11

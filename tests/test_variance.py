@@ -242,8 +242,8 @@ def test_gpu_variance_synthetic_all_paths(monkeypatch, tiled_min):
     """Blocks on the one-wave (m < 64), one-workgroup and tiled factor paths, an empty block,
     n_test > 64 (two workgroups of test individuals), permuted test rows, missing calls."""
     from dbslmm_amd import Context, Plan
-    monkeypatch.setenv("DBSLMM_TILED_MIN", tiled_min)
     prob, tbed, ind, tsp, tlp = synth_variance_case()
+    prob.opts["tiled_min"] = int(tiled_min)
     ref = synth_oracle(prob, tbed, ind, tsp, tlp)
     plan = Plan(Context(0), prob)
     plan.run()

@@ -1,6 +1,7 @@
 """Diagnostics: per-tile timeline of the forward substitution for the largest tiled block
 (DBSLMM_TRSV_STAMPS=1, config-4 h2f run): claim -> last hand-off staged -> stream done -> publish.
-    DBSLMM_TRSV_STAMPS=1 python tools/trsv_stamps.py"""
+Needs the diagnostic build (make -C dbslmm_amd/csrc diag -> libdbslmm_hip_diag.so).
+    python tools/trsv_stamps.py"""
 import ctypes
 import os
 import sys
@@ -9,6 +10,8 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["DBSLMM_TRSV_STAMPS"] = "1"
+os.environ["DBSLMM_LIB_PATH"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                             "dbslmm_amd", "libdbslmm_hip_diag.so")
 from dbslmm_amd import Context, Plan, synth  # noqa: E402
 
 panel = synth.simulate(1000000, 10000, pop="EUR", seed=1, engine="gpu", device=0)
