@@ -11,9 +11,12 @@ Gram + three factorisations and solves per step).  --config 2 is the small confi
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-Multi-GPU: LD blocks are independent, so each rank solves its own shard (its own synthetic
-panel of the same shape, seed = rank) with no data-path collective -> weak scaling; the job
-value is the SNPs of all ranks / the max-over-ranks time.  Rank 0 prints ONE JSON line.
+Multi-GPU (strong scaling, the default): ONE problem -- the same workload as N=1 -- with its LD
+blocks sharded over the ranks (longest processing time first on n_ref m(m+1) + m^3/3, each rank
+holding only its blocks' .bed rows, dbslmm_amd/dist.py); every step each rank solves its shard and
+the betas are gathered to rank 0 with one RCCL `gather` (the path's only exchange).  value = the
+problem's SNPs / the max-over-ranks time.  --replicas: N independent copies of the workload
+(seed = 1 + rank, no exchange) -> weak scaling.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -59,6 +62,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host threads (OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process group backend (nccl = RCCL over xGMI; gloo only for rehearsals)")
+    ap.add_argument("--rank-device", type=int, default=None,
+                    help="rehearsal on a 1-GPU box: every rank on this device instead of LOCAL_RANK")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N>1: independent replicas of the workload per rank (weak scaling) instead "
+                         "of one problem sharded over the ranks (strong scaling)")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
@@ -287,31 +297,52 @@ def main():
     import numpy as np
     import torch
     dist = None
+    if args.rank_device is not None:
+        local = args.rank_device
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
+    cdev = "cuda" if args.dist_backend == "nccl" else "cpu"    # collective tensors
 
     from dbslmm_amd import Context, KERNEL_NAMES, Plan, synth
+    from dbslmm_amd.dist import ShardGather, shard_blocks, sub_problem
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    panel = synth.simulate(args.snps, args.n_ref, pop=args.pop, seed=1 + rank, engine=args.gen,
-                           device=local if world > 1 else 0)
-    prob = synth.make_problem(panel, lmm_only=args.lmm_only)
+    sharded = world > 1 and not args.replicas
+    panel = synth.simulate(args.snps, args.n_ref, pop=args.pop, seed=1 if sharded else 1 + rank,
+                           engine=args.gen, device=local if world > 1 else 0)
+    full = synth.make_problem(panel, lmm_only=args.lmm_only)
+    del panel
+    sigmas = [full.sigma_s * f for f in args.h2f] if args.h2f else None
+    gather = None
+    if sharded:
+        m_b = np.diff(full.s_ptr) + (np.diff(full.l_ptr) if full.l_ptr is not None else 0)
+        shards = shard_blocks(m_b, full.n_ref, world)
+        prob, s_idx, l_idx = sub_problem(full, shards[rank], compact=True)
+    else:
+        prob = full
     ctx = Context(local if world > 1 else 0)
     plan = Plan(ctx, prob)
     wl = plan.workload()
-
-    sigmas = [prob.sigma_s * f for f in args.h2f] if args.h2f else None
+    if sharded:
+        gather = ShardGather(full.n_s, full.n_l, s_idx, l_idx, k=len(sigmas) if sigmas else 1,
+                             device=cdev)
 
     def step():
         if sigmas:
-            plan.run_multi(sigmas)      # one Gram, len(sigmas) solves (synchronous)
+            res = plan.run_multi(sigmas)      # one Gram, len(sigmas) solves (synchronous)
+            if gather:
+                gather([(r[0], r[1]) for r in res])
+        elif gather:
+            plan.run()
+            bs, bl, _ = plan.download()
+            gather([(bs, bl)])
         else:
             plan.run()
 
@@ -338,9 +369,12 @@ def main():
     else:
         res = [plan.download()]
     status = res[0][2]
+    st = torch.tensor([int(np.sum((status != 0) & (status != 1)))], dtype=torch.int64, device=cdev)
+    if dist is not None:
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    snps = torch.tensor([wl["snps"]], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    snps = torch.tensor([wl["snps"]], dtype=torch.float64, device=cdev)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(snps, op=dist.ReduceOp.SUM)
@@ -365,24 +399,28 @@ def main():
             "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (AR(1)-LD PLINK panel, seed = 1 + rank)",
+            "scaling": "weak" if args.replicas else "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (AR(1)-LD PLINK panel, seed = %s)" % ("1 + rank" if args.replicas else "1"),
             "config": {"workload": f"synthetic {args.snps} SNP x {args.n_ref} indiv, 22 chr "
                                    f"{args.pop} LD blocks, {'LMM-only' if args.lmm_only else 'DBSLMM large+small'}, "
                                    f"h2=0.5 (BASELINE configs[{args.config - 1}])", "generator": args.gen,
                        "h2f": args.h2f,
-                       "snps_per_gpu": wl["snps"], "n_ref": args.n_ref, "blocks": wl["blocks"],
+                       "snps_rank0": wl["snps"], "snps_total": total_snps, "n_ref": args.n_ref,
+                       "blocks_rank0": wl["blocks"],
                        "gram": "exact int8 dosages on v_mfma_i32_32x32x32_i8, fp64 epilogue",
                        "solve": "fp64 Cholesky of the joint per-block matrix" + (
                            "; h2f: tiled blocks factored once (base h2f), the other h2f solves by "
                            "%d Chebyshev iterations on that factor" % wl["cheb_iters"]
                            if wl["cheb_iters"] > 0 else ""),
-                       "parallelism": f"ld-block shards x{world}"},
+                       "parallelism": (f"{world} independent replicas (no exchange)" if args.replicas else
+                                       f"LD blocks of one problem sharded over {world} GPU(s) (LPT), "
+                                       f"betas gathered to rank 0 by one RCCL gather per step"
+                                       if world > 1 else "1 GPU")},
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": cpu,
             "max_dbeta_vs_cpu_ref": dbeta,
-            "status_nonzero_blocks": int(np.sum((status != 0) & (status != 1))),
+            "status_nonzero_blocks": int(st.item()),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

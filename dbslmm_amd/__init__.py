@@ -32,16 +32,25 @@ def _ptr(a):
 
 
 class Context:
-    """One HIP device (dbslmm_ctx_create)."""
+    """One HIP device (dbslmm_ctx_create), or several (a list of ordinals, repeats allowed:
+    dbslmm_ctx_create_multi -- every plan's LD blocks are sharded over the devices)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device=0):
         self.lib = _lib.load()
         h = C.c_void_p()
-        rc = self.lib.dbslmm_ctx_create(int(device), C.byref(h))
+        if isinstance(device, (list, tuple)):
+            ids = np.ascontiguousarray(device, dtype=np.int32)
+            rc = self.lib.dbslmm_ctx_create_multi(len(ids), _ptr(ids), C.byref(h))
+        else:
+            rc = self.lib.dbslmm_ctx_create(int(device), C.byref(h))
         if rc != 0:
             raise DbslmmError(f"dbslmm_ctx_create(device={device}) failed rc={rc}")
         self.h = h
         self.device = device
+
+    @property
+    def num_devices(self) -> int:
+        return int(self.lib.dbslmm_ctx_num_devices(self.h))
 
     def check(self, rc: int, what: str):
         if rc != 0:
@@ -163,6 +172,12 @@ class Plan:
                 "cheb_iters", "cheb_base")
         return dict(zip(keys, w.tolist()))
 
+    def shard_info(self) -> np.ndarray:
+        """Device index (in the context's device order) solving each block; -1 = empty block."""
+        out = np.zeros(self.prob.num_block, dtype=np.int32)
+        self.ctx.check(self.ctx.lib.dbslmm_plan_shard_info(self.h, _ptr(out)), "plan_shard_info")
+        return out
+
     def download(self):
         p = self.prob
         bs = np.zeros(p.n_s)
@@ -203,9 +218,10 @@ class Plan:
 
 
 class DBSLMMFIT:
-    """Mirror of the reference's DBSLMMFIT::est (scr/dbslmmfit.hpp:35-66) on one GPU."""
+    """Mirror of the reference's DBSLMMFIT::est (scr/dbslmmfit.hpp:35-66) on one GPU, or on
+    several (device = a list of ordinals: the LD blocks sharded over them)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device=0):
         self.ctx = Context(device)
 
     def est(self, prob: BlockProblem):

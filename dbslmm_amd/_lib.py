@@ -18,6 +18,7 @@ EXPORTS = (
     "dbslmm_plan_download", "dbslmm_plan_set_sigma", "dbslmm_plan_destroy", "dbslmm_plan_run_multi",
     "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
     "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
+    "dbslmm_ctx_create_multi", "dbslmm_ctx_num_devices", "dbslmm_plan_shard_info",
 )
 
 ABI_VERSION = 5
@@ -73,6 +74,9 @@ def load(path: str | None = None):
     V, P = C.c_void_p, C.POINTER
     L.dbslmm_abi_version.restype = C.c_int
     L.dbslmm_ctx_create.argtypes = [C.c_int, P(V)]
+    L.dbslmm_ctx_create_multi.argtypes = [C.c_int32, V, P(V)]
+    L.dbslmm_ctx_num_devices.argtypes = [V]
+    L.dbslmm_plan_shard_info.argtypes = [V, V]
     L.dbslmm_ctx_destroy.argtypes = [V]
     L.dbslmm_ctx_destroy.restype = None
     L.dbslmm_last_error.argtypes = [V]

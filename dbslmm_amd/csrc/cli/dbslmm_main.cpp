@@ -6,7 +6,9 @@
 // (reference: scr/dtpr.cpp:47-220, 383-481); the hot path -- the MAF pass of readBim and
 // DBSLMMFIT::est -- goes through the C-ABI (include/dbslmm_hip.h) to the GPU.
 //
-// Extensions (not in the reference): --gpu N (HIP device), --tau T (default 0.8 as hard-coded at
+// Extensions (not in the reference): --gpu N (HIP device), --gpus N (devices 0..N-1: the LD
+// blocks sharded over N GPUs, dbslmm_ctx_create_multi), --gpu-ids a,b,.. (explicit device list,
+// repeats allowed), --tau T (default 0.8 as hard-coded at
 // scr/dbslmmfit.cpp:697,751), --precise-out (17 significant digits), --dry-run (stop after
 // matching; prints counts, no GPU).  With -dat_str and -test_indicator_file the test-set variance
 // matrix is written to ./variance.txt (arma_ascii, scr/dbslmmfit.cpp:242), evaluated on the GPU
@@ -46,6 +48,7 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     double mafMax = 1.0, h = -1.0;
     // extensions
     int gpu = 0;
+    string gpu_ids;                 // --gpus N -> "0,1,..,N-1"; --gpu-ids a,b,..
     double tau = 0.8;
     bool precise = false, dry_run = false, h2f_merged = false;
     string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
@@ -82,6 +85,8 @@ void print_help() {
               << " -t        [filename]   specify input thread.\n"
               << " -eff      [filename]   specify output the estimate effect SNPs.\n"
               << " --gpu     [num]        HIP device (extension)\n"
+              << " --gpus    [num]        shard the LD blocks over devices 0..num-1 (extension)\n"
+              << " --gpu-ids [list]       shard over the listed devices, e.g. 0,1,2 (extension)\n"
               << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
               << " --precise-out          17 significant digits in <eff>.txt (extension)\n"
               << " -h2f      [list]       h2 factors, e.g. 0.8,1,1.2: one Gram, one solve per factor,\n"
@@ -113,6 +118,13 @@ void assign(int argc, char** argv, Param& p) {
         else if (is("--test_indicator_file", "-test_indicator_file")) { if ((v = take(i))) p.test_indicator_file = v; }
         else if (is("--dat_str", "-dat_str")) { if ((v = take(i))) p.dat_str = v; }
         else if (!strcmp(a, "--gpu")) { if ((v = take(i))) p.gpu = atoi(v); }
+        else if (!strcmp(a, "--gpus")) {
+            if ((v = take(i))) {
+                p.gpu_ids.clear();
+                for (int g = 0; g < std::max(1, atoi(v)); ++g) p.gpu_ids += (g ? "," : "") + std::to_string(g);
+            }
+        }
+        else if (!strcmp(a, "--gpu-ids")) { if ((v = take(i))) p.gpu_ids = v; }
         else if (!strcmp(a, "--tau")) { if ((v = take(i))) p.tau = atof(v); }
         else if (!strcmp(a, "--precise-out")) p.precise = true;
         else if (is("--h2f", "-h2f")) { if ((v = take(i))) p.h2f = v; }
@@ -346,7 +358,15 @@ int main(int argc, char** argv) {
     Mapped bed;
     if (!p.dry_run) {
         if (!bed.open(p.r + ".bed")) return fail(p.r + ".bed cannot be opened");
-        if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) return fail("no usable HIP device (dbslmm_ctx_create)");
+        if (p.gpu_ids.empty()) {
+            if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) return fail("no usable HIP device (dbslmm_ctx_create)");
+        } else {
+            vector<int32_t> ids;
+            for (const string& t : split(p.gpu_ids, ',')) ids.push_back(atoi(t.c_str()));
+            if (ids.empty() || dbslmm_ctx_create_multi(static_cast<int32_t>(ids.size()), ids.data(), &ctx) != DBSLMM_OK)
+                return fail("no usable HIP devices (dbslmm_ctx_create_multi, --gpus / --gpu-ids)");
+            std::cout << "Sharding the LD blocks over " << ids.size() << " GPUs.\n";
+        }
     } else if (constr) {
         return fail("--dry-run needs -mafMax 1 (the MAF pass runs on the GPU)");
     }

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dbslmm_hip.h"
@@ -75,10 +76,23 @@ struct dbslmm_ctx {
     hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
     int n_cu = 256;                  // compute units (persistent substitution grid)
     std::string err;
+    std::vector<dbslmm_ctx*> subs;   // multi-device context (multi.hip): one context per device,
+                                     // device = -1 and no streams of its own
+};
+struct dbslmm_plan;
+// the shards of a multi-device plan (multi.hip)
+struct DeviceShard {
+    dbslmm_plan* plan = nullptr;
+    std::vector<int32_t> blocks;        // original block ids, in sub-problem order
+    std::vector<int64_t> s_idx, l_idx;  // sub small / large SNP -> original beta position
+};
+struct dbslmm_mplan {
+    std::vector<DeviceShard> shards;
 };
 
 struct dbslmm_plan {
     dbslmm_ctx* ctx = nullptr;
+    dbslmm_mplan* mp = nullptr;        // multi-device plan: every call fans out over its shards
     int32_t n_ref = 0, n_obs = 0, num_block = 0;
     double sigma_s = 0.0, tau = 0.8;
     int64_t n_s = 0, n_l = 0, bytes_per_snp = 0, kpad = 0, bed_len = 0;
@@ -166,6 +180,25 @@ struct dbslmm_plan {
             (ctx)->err = msg;                       \
             return DBSLMM_E_ARG;                    \
         }                                           \
+    } while (0)
+
+// multi-device plans (multi.hip)
+static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out);
+static void mp_destroy(dbslmm_plan* p);
+static int mp_download(dbslmm_plan* p, int copy, double* beta_s, double* beta_l, int32_t* block_status);
+static int mp_run(dbslmm_plan* p, const double* sigmas, int n, bool wait);
+static int mp_sync(dbslmm_plan* p);
+static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diags, int32_t* n_test_out);
+static int mp_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int32_t n_ref, int64_t n_snp, double* maf);
+// context-level tools on a multi-device context run on its first device
+#define ON_FIRST_DEVICE(ctx, call)                                       \
+    do {                                                                 \
+        if (!(ctx)->subs.empty()) {                                      \
+            dbslmm_ctx* ctx0_ = (ctx)->subs[0];                          \
+            const int rc_ = call;                                        \
+            if (rc_ != DBSLMM_OK) (ctx)->err = ctx0_->err;               \
+            return rc_;                                                  \
+        }                                                                \
     } while (0)
 
 template <typename T>
@@ -392,6 +425,11 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
 
 void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     if (!ctx) return;
+    for (dbslmm_ctx* s : ctx->subs) dbslmm_ctx_destroy(s);
+    if (ctx->device < 0) {
+        delete ctx;
+        return;
+    }
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
@@ -406,6 +444,11 @@ const char* dbslmm_last_error(const dbslmm_ctx* ctx) { return ctx ? ctx->err.c_s
 
 void dbslmm_plan_destroy(dbslmm_plan* p) {
     if (!p) return;
+    if (p->mp) {
+        mp_destroy(p);
+        delete p;
+        return;
+    }
     (void)hipSetDevice(p->ctx->device);
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
@@ -426,6 +469,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
 
 int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out) {
     if (!ctx) return DBSLMM_E_ARG;
+    if (!ctx->subs.empty()) return mp_create(ctx, pr, out);
     ARG_CHECK(ctx, pr && out, "null problem/out");
     *out = nullptr;
     ARG_CHECK(ctx, pr->bed && pr->n_ref > 1 && pr->n_obs > 0 && pr->num_block >= 0, "bad sizes");
@@ -722,6 +766,8 @@ int dbslmm_plan_set_sigma(dbslmm_plan* p, double sigma_s) {
     if (!p) return DBSLMM_E_ARG;
     ARG_CHECK(p->ctx, sigma_s > 0.0 && std::isfinite(sigma_s), "sigma_s must be > 0");
     p->sigma_s = sigma_s;
+    if (p->mp)
+        for (auto& sh : p->mp->shards) sh.plan->sigma_s = sigma_s;
     return DBSLMM_OK;
 }
 
@@ -730,6 +776,8 @@ int dbslmm_plan_enable_timing(dbslmm_plan* p, int enable) {
     p->timing = enable != 0;
     for (double& v : p->ms_acc) v = 0.0;
     p->ms_runs = 0;
+    if (p->mp)
+        for (auto& sh : p->mp->shards) dbslmm_plan_enable_timing(sh.plan, enable);
     return DBSLMM_OK;
 }
 
@@ -1293,6 +1341,7 @@ static int download_copy(dbslmm_plan* p, int c, double* beta_s, double* beta_l, 
 
 int dbslmm_plan_run(dbslmm_plan* p) {
     if (!p) return DBSLMM_E_ARG;
+    if (p->mp) return mp_run(p, &p->sigma_s, 1, false);
     return run_impl(p, true, &p->sigma_s, 1);
 }
 
@@ -1305,6 +1354,17 @@ int dbslmm_plan_run_multi(dbslmm_plan* p, const double* sigmas, int32_t n_sigma,
     ARG_CHECK(ctx, sigmas && n_sigma > 0 && n_sigma <= 64, "sigmas / n_sigma (1..64)");
     for (int i = 0; i < n_sigma; ++i)
         ARG_CHECK(ctx, sigmas[i] > 0.0 && std::isfinite(sigmas[i]), "sigma_s must be > 0");
+    if (p->mp) {
+        for (auto& sh : p->mp->shards)
+            ARG_CHECK(ctx, static_cast<int64_t>(sh.plan->n_nonempty) * n_sigma < 32768,
+                      "blocks x sigmas per device must stay below 32768 (packed work items)");
+        int rc = mp_run(p, sigmas, n_sigma, true);
+        for (int i = 0; i < n_sigma && !rc; ++i)
+            rc = mp_download(p, i, beta_s ? beta_s + static_cast<int64_t>(i) * p->n_s : nullptr,
+                             beta_l ? beta_l + static_cast<int64_t>(i) * p->n_l : nullptr,
+                             block_status ? block_status + static_cast<int64_t>(i) * p->num_block : nullptr);
+        return rc;
+    }
     ARG_CHECK(ctx, static_cast<int64_t>(p->n_nonempty) * n_sigma < 32768,
               "blocks x sigmas must stay below 32768 (packed work items)");
     int rc = run_impl(p, true, sigmas, n_sigma);
@@ -1318,6 +1378,7 @@ int dbslmm_plan_run_multi(dbslmm_plan* p, const double* sigmas, int32_t n_sigma,
 
 int dbslmm_plan_sync(dbslmm_plan* p) {
     if (!p) return DBSLMM_E_ARG;
+    if (p->mp) return mp_sync(p);
     HIP_TRY(p->ctx, hipSetDevice(p->ctx->device));
     HIP_TRY(p->ctx, hipStreamSynchronize(p->ctx->stream));
     if (const int rc = check_trsv(p)) return rc;
@@ -1328,6 +1389,19 @@ int dbslmm_plan_sync(dbslmm_plan* p) {
 
 int dbslmm_plan_kernel_ms(dbslmm_plan* p, double* ms_out, int32_t* launches_out) {
     if (!p || !ms_out) return DBSLMM_E_ARG;
+    if (p->mp) {   // per kernel class the slowest device (the critical path of the node)
+        int32_t runs = INT32_MAX;
+        for (int k = 0; k < DBSLMM_K_COUNT; ++k) ms_out[k] = 0.0;
+        for (auto& sh : p->mp->shards) {
+            double ms[DBSLMM_K_COUNT];
+            int32_t n = 0;
+            dbslmm_plan_kernel_ms(sh.plan, ms, &n);
+            for (int k = 0; k < DBSLMM_K_COUNT; ++k) ms_out[k] = std::max(ms_out[k], ms[k]);
+            runs = std::min(runs, n);
+        }
+        if (launches_out) *launches_out = runs == INT32_MAX ? 0 : runs;
+        return DBSLMM_OK;
+    }
     for (int k = 0; k < DBSLMM_K_COUNT; ++k) ms_out[k] = p->ms_runs ? p->ms_acc[k] / p->ms_runs : 0.0;
     if (launches_out) *launches_out = p->ms_runs;
     return DBSLMM_OK;
@@ -1345,12 +1419,29 @@ extern "C" int dbslmm_diag_trsv_stamps(dbslmm_plan* p, unsigned long long* out, 
 
 int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     if (!p || !out) return DBSLMM_E_ARG;
+    if (p->mp) {   // sums over the devices; [12] launches, [14] iterations: the max; [15] device 0's
+        for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = 0.0;
+        for (auto& sh : p->mp->shards) {
+            double w[DBSLMM_WORKLOAD_LEN];
+            dbslmm_plan_workload(sh.plan, w);
+            for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i)
+                out[i] = (i == 12 || i == 14) ? std::max(out[i], w[i]) : out[i] + w[i];
+        }
+        double w0[DBSLMM_WORKLOAD_LEN];
+        dbslmm_plan_workload(p->mp->shards[0].plan, w0);
+        out[15] = w0[15];
+        return DBSLMM_OK;
+    }
     for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = p->wl[i];
     return DBSLMM_OK;
 }
 
 int dbslmm_plan_download(dbslmm_plan* p, double* beta_s, double* beta_l, int32_t* block_status) {
     if (!p) return DBSLMM_E_ARG;
+    if (p->mp) {
+        if (!p->ran) { p->ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
+        return mp_download(p, p->var_copy, beta_s, beta_l, block_status);
+    }
     return download_copy(p, p->var_copy, beta_s, beta_l, block_status);
 }
 
@@ -1375,6 +1466,7 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     if (!p) return DBSLMM_E_ARG;
     dbslmm_ctx* ctx = p->ctx;
     if (!p->ran) { ctx->err = "plan_variance before plan_run"; return DBSLMM_E_STATE; }
+    if (p->mp) return mp_variance(p, tp, diags, n_test_out);
     ARG_CHECK(ctx, tp && tp->bed && tp->indicator && tp->n_total > 0, "bad test panel");
     if (p->cheb_pending_var) {
         // the last h2f run iterated the last sigma's tiled blocks on another copy's factor and
@@ -1467,6 +1559,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
     const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
     ARG_CHECK(ctx, bed_len >= 3 + n_snp * bps, "bed image shorter than n_snp rows");
     if (n_snp == 0) return DBSLMM_OK;
+    if (!ctx->subs.empty()) return mp_bed_maf(ctx, bed, n_ref, n_snp, maf);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     uint8_t* d_bed = nullptr;
     int32_t* d_pos = nullptr;
@@ -1505,6 +1598,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
 int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t n_ref,
                         const int32_t* pos, int32_t n_rows, double* out, double* maf) {
     if (!ctx) return DBSLMM_E_ARG;
+    ON_FIRST_DEVICE(ctx, dbslmm_read_snp_std(ctx0_, bed, bed_len, n_ref, pos, n_rows, out, maf));
     ARG_CHECK(ctx, bed && pos && out && n_ref > 1 && n_rows >= 0, "bad arguments");
     const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
     for (int32_t j = 0; j < n_rows; ++j)
@@ -1559,6 +1653,7 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
                         int32_t num_block, const int64_t* ptr, const int32_t* pos,
                         const double* z1, const double* z2, double* nume, double* deno) {
     if (!ctx) return DBSLMM_E_ARG;
+    ON_FIRST_DEVICE(ctx, dbslmm_valid_blocks(ctx0_, bed, bed_len, n_ref, num_block, ptr, pos, z1, z2, nume, deno));
     ARG_CHECK(ctx, bed && ptr && nume && deno && n_ref > 1 && num_block >= 0, "bad arguments");
     const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
     const int64_t n_rows = ptr[num_block];
@@ -1633,3 +1728,5 @@ int dbslmm_debug_stamps(double* out8) {
 #endif
 
 }  // extern "C"
+
+#include "multi.hip"

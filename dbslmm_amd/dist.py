@@ -37,9 +37,11 @@ def shard_blocks(m_per_block: np.ndarray, n_ref: int, world: int) -> list[np.nda
     return [np.array(sorted(o), dtype=np.int64) for o in owned]
 
 
-def sub_problem(prob, blocks: np.ndarray):
+def sub_problem(prob, blocks: np.ndarray, compact: bool = False):
     """The BlockProblem restricted to `blocks` (kept in block order), plus the positions of its
-    small / large SNPs in the full problem's beta_s / beta_l."""
+    small / large SNPs in the full problem's beta_s / beta_l.  compact: the sub-problem gets its
+    own .bed image holding only its rows (what one GPU of a sharded solve receives; the C-ABI's
+    multi-device plans do the same, multi.hip)."""
     from . import BlockProblem
     s_idx = [np.arange(prob.s_ptr[b], prob.s_ptr[b + 1]) for b in blocks]
     s_idx = np.concatenate(s_idx) if s_idx else np.zeros(0, dtype=np.int64)
@@ -51,9 +53,19 @@ def sub_problem(prob, blocks: np.ndarray):
         l_idx = np.concatenate(li) if li else np.zeros(0, dtype=np.int64)
         l_ptr = np.concatenate([[0], np.cumsum(np.diff(prob.l_ptr)[blocks])]).astype(np.int64)
         kw = dict(l_ptr=l_ptr, l_pos=prob.l_pos[l_idx], z_l=prob.z_l[l_idx])
-    sub = BlockProblem(bed=prob.bed, n_ref=prob.n_ref, n_obs=prob.n_obs, sigma_s=prob.sigma_s,
-                       s_ptr=s_ptr, s_pos=prob.s_pos[s_idx], z_s=prob.z_s[s_idx], tau=prob.tau,
-                       **kw)
+    bed, s_pos = prob.bed, prob.s_pos[s_idx]
+    if compact:
+        bps = (prob.n_ref + 3) // 4
+        rows = np.concatenate([s_pos, kw.get("l_pos", np.zeros(0, dtype=np.int32))])
+        uniq, inv = np.unique(rows, return_inverse=True)
+        body = prob.bed[3:3 + (int(uniq.max()) + 1 if uniq.size else 0) * bps].reshape(-1, bps)
+        bed = np.concatenate([prob.bed[:3], body[uniq].reshape(-1)]) if uniq.size else prob.bed[:3 + bps]
+        s_pos = inv[:s_pos.size].astype(np.int32)
+        if "l_pos" in kw:
+            kw["l_pos"] = inv[s_pos.size:].astype(np.int32)
+    sub = BlockProblem(bed=bed, n_ref=prob.n_ref, n_obs=prob.n_obs, sigma_s=prob.sigma_s,
+                       s_ptr=s_ptr, s_pos=s_pos, z_s=prob.z_s[s_idx], tau=prob.tau,
+                       opts=dict(prob.opts), **kw)
     return sub, s_idx.astype(np.int64), l_idx.astype(np.int64)
 
 
@@ -83,6 +95,49 @@ def gather_beta(n_s: int, n_l: int, s_idx, l_idx, beta_s, beta_l, device="cpu"):
         a = t[:, :k].cpu().numpy()
         full[a[0].astype(np.int64)] = a[1]
     return full[:n_s], full[n_s:]
+
+
+class ShardGather:
+    """Per-step gather of this rank's betas to rank 0 for a fixed shard layout: the counts and
+    the padded width are exchanged once; each call is ONE `gather` of a [k, width] fp64 buffer
+    (k = solves per step, e.g. the h2f factors) -- over RCCL/xGMI with the nccl backend."""
+
+    def __init__(self, n_s, n_l, s_idx, l_idx, k=1, device="cpu"):
+        import torch
+        import torch.distributed as dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.n_s, self.n_l, self.k, self.device = n_s, n_l, k, device
+        self.idx = np.concatenate([s_idx, n_s + np.asarray(l_idx, dtype=np.int64)]).astype(np.int64)
+        cnt = torch.tensor([self.idx.size], dtype=torch.int64, device=device)
+        cnts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(cnts, cnt)
+        self.cnts = [int(c.item()) for c in cnts]
+        self.width = max(1, max(self.cnts))
+        self.buf = torch.zeros((k, self.width), dtype=torch.float64, device=device)
+        self.out = [torch.empty_like(self.buf) for _ in range(self.world)] if self.rank == 0 else None
+        idx = torch.full((self.width,), -1, dtype=torch.int64, device=device)
+        idx[:self.idx.size] = torch.from_numpy(self.idx).to(device)
+        self.idxs = [torch.empty_like(idx) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(idx, gather_list=self.idxs, dst=0)
+        if self.rank == 0:
+            self.idxs = [t[:c].cpu().numpy() for t, c in zip(self.idxs, self.cnts)]
+
+    def __call__(self, betas):
+        """betas: k pairs (beta_s, beta_l) of this rank's shard -> on rank 0 the full k pairs in
+        the original order (None elsewhere)."""
+        import torch
+        import torch.distributed as dist
+        host = np.zeros((self.k, self.width))
+        for c, (bs, bl) in enumerate(betas):
+            host[c, :self.idx.size] = np.concatenate([bs, bl])
+        self.buf.copy_(torch.from_numpy(host))
+        dist.gather(self.buf, gather_list=self.out, dst=0)
+        if self.rank != 0:
+            return None
+        full = np.full((self.k, self.n_s + self.n_l), np.nan)
+        for t, ix in zip(self.out, self.idxs):
+            full[:, ix] = t[:, :ix.size].cpu().numpy()
+        return [(full[c, :self.n_s], full[c, self.n_s:]) for c in range(self.k)]
 
 
 def est_distributed(prob, solve=None, device=None):

@@ -18,7 +18,9 @@
  * Conventions: plain pointers and sizes, no C++ types, no exceptions across the boundary.
  * Every call returns 0 on success or a negative DBSLMM_E* code; dbslmm_last_error(ctx) then
  * holds a message.  The caller owns every buffer; inputs are read-only for the call.  One call
- * at a time per context; distinct contexts are independent (one context drives one GPU).
+ * at a time per context; distinct contexts are independent.  A context drives one GPU
+ * (dbslmm_ctx_create) or several (dbslmm_ctx_create_multi: the LD blocks of every plan are
+ * sharded over the devices).
  */
 #ifndef DBSLMM_HIP_H_
 #define DBSLMM_HIP_H_
@@ -126,6 +128,21 @@ int dbslmm_abi_version(void);
 
 /* Create a context on HIP device `device` (ordinal as seen by this process). */
 int dbslmm_ctx_create(int device, dbslmm_ctx** out);
+
+/* Create a context over n_dev HIP devices (ordinals; a device may repeat: several shards on one
+ * GPU).  Replaces the reference's only parallelism, OpenMP over LD blocks
+ * (scr/dbslmmfit.cpp:191-220), with one GPU per shard: plan_create assigns the non-empty LD
+ * blocks to the devices (longest processing time first on n_ref m (m+1) + m^3/3), uploads to each
+ * device only the .bed rows of its blocks, and every plan / est call then drives all devices
+ * concurrently (one host thread per device) and returns beta, status and variance columns in the
+ * caller's original order.  dbslmm_bed_maf splits its rows over the devices; read_snp_std and
+ * valid_blocks run on the first device.  n_dev == 1 is dbslmm_ctx_create(device_ids[0]). */
+int dbslmm_ctx_create_multi(int32_t n_dev, const int32_t* device_ids, dbslmm_ctx** out);
+/* Devices a context drives (1 for dbslmm_ctx_create). */
+int dbslmm_ctx_num_devices(const dbslmm_ctx* ctx);
+/* block_device[b] (num_block entries) = the device index (0 .. n_dev-1, in device_ids order) that
+ * solves block b, -1 for an empty block; all 0 on a single-device context. */
+int dbslmm_plan_shard_info(const dbslmm_plan* plan, int32_t* block_device);
 void dbslmm_ctx_destroy(dbslmm_ctx* ctx);
 const char* dbslmm_last_error(const dbslmm_ctx* ctx);
 

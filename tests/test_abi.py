@@ -64,3 +64,24 @@ def test_ctx_create_without_gpu_fails_cleanly():
     from dbslmm_amd import Context, DbslmmError
     with pytest.raises(DbslmmError):
         Context(0)
+
+
+def test_multi_ctx_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from dbslmm_amd import Context, DbslmmError
+    with pytest.raises(DbslmmError):
+        Context([0, 0])
+
+
+def test_options_struct_matches_header():
+    """The ctypes mirror of dbslmm_options / dbslmm_problem has the header's field order."""
+    from dbslmm_amd import _lib
+    src = open(HEADER).read()
+    body = re.search(r"typedef struct dbslmm_options \{(.*?)\} dbslmm_options;", src, re.S).group(1)
+    names = re.findall(r"(\w+);", body)
+    assert names == [f[0] for f in _lib.Options._fields_]
+    body = re.search(r"typedef struct dbslmm_problem \{(.*?)\} dbslmm_problem;", src, re.S).group(1)
+    names = re.findall(r"(\w+);", body)
+    assert names == [f[0] for f in _lib.Problem._fields_]

@@ -147,3 +147,23 @@ def test_cli_h2f_tuning_matches_separate_runs(tmp_path, monkeypatch, cheb):
             kr, vr = _eff_rows(ref)
             assert kt == kr
             assert np.max(np.abs(vt - vr)) <= 1e-12 * np.max(np.abs(vr))
+
+
+@pytest.mark.gpu
+def test_cli_gpu_ids_shards_match_single_gpu(tmp_path):
+    """--gpu-ids 0,0,0 (the LD blocks of chromosome 1 sharded over three contexts; on a node
+    --gpus N uses devices 0..N-1) writes the same <eff>.txt byte for byte as one GPU."""
+    from dbslmm_amd import synth
+    panel = synth.simulate(6000, 300, pop="EUR", chroms=[1], seed=11, large_every=4)
+    f = synth.write_plink(panel, str(tmp_path / "p"))
+    base = ["-s", f["s"], "-l", f["l"], "-r", f["ref"], "-b", f["b"], "-n", str(f["n"]),
+            "-nsnp", str(f["nsnp"]), "-h", "0.5", "--precise-out"]
+    outs = []
+    for extra, name in (([], "one"), (["--gpu-ids", "0,0,0"], "three")):
+        eff = str(tmp_path / name)
+        r = run(base + extra + ["-eff", eff], cwd=str(tmp_path))
+        assert r.returncode == 0, r.stderr
+        outs.append(open(eff + ".txt").read())
+    assert "Sharding the LD blocks over 3 GPUs" in r.stdout
+    assert len(outs[0].splitlines()) > 5000
+    assert outs[0] == outs[1]

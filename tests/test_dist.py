@@ -109,3 +109,57 @@ def test_two_rank_gpu_shards_match_single_gpu(tmp_path):
     assert normwise(got, ref) < 1e-12
     os_, ol, _ = _oracle_solve(prob)
     assert normwise(got, np.concatenate([os_, ol])) < 1e-10
+
+
+def test_compact_sub_problem_same_rows():
+    """compact=True: the sub-problem's own .bed holds exactly its rows; every SNP's row bytes are
+    the full panel's row bytes."""
+    from dbslmm_amd.dist import sub_problem
+    prob = _problem()
+    blocks = np.array([1, 2, 6])
+    sub, s_idx, l_idx = sub_problem(prob, blocks, compact=True)
+    bps = (prob.n_ref + 3) // 4
+    row = lambda bed, r: bed[3 + r * bps: 3 + (r + 1) * bps]
+    for i, j in enumerate(s_idx):
+        assert np.array_equal(row(sub.bed, sub.s_pos[i]), row(prob.bed, prob.s_pos[j]))
+    for i, j in enumerate(l_idx):
+        assert np.array_equal(row(sub.bed, sub.l_pos[i]), row(prob.bed, prob.l_pos[j]))
+    assert sub.bed.size == 3 + (s_idx.size + l_idx.size) * bps
+    a = _oracle_solve(sub)
+    b = _oracle_solve(sub_problem(prob, blocks)[0])
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
+def _gather_worker(rank, world, port, out_path):
+    """The bench's per-step path: compact shard per rank, oracle solve, ShardGather (k = 2 solves
+    per step, called twice)."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle"), here):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from dbslmm_amd import dist as D
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    prob = _problem()
+    m = np.diff(prob.s_ptr) + np.diff(prob.l_ptr)
+    sub, s_idx, l_idx = D.sub_problem(prob, D.shard_blocks(m, prob.n_ref, world)[rank], compact=True)
+    g = D.ShardGather(prob.n_s, prob.n_l, s_idx, l_idx, k=2)
+    bs, bl, _ = _oracle_solve(sub)
+    for _ in range(2):
+        res = g([(bs, bl), (2 * bs, 2 * bl)])
+    if rank == 0:
+        np.save(out_path, np.stack([np.concatenate(r) for r in res]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_gather_per_step(tmp_path, world):
+    out = str(tmp_path / "beta.npy")
+    mp.spawn(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    bs, bl, _ = _oracle_solve(_problem())
+    ref = np.concatenate([bs, bl])
+    np.testing.assert_array_equal(got[0], ref)
+    np.testing.assert_array_equal(got[1], 2 * ref)
