@@ -59,6 +59,8 @@ def parse():
                          "(DBSLMM tuning, config 4)")
     ap.add_argument("--gen", choices=("numpy", "gpu"), default=None,
                     help="synthetic panel generator (default: numpy for config 2, gpu above)")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="dbslmm_options field (path thresholds; experiments), repeatable")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host threads (OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -318,6 +320,9 @@ def main():
     panel = synth.simulate(args.snps, args.n_ref, pop=args.pop, seed=1 if sharded else 1 + rank,
                            engine=args.gen, device=local if world > 1 else 0)
     full = synth.make_problem(panel, lmm_only=args.lmm_only)
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        full.opts[k] = float(v) if k == "cheb_tol" else int(v)
     del panel
     sigmas = [full.sigma_s * f for f in args.h2f] if args.h2f else None
     gather = None
@@ -404,7 +409,7 @@ def main():
             "config": {"workload": f"synthetic {args.snps} SNP x {args.n_ref} indiv, 22 chr "
                                    f"{args.pop} LD blocks, {'LMM-only' if args.lmm_only else 'DBSLMM large+small'}, "
                                    f"h2=0.5 (BASELINE configs[{args.config - 1}])", "generator": args.gen,
-                       "h2f": args.h2f,
+                       "h2f": args.h2f, "options": dict(full.opts),
                        "snps_rank0": wl["snps"], "snps_total": total_snps, "n_ref": args.n_ref,
                        "blocks_rank0": wl["blocks"],
                        "gram": "exact int8 dosages on v_mfma_i32_32x32x32_i8, fp64 epilogue",
