@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="dbslmm_options field (path thresholds; experiments), repeatable")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end leg (PLINK files in page cache -> the dbslmm CLI -> <eff>.txt)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host threads (OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -291,6 +293,49 @@ def cpu_leg(args, prob, res, sigmas, wl):
     return cpu, dbeta
 
 
+def e2e_leg(args, panel):
+    """End to end through the drop-in CLI: the workload's synthetic panel written as PLINK
+    ref.{bed,bim,fam} + GEMMA summaries + block file (page cache), then `dbslmm` (mmap'd .bed ->
+    one staged upload -> GPU MAF pass -> parse/match -> plan -> solve -> <eff>.txt per h2f) in a
+    fresh process, twice; the second run is reported.  SNPs/s = solved SNPs / the process's wall
+    time (HIP initialisation included; `ctx` is that part)."""
+    import shutil
+    import subprocess
+    import tempfile
+    from dbslmm_amd import synth
+    d = tempfile.mkdtemp(prefix="dbslmm_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        t0 = time.perf_counter()
+        f = synth.write_plink(panel, d)
+        t_files = time.perf_counter() - t0
+        cmd = [os.path.join(ROOT, "dbslmm_amd", "bin", "dbslmm"), "-s", f["s"], "-r", f["ref"], "-b", f["b"],
+               "-n", str(f["n"]), "-nsnp", str(f["nsnp"]), "-h", "0.5", "-mafMax", "0.2",
+               "-eff", os.path.join(d, "eff"), "--timing"]
+        if not args.lmm_only:
+            cmd += ["-l", f["l"]]
+        if args.h2f:
+            cmd += ["-h2f", ",".join("%g" % x for x in args.h2f)]
+        runs = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            wall = time.perf_counter() - t1
+            if r.returncode != 0:
+                return dict(error=f"dbslmm CLI rc={r.returncode}: {r.stderr[-400:]}")
+            line = [x for x in r.stderr.splitlines() if x.startswith("TIMING ")]
+            ph = json.loads(line[-1][7:]) if line else {}
+            runs.append((wall, ph))
+        wall, ph = runs[-1]
+        n = ph.get("snps", 0)
+        return dict(value=n / wall, unit="SNPs/s", seconds=wall, snps=n, phases_s=ph,
+                    value_after_init=n / max(1e-9, wall - ph.get("ctx", 0.0)),
+                    files_written_s=t_files, solves_per_snp=len(args.h2f) if args.h2f else 1,
+                    note="page-cached PLINK files -> dbslmm CLI -> <eff>.txt, one process on GPU 0 "
+                         "(HIP init, .bed upload, GPU MAF pass, host parse/match, plan, solve, writer)")
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -323,7 +368,8 @@ def main():
     for kv in args.opt:
         k, v = kv.split("=", 1)
         full.opts[k] = float(v) if k == "cheb_tol" else int(v)
-    del panel
+    if world > 1 or args.no_e2e:
+        del panel
     sigmas = [full.sigma_s * f for f in args.h2f] if args.h2f else None
     gather = None
     if sharded:
@@ -398,6 +444,10 @@ def main():
     dbeta = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, dbeta = cpu_leg(args, prob, res, sigmas, wl)
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = e2e_leg(args, panel)
+        del panel
 
     if rank == 0:
         line = {
@@ -424,6 +474,7 @@ def main():
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
             "max_dbeta_vs_cpu_ref": dbeta,
             "status_nonzero_blocks": int(st.item()),
         }

@@ -52,6 +52,17 @@ class Context:
     def num_devices(self) -> int:
         return int(self.lib.dbslmm_ctx_num_devices(self.h))
 
+    def cache_bed(self, bed):
+        """Keep a device copy of this .bed image (dbslmm_ctx_cache_bed); bed_maf / plan_create on
+        the same array then skip their upload.  None releases it."""
+        if bed is None:
+            self._cached_bed = None
+            self.check(self.lib.dbslmm_ctx_cache_bed(self.h, None, 0), "ctx_cache_bed")
+            return
+        b = np.ascontiguousarray(bed, dtype=np.uint8)
+        self.check(self.lib.dbslmm_ctx_cache_bed(self.h, _ptr(b), b.size), "ctx_cache_bed")
+        self._cached_bed = b       # the host range must stay alive and unchanged
+
     def check(self, rc: int, what: str):
         if rc != 0:
             msg = self.lib.dbslmm_last_error(self.h).decode(errors="replace")

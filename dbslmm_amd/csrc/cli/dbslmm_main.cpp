@@ -50,7 +50,7 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     int gpu = 0;
     string gpu_ids;                 // --gpus N -> "0,1,..,N-1"; --gpu-ids a,b,..
     double tau = 0.8;
-    bool precise = false, dry_run = false, h2f_merged = false;
+    bool precise = false, dry_run = false, h2f_merged = false, timing = false;
     string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
 };
 
@@ -89,6 +89,7 @@ void print_help() {
               << " --gpu-ids [list]       shard over the listed devices, e.g. 0,1,2 (extension)\n"
               << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
               << " --precise-out          17 significant digits in <eff>.txt (extension)\n"
+              << " --timing               phase wall times as one JSON line on stderr (extension)\n"
               << " -h2f      [list]       h2 factors, e.g. 0.8,1,1.2: one Gram, one solve per factor,\n"
               << "                        <eff>_h2f<f>.txt each (software/DBSLMM.R tuning, extension)\n"
               << " --h2f-merged           -h2f: one factorisation per factor instead of one factor +\n"
@@ -130,6 +131,7 @@ void assign(int argc, char** argv, Param& p) {
         else if (is("--h2f", "-h2f")) { if ((v = take(i))) p.h2f = v; }
         else if (!strcmp(a, "--h2f-merged")) p.h2f_merged = true;
         else if (!strcmp(a, "--dry-run")) p.dry_run = true;
+        else if (!strcmp(a, "--timing")) p.timing = true;
     }
 }
 
@@ -324,7 +326,25 @@ int fail(const string& msg) {
 
 }  // namespace
 
+// --timing: wall time of each phase (seconds), printed as one JSON line on stderr at exit
+struct Phases {
+    double t0 = walltime(), last = t0;
+    string json;
+    void mark(const char* name) {
+        const double t = walltime();
+        char buf[96];
+        snprintf(buf, sizeof(buf), "%s\"%s\": %.6f", json.empty() ? "" : ", ", name, t - last);
+        json += buf;
+        last = t;
+    }
+    void print(int64_t n_snp) const {
+        fprintf(stderr, "TIMING {%s, \"total\": %.6f, \"snps\": %lld}\n", json.c_str(), walltime() - t0,
+                static_cast<long long>(n_snp));
+    }
+};
+
 int main(int argc, char** argv) {
+    Phases ph;
     if (argc <= 1) { print_header(); return 0; }
     if (argc == 2 && argv[1][0] == '-' && argv[1][1] == 'h') { print_help(); return 0; }
     Param p;
@@ -360,6 +380,11 @@ int main(int argc, char** argv) {
         if (!bed.open(p.r + ".bed")) return fail(p.r + ".bed cannot be opened");
         if (p.gpu_ids.empty()) {
             if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) return fail("no usable HIP device (dbslmm_ctx_create)");
+            ph.mark("ctx");
+            // one staged upload of the .bed serves both the MAF pass and the plan
+            if (dbslmm_ctx_cache_bed(ctx, bed.p, static_cast<int64_t>(bed.n)) != DBSLMM_OK)
+                return fail(string("uploading the .bed: ") + dbslmm_last_error(ctx));
+            ph.mark("bed_upload");
         } else {
             vector<int32_t> ids;
             for (const string& t : split(p.gpu_ids, ',')) ids.push_back(atoi(t.c_str()));
@@ -376,6 +401,7 @@ int main(int argc, char** argv) {
         maf.resize(n_snp_bim);
         if (dbslmm_bed_maf(ctx, bed.p, static_cast<int64_t>(bed.n), n_ref, n_snp_bim, maf.data()) != DBSLMM_OK)
             return fail(string("MAF pass: ") + dbslmm_last_error(ctx));
+        ph.mark("maf");
     } else {
         std::cout << "[WARNING] Do not consider the difference between reference panel and summary data ...\n";
     }
@@ -442,6 +468,7 @@ int main(int argc, char** argv) {
         return 0;
     }
 
+    ph.mark("parse");
     const double sigma_s = p.h / static_cast<double>(p.nsnp);                 // dbslmm.cpp:332
     dbslmm_problem prob{};
     prob.bed = bed.p;
@@ -481,7 +508,9 @@ int main(int argc, char** argv) {
     const double t0 = walltime();
     dbslmm_plan* plan = nullptr;
     int rc = dbslmm_plan_create(ctx, &prob, &plan);
+    ph.mark("plan");
     if (rc == DBSLMM_OK) rc = dbslmm_plan_run_multi(plan, sigmas.data(), nf, beta_s.data(), beta_l.data(), status.data());
+    ph.mark("solve");
     if (rc != DBSLMM_OK) {
         dbslmm_plan_destroy(plan);
         return fail(string("dbslmm_plan_run_multi: ") + dbslmm_last_error(ctx));
@@ -509,6 +538,7 @@ int main(int argc, char** argv) {
     }
     dbslmm_plan_destroy(plan);
     std::cout << "Fitting time: " << walltime() - t0 << " seconds.\n";
+    ph.mark("variance");
 
     for (int f = 0; f < nf; ++f) {
         int n_bad = 0;
@@ -543,6 +573,8 @@ int main(int argc, char** argv) {
         emit(info_l, bl, 1);
         emit(info_s, bs, 0);
     }
+    ph.mark("write");
     dbslmm_ctx_destroy(ctx);
+    if (p.timing) ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));
     return 0;
 }

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -76,6 +77,11 @@ struct dbslmm_ctx {
     hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
     int n_cu = 256;                  // compute units (persistent substitution grid)
     std::string err;
+    // device copy of a caller's .bed image (dbslmm_ctx_cache_bed): bed_maf and plan_create on the
+    // same host range (pointer and length) read it instead of uploading again
+    const uint8_t* bed_host = nullptr;
+    int64_t bed_host_len = 0;
+    uint8_t* d_bed_cache = nullptr;
     std::vector<dbslmm_ctx*> subs;   // multi-device context (multi.hip): one context per device,
                                      // device = -1 and no streams of its own
 };
@@ -200,6 +206,58 @@ static int mp_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int32_t n_ref, int64_
             return rc_;                                                  \
         }                                                                \
     } while (0)
+
+// Host -> device copy of a large, possibly pageable (mmap'd, page-cache backed) buffer through two
+// pinned staging buffers: while chunk k is DMA'd, host threads copy chunk k + 1 into the other
+// buffer (the page-cache reads of an mmap'd .bed are the slow side, so they run on several
+// threads).  Small buffers take a plain hipMemcpy.  Ends synchronised.
+static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_t st) {
+    constexpr size_t kChunk = size_t(64) << 20;
+    if (n <= 2 * kChunk) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice);
+    void* stage[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+        e = hipHostMalloc(&stage[b], kChunk, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&done[b], hipEventDisableTiming);
+    }
+    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (size_t off = 0, k = 0; off < n && e == hipSuccess; off += kChunk, ++k) {
+        const int b = static_cast<int>(k & 1);
+        const size_t len = std::min(kChunk, n - off);
+        if (k >= 2 && (e = hipEventSynchronize(done[b])) != hipSuccess) break;   // buffer b free again
+        const char* s0 = static_cast<const char*>(src) + off;
+        char* d0 = static_cast<char*>(stage[b]);
+        std::vector<std::thread> th;
+        const size_t part = (len + hw - 1) / hw;
+        for (unsigned t = 0; t < hw; ++t) {
+            const size_t a = t * part, z = std::min(len, a + part);
+            if (a < z) th.emplace_back([=] { memcpy(d0 + a, s0 + a, z - a); });
+        }
+        for (auto& t : th) t.join();
+        e = hipMemcpyAsync(static_cast<char*>(dst) + off, stage[b], len, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(done[b], st);
+    }
+    const hipError_t e2 = hipStreamSynchronize(st);
+    for (int b = 0; b < 2; ++b) {
+        if (done[b]) (void)hipEventDestroy(done[b]);
+        if (stage[b]) (void)hipHostFree(stage[b]);
+    }
+    return e != hipSuccess ? e : e2;
+}
+
+// The .bed image on the device: a device-to-device copy of the context's cached image when the
+// caller passes the same host range, else a staged upload.  dst holds bed_len + 16 bytes (zero pad).
+static hipError_t bed_to_device(dbslmm_ctx* ctx, uint8_t* dst, const uint8_t* bed, int64_t bed_len) {
+    hipError_t e = hipMemsetAsync(dst + bed_len, 0, 16, ctx->stream);
+    if (e != hipSuccess) return e;
+    if (ctx->d_bed_cache && bed == ctx->bed_host && bed_len == ctx->bed_host_len) {
+        e = hipMemcpyAsync(dst, ctx->d_bed_cache, bed_len, hipMemcpyDeviceToDevice, ctx->stream);
+        return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+    }
+    e = hipStreamSynchronize(ctx->stream);
+    return e != hipSuccess ? e : upload_staged(dst, bed, bed_len, ctx->stream);
+}
 
 template <typename T>
 static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
@@ -431,6 +489,7 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
         return;
     }
     (void)hipSetDevice(ctx->device);
+    if (ctx->d_bed_cache) (void)hipFree(ctx->d_bed_cache);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
@@ -441,6 +500,24 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
 }
 
 const char* dbslmm_last_error(const dbslmm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len) {
+    if (!ctx) return DBSLMM_E_ARG;
+    if (!ctx->subs.empty()) return DBSLMM_OK;   // multi-device: each device gets its own rows
+    ARG_CHECK(ctx, (bed == nullptr) == (bed_len == 0) && bed_len >= 0, "bed / bed_len");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (ctx->d_bed_cache) HIP_TRY(ctx, hipFree(ctx->d_bed_cache));
+    ctx->d_bed_cache = nullptr;
+    ctx->bed_host = nullptr;
+    ctx->bed_host_len = 0;
+    if (!bed) return DBSLMM_OK;
+    HIP_TRY(ctx, hipMalloc(&ctx->d_bed_cache, bed_len + 16));
+    HIP_TRY(ctx, hipMemset(ctx->d_bed_cache + bed_len, 0, 16));
+    HIP_TRY(ctx, upload_staged(ctx->d_bed_cache, bed, bed_len, ctx->stream));
+    ctx->bed_host = bed;
+    ctx->bed_host_len = bed_len;
+    return DBSLMM_OK;
+}
 
 void dbslmm_plan_destroy(dbslmm_plan* p) {
     if (!p) return;
@@ -716,8 +793,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     };
     if (e != hipSuccess) return fail("hipSetDevice");
     if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
-    if ((e = hipMemset(p->d_bed, 0, pr->bed_len + 16)) != hipSuccess) return fail("hipMemset bed");
-    if ((e = hipMemcpy(p->d_bed, pr->bed, pr->bed_len, hipMemcpyHostToDevice)) != hipSuccess) return fail("upload bed");
+    if ((e = bed_to_device(ctx, p->d_bed, pr->bed, pr->bed_len)) != hipSuccess) return fail("upload bed");
     // + kHT spare rows: a 256-row Gram tile may read past the last slot (results discarded)
     const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kHT) * (p->kpad / 4);
     if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
@@ -1569,9 +1645,9 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
     int rc = DBSLMM_OK;
     do {
         hipError_t e;
-        if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
-            (e = hipMemset(d_bed, 0, bed_len + 16)) != hipSuccess ||
-            (e = hipMemcpy(d_bed, bed, bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
+        const bool cached = ctx->d_bed_cache && bed == ctx->bed_host && bed_len == ctx->bed_host_len;
+        if ((!cached && ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
+                         (e = bed_to_device(ctx, d_bed, bed, bed_len)) != hipSuccess)) ||
             (e = dev_upload(&d_pos, pos)) != hipSuccess ||
             (e = hipMalloc(&d_maf, n_snp * sizeof(double))) != hipSuccess) {
             ctx->err = std::string("bed_maf alloc/upload: ") + hipGetErrorString(e);
@@ -1579,7 +1655,8 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
             break;
         }
         dim3 grid(static_cast<unsigned>((n_snp + 3) / 4));
-        hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, ctx->stream, d_bed, n_ref, bps,
+        hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, ctx->stream, cached ? ctx->d_bed_cache : d_bed,
+                           n_ref, bps,
                            d_pos, d_pos, static_cast<int32_t>(n_snp), nullptr, round_up(n_ref, 64),
                            nullptr, nullptr, nullptr, d_maf, nullptr);
         if ((e = hipGetLastError()) != hipSuccess ||

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 5
+#define DBSLMM_ABI_VERSION 6
 
 enum {
     DBSLMM_OK = 0,
@@ -145,6 +145,13 @@ int dbslmm_ctx_num_devices(const dbslmm_ctx* ctx);
 int dbslmm_plan_shard_info(const dbslmm_plan* plan, int32_t* block_device);
 void dbslmm_ctx_destroy(dbslmm_ctx* ctx);
 const char* dbslmm_last_error(const dbslmm_ctx* ctx);
+/* Keep a device copy of the caller's .bed image on the context (staged upload through pinned
+ * buffers): dbslmm_bed_maf and dbslmm_plan_create calls that pass the same host range (bed,
+ * bed_len) then read it instead of uploading again -- the reference reads the .bed once for the
+ * MAF pass (IO::readBim, dtpr.cpp:93-102) and again per block in calcBlock (dbslmmfit.cpp:
+ * 384-387).  The caller must not modify the buffer while it is cached.  bed == NULL releases the
+ * copy.  A multi-device context ignores the call (each device holds only its shard's rows). */
+int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len);
 
 /* DBSLMMFIT::est replacement: upload, solve, download, free.  beta_s has s_ptr[num_block]
  * entries, beta_l l_ptr[num_block] (ignored when l_ptr == NULL); block_status (optional) has

@@ -1,4 +1,5 @@
 """The drop-in `dbslmm` CLI: argument handling and host parsing (CPU), end-to-end (GPU)."""
+import json
 import os
 import subprocess
 
@@ -167,3 +168,29 @@ def test_cli_gpu_ids_shards_match_single_gpu(tmp_path):
     assert "Sharding the LD blocks over 3 GPUs" in r.stdout
     assert len(outs[0].splitlines()) > 5000
     assert outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+def test_cli_timing_and_mafmax_multichrom(tmp_path):
+    """--timing prints the phase wall times as one JSON line on stderr; the run goes through the
+    cached .bed (one upload for the MAF pass and the plan) and writes the same rows as a run
+    without it -- over three chromosomes in one call (blocks in chromosome order)."""
+    from dbslmm_amd import synth
+    panel = synth.simulate(9000, 256, pop="EUR", chroms=[20, 21, 22], seed=4, large_every=5)
+    f = synth.write_plink(panel, str(tmp_path / "p"))
+    base = ["-s", f["s"], "-l", f["l"], "-r", f["ref"], "-b", f["b"], "-n", str(f["n"]),
+            "-nsnp", str(f["nsnp"]), "-h", "0.5", "-mafMax", "0.2", "--precise-out"]
+    eff = str(tmp_path / "t")
+    r = run(base + ["-eff", eff, "--timing"], cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    line = [x for x in r.stderr.splitlines() if x.startswith("TIMING ")]
+    assert len(line) == 1, r.stderr
+    ph = json.loads(line[0][7:])
+    for k in ("ctx", "bed_upload", "maf", "parse", "plan", "solve", "write", "total"):
+        assert ph[k] >= 0.0, k
+    rows = open(eff + ".txt").read().splitlines()
+    assert ph["snps"] == len(rows) > 8000
+    # a second run writes the same rows (deterministic reductions)
+    eff2 = str(tmp_path / "u")
+    r = run(base + ["-eff", eff2], cwd=str(tmp_path))
+    assert r.returncode == 0 and open(eff2 + ".txt").read().splitlines() == rows

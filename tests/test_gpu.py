@@ -222,3 +222,32 @@ def test_run_multi_sigma_matches_separate_solves(fit, monkeypatch):
         np.testing.assert_array_equal(bl, rl)
         np.testing.assert_array_equal(st, rst)
     assert not np.array_equal(multi[0][0], multi[2][0])
+
+
+def test_cached_and_staged_bed_upload_identical(fit):
+    """dbslmm_ctx_cache_bed: one staged (pinned, chunked) upload serves bed_maf and plan_create;
+    results equal the uncached path bit for bit.  The 200 MB image takes the staged path (> 2
+    chunks of 64 MB, ragged tail)."""
+    from dbslmm_amd import Context, Plan, bed_maf
+    rng = np.random.default_rng(3)
+    n_ref, n_snp = 1001, 800_003
+    bps = (n_ref + 3) // 4
+    bed = rng.integers(0, 256, size=3 + n_snp * bps, dtype=np.uint8)
+    bed[:3] = (0x6C, 0x1B, 0x01)
+    plain = bed_maf(fit.ctx, bed, n_ref, n_snp)
+    ctx = Context(0)
+    ctx.cache_bed(bed)
+    np.testing.assert_array_equal(bed_maf(ctx, bed, n_ref, n_snp), plain)
+    ctx.cache_bed(None)
+    d = td_problem(nsnp=996, tau=0.8)
+    ctx.cache_bed(d["bed"])
+    from dbslmm_amd import BlockProblem
+    prob = BlockProblem(bed=d["bed"], n_ref=d["n_ref"], n_obs=d["n_obs"], sigma_s=d["sigma_s"],
+                        s_ptr=d["s_ptr"], s_pos=d["s_pos"], z_s=d["z_s"], l_ptr=d["l_ptr"],
+                        l_pos=d["l_pos"], z_l=d["z_l"], tau=0.8)
+    plan = Plan(ctx, prob)
+    plan.run()
+    a = plan.download()
+    b = fit.est(prob)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
