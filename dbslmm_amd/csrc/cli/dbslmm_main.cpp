@@ -30,6 +30,7 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -135,49 +136,65 @@ void assign(int argc, char** argv, Param& p) {
     }
 }
 
-// IO::readBim (scr/dtpr.cpp:83-123): maf from the GPU MAF pass when constr.
+// IO::readBim (scr/dtpr.cpp:83-123): maf from the GPU MAF pass when constr.  Lines are split on
+// several threads; the map keeps the first occurrence of a SNP id, as std::map::insert does.
 bool read_bim(const string& ref, const vector<double>& maf, std::unordered_map<string, Allele>& bim,
               vector<string>& order) {
-    std::ifstream f(ref + ".bim");
-    if (!f) return false;
-    string line;
-    int64_t count = 0;
-    while (std::getline(f, line)) {
-        auto t = split(line, '\t');
-        if (t.size() < 6) { ++count; continue; }
-        const double m = count < static_cast<int64_t>(maf.size()) ? maf[count] : 0.0;
-        if (bim.find(t[1]) == bim.end()) {                 // std::map::insert keeps the first
-            bim.emplace(t[1], Allele{count, t[4], t[5], m});
-            order.push_back(t[1]);
+    const string text = read_file(ref + ".bim");
+    if (text.empty()) { std::ifstream f(ref + ".bim"); return static_cast<bool>(f); }
+    const vector<string_view> lines = lines_of(text);
+    struct Row { string_view snp, a1, a2; bool ok; };
+    vector<Row> rows(lines.size());
+    parallel_chunks(lines.size(), host_threads(), [&](size_t lo, size_t hi) {
+        vector<string_view> t;
+        for (size_t i = lo; i < hi; ++i) {
+            split_view(lines[i], '\t', t);
+            rows[i] = t.size() < 6 ? Row{{}, {}, {}, false} : Row{t[1], t[4], t[5], true};
         }
-        ++count;
+    });
+    bim.reserve(rows.size());
+    for (size_t count = 0; count < rows.size(); ++count) {
+        const Row& r = rows[count];
+        if (!r.ok) continue;
+        const double m = count < maf.size() ? maf[count] : 0.0;
+        auto ins = bim.emplace(string(r.snp), Allele{static_cast<int64_t>(count), string(r.a1), string(r.a2), m});
+        if (ins.second) order.push_back(ins.first->first);
     }
     return true;
 }
 
 // IO::readSumm (scr/dtpr.cpp:178-220): GEMMA, no header; z = beta/se when se starts with a digit
-// and > 1e-20, else 0.
+// and > 1e-20, else 0.  Parsed in contiguous line chunks on several threads, kept in file order.
 vector<Summ> read_summ(const string& path) {
-    vector<Summ> out;
-    std::ifstream f(path);
-    string line;
-    while (std::getline(f, line)) {
-        auto t = split(line, '\t');
-        if (t.size() < 11) continue;
-        Summ s;
-        s.z = 0.0;
-        if (isdigit(static_cast<unsigned char>(t[9].c_str()[0]))) {
-            const double se = atof(t[9].c_str());
-            if (se - 0.0 > 1e-20) s.z = atof(t[8].c_str()) / se;
+    const string text = read_file(path);
+    const vector<string_view> lines = lines_of(text);
+    vector<Summ> rows(lines.size());
+    vector<char> ok(lines.size(), 0);
+    parallel_chunks(lines.size(), host_threads(), [&](size_t lo, size_t hi) {
+        vector<string_view> t;
+        for (size_t i = lo; i < hi; ++i) {
+            split_view(lines[i], '\t', t);
+            if (t.size() < 11) continue;
+            Summ& s = rows[i];
+            s.z = 0.0;
+            const string se_s(t[9]), b_s(t[8]), ps_s(t[2]), af_s(t[7]);
+            if (isdigit(static_cast<unsigned char>(se_s.c_str()[0]))) {
+                const double se = atof(se_s.c_str());
+                if (se - 0.0 > 1e-20) s.z = atof(b_s.c_str()) / se;
+            }
+            s.snp = string(t[1]);
+            s.ps = atol(ps_s.c_str());
+            s.a1 = string(t[5]);
+            s.a2 = string(t[6]);
+            const double af = atof(af_s.c_str());
+            s.maf = std::min(af, 1.0 - af);
+            ok[i] = 1;
         }
-        s.snp = t[1];
-        s.ps = atol(t[2].c_str());
-        s.a1 = t[5];
-        s.a2 = t[6];
-        const double af = atof(t[7].c_str());
-        s.maf = std::min(af, 1.0 - af);
-        out.push_back(s);
-    }
+    });
+    vector<Summ> out;
+    out.reserve(rows.size());
+    for (size_t i = 0; i < rows.size(); ++i)
+        if (ok[i]) out.push_back(std::move(rows[i]));
     return out;
 }
 
@@ -188,21 +205,36 @@ struct Pos { string snp; long ps; int64_t pos; string a1; double maf, z; };
 // operator[] does, and is never kept.
 vector<Pos> match_ref(const vector<Summ>& summ, const std::unordered_map<string, Allele>& bim,
                       double maf_max, vector<char>& good) {
-    vector<Pos> inter;
     good.assign(summ.size(), 0);
-    int dis = 0, mafc = 0;
     static const Allele empty{0, "", "", 0.0};
-    for (size_t i = 0; i < summ.size(); ++i) {
-        auto it = bim.find(summ[i].snp);
-        const Allele& b = it == bim.end() ? empty : it->second;
-        const bool a1 = b.a1 == summ[i].a1, a2 = b.a2 == summ[i].a2;
-        const bool mb = std::fabs(b.maf - summ[i].maf) < maf_max;
-        if (!a1 || !a2) ++dis;
-        if (!mb) ++mafc;
-        if (a1 && a2 && mb && it != bim.end()) {
-            inter.push_back({summ[i].snp, summ[i].ps, b.pos, summ[i].a1, summ[i].maf, summ[i].z});
-            good[i] = 1;
-        }
+    const unsigned T = host_threads();
+    vector<vector<Pos>> part(T);
+    vector<int> dis_t(T, 0), maf_t(T, 0);
+    vector<size_t> lo_t(T + 1, 0);
+    for (unsigned t = 0; t <= T; ++t) lo_t[t] = summ.size() * t / T;
+    vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = lo_t[t]; i < lo_t[t + 1]; ++i) {
+                auto it = bim.find(summ[i].snp);
+                const Allele& b = it == bim.end() ? empty : it->second;
+                const bool a1 = b.a1 == summ[i].a1, a2 = b.a2 == summ[i].a2;
+                const bool mb = std::fabs(b.maf - summ[i].maf) < maf_max;
+                if (!a1 || !a2) ++dis_t[t];
+                if (!mb) ++maf_t[t];
+                if (a1 && a2 && mb && it != bim.end()) {
+                    part[t].push_back({summ[i].snp, summ[i].ps, b.pos, summ[i].a1, summ[i].maf, summ[i].z});
+                    good[i] = 1;
+                }
+            }
+        });
+    for (auto& x : th) x.join();
+    vector<Pos> inter;
+    int dis = 0, mafc = 0;
+    for (unsigned t = 0; t < T; ++t) {
+        dis += dis_t[t];
+        mafc += maf_t[t];
+        for (auto& e : part[t]) inter.push_back(std::move(e));
     }
     std::cout << "Number of allele discrepency: " << dis << "\n";
     std::cout << "Number of maf discrepency:    " << mafc << "\n";
@@ -558,20 +590,43 @@ int main(int argc, char** argv) {
             else
                 name += string("_h2f") + hh;
         }
-        // output writer (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small rows
-        std::ofstream out(name + ".txt");
-        if (p.precise) out.precision(17);
+        // output writer (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small rows;
+        // ostream's default double format is printf %g at precision 6 (17 with --precise-out),
+        // formatted in parallel chunks and written in order
+        FILE* out = fopen((name + ".txt").c_str(), "wb");
+        if (!out) return fail(name + ".txt cannot be written");
         const double* bs = beta_s.data() + static_cast<size_t>(f) * info_s.size();
         const double* bl = beta_l.data() + static_cast<size_t>(f) * info_l.size();
+        const int prec = p.precise ? 17 : 6;
         auto emit = [&](const vector<Info>& info, const double* beta, int flag) {
-            for (size_t i = 0; i < info.size(); ++i) {
-                const double noscl = beta[i] / std::sqrt(2 * info[i].maf * (1 - info[i].maf));
-                if (std::isinf(noscl)) continue;
-                out << info[i].snp << " " << info[i].a1 << " " << beta[i] << " " << noscl << " " << flag << "\n";
-            }
+            const unsigned T = host_threads();
+            vector<string> buf(T);
+            vector<std::thread> th;
+            for (unsigned t = 0; t < T; ++t)
+                th.emplace_back([&, t] {
+                    const size_t lo = info.size() * t / T, hi = info.size() * (t + 1) / T;
+                    string& o = buf[t];
+                    o.reserve((hi - lo) * 48);
+                    char num[64];
+                    for (size_t i = lo; i < hi; ++i) {
+                        const double noscl = beta[i] / std::sqrt(2 * info[i].maf * (1 - info[i].maf));
+                        if (std::isinf(noscl)) continue;
+                        o += info[i].snp;
+                        o += ' ';
+                        o += info[i].a1;
+                        o += ' ';
+                        o.append(num, static_cast<size_t>(snprintf(num, sizeof(num), "%.*g", prec, beta[i])));
+                        o += ' ';
+                        o.append(num, static_cast<size_t>(snprintf(num, sizeof(num), "%.*g", prec, noscl)));
+                        o += flag ? " 1\n" : " 0\n";
+                    }
+                });
+            for (auto& x : th) x.join();
+            for (const string& o : buf) fwrite(o.data(), 1, o.size(), out);
         };
         emit(info_l, bl, 1);
         emit(info_s, bs, 0);
+        fclose(out);
     }
     ph.mark("write");
     dbslmm_ctx_destroy(ctx);

@@ -162,6 +162,7 @@ struct dbslmm_plan {
     double* d_cheb = nullptr;
     double* d_coef = nullptr;
     int32_t coef_cap = 0;
+    std::vector<double> h_coef;              // the coefficients in d_coef
     std::vector<hipGraphExec_t> graph_copy;  // the single-copy tiled sequence on copy c
     int32_t cheb_base = -1;                  // base copy of the last Chebyshev run (-1: none)
     bool cheb_pending_var = false;           // copy var_copy's tiled blocks are not factored yet
@@ -1119,14 +1120,20 @@ static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
     if (!p->d_cheb)
         HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    // the coefficients depend only on the sigmas: uploaded when they change, synchronously (the
+    // host vector is a temporary of the run; an asynchronous copy from pageable memory may still
+    // be pending when it is freed) after every earlier run that reads d_coef has finished
+    if (cp.coef == p->h_coef) return DBSLMM_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(st));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream2));
     if (p->coef_cap < static_cast<int32_t>(cp.coef.size())) {
         if (p->d_coef) (void)hipFree(p->d_coef);
         p->d_coef = nullptr;
         HIP_TRY(ctx, hipMalloc(&p->d_coef, cp.coef.size() * sizeof(double)));
         p->coef_cap = static_cast<int32_t>(cp.coef.size());
     }
-    HIP_TRY(ctx, hipMemcpyAsync(p->d_coef, cp.coef.data(), cp.coef.size() * sizeof(double),
-                                hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx, hipMemcpy(p->d_coef, cp.coef.data(), cp.coef.size() * sizeof(double), hipMemcpyHostToDevice));
+    p->h_coef = cp.coef;
     return DBSLMM_OK;
 }
 
