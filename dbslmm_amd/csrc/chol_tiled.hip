@@ -94,6 +94,24 @@ __device__ __forceinline__ void stage64(double* S, const double* A, int ld, int 
     }
 }
 
+// stage_tile split into its loads (registers) and its LDS stores, so the next slice of a
+// pending update is in flight while the current one is multiplied
+__device__ __forceinline__ void tile32_load(double (&v)[kT * kT / kWave], const double* A, int ld, int r0, int c0,
+                                            int lane) {
+#pragma unroll
+    for (int it = 0; it < kT * kT / kWave; ++it) {
+        const int e = it * kWave + lane;
+        v[it] = A[static_cast<int64_t>(r0 + (e >> 5)) * ld + c0 + (e & 31)];
+    }
+}
+__device__ __forceinline__ void tile32_store(const double (&v)[kT * kT / kWave], double* W, int lane) {
+#pragma unroll
+    for (int it = 0; it < kT * kT / kWave; ++it) {
+        const int e = it * kWave + lane;
+        W[(e >> 5) * kTS + (e & 31)] = v[it];
+    }
+}
+
 }  // namespace chol
 
 // ---------------------------------------------------------------- 128-column regions
@@ -329,10 +347,13 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     }
     if (update) {
         double* P = X32;   // staging of one 32-column slice of the panel rows (4 sub-tiles)
-        const int cp = c0 - 2 * kBT * update;
-        for (int k = 0; k < 4 * update; ++k) {
-            __syncthreads();
-            stage_tile(P + wave * kSub, A, ld, c0 + kT * wave, cp + kT * k, lane);
+        const int cp = c0 - 2 * kBT * update, nk = 4 * update;
+        double nv[kT * kT / chol::kWave];
+        tile32_load(nv, A, ld, c0 + kT * wave, cp, lane);
+        for (int k = 0; k < nk; ++k) {
+            __syncthreads();                  // every wave is done with the previous slice
+            tile32_store(nv, P + wave * kSub, lane);
+            if (k + 1 < nk) tile32_load(nv, A, ld, c0 + kT * wave, cp + kT * (k + 1), lane);
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < 3; ++u)
@@ -490,12 +511,23 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
         // launch of region s's columns would do): A_i -= L_{i,.} L_{R,.}^T, R = region s's 128
         // rows; wave (qi, qj) updates its quadrant of both 64-column halves, operands staged 32
         // columns at a time (sub-tiles 0-1: rows of tile i, 2-5: rows of the region)
-        const int cp = c0 - 2 * kBT * upd;
+        const int cp = c0 - 2 * kBT * upd, nk = 4 * upd;
         load_acc(u0, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);
         if (two) load_acc(cc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);
-        for (int kc = 0; kc < 4 * upd; ++kc) {
-            for (int q = wave; q < 6; q += 4)
-                stage_tile(lds + q * kSub, A, ld, q < 2 ? kBT * i + kT * q : c0 + kT * (q - 2), cp + kT * kc, lane);
+        // sub-tile q of a slice: rows of tile i (q < 2) or of the region (q >= 2); wave w stages
+        // q = w and (waves 0, 1) q = w + 4, the next slice in flight during the current MFMAs
+        const int qa = wave, qb = wave + 4;
+        const int ra = qa < 2 ? kBT * i + kT * qa : c0 + kT * (qa - 2), rb = c0 + kT * (qb - 2);
+        double na[kT * kT / chol::kWave], nb[kT * kT / chol::kWave];
+        tile32_load(na, A, ld, ra, cp, lane);
+        if (qb < 6) tile32_load(nb, A, ld, rb, cp, lane);
+        for (int kc = 0; kc < nk; ++kc) {
+            tile32_store(na, lds + qa * kSub, lane);
+            if (qb < 6) tile32_store(nb, lds + qb * kSub, lane);
+            if (kc + 1 < nk) {
+                tile32_load(na, A, ld, ra, cp + kT * (kc + 1), lane);
+                if (qb < 6) tile32_load(nb, A, ld, rb, cp + kT * (kc + 1), lane);
+            }
             __syncthreads();
             mfma_tile(u0, lds + qi * kSub, lds + (2 + qj) * kSub, -1.0, lane);
             if (two) mfma_tile(cc, lds + qi * kSub, lds + (4 + qj) * kSub, -1.0, lane);
