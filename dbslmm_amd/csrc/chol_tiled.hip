@@ -290,6 +290,25 @@ __device__ __forceinline__ void store_acc_t(const v4d (&acc)[2][2], double* A, i
             }
 }
 
+// A 64 x 64 tile of L held in 4 LDS sub-tiles (S[2a + b] = rows 32 a.., cols 32 b..) -> A at
+// (r0, c0), and transposed into the upper triangle at (c0, r0) for the row-streaming backward
+// substitution (rows >= m not copied).  Both writes in whole 512-B row segments (the per-lane
+// MFMA layout would scatter 32-B pieces over 16 rows per instruction).
+__device__ __forceinline__ void store64_both(const double* S, double* A, int ld, int r0, int c0, int m, int tid) {
+    constexpr int NT = kLargeThreads;
+#pragma unroll 4
+    for (int it = 0; it < kBT * kBT / NT; ++it) {
+        const int e = it * NT + tid, r = e >> 6, c = e & 63;
+        A[static_cast<int64_t>(r0 + r) * ld + c0 + c] = S[(2 * (r >> 5) + (c >> 5)) * kSub + (r & 31) * kTS + (c & 31)];
+    }
+#pragma unroll 4
+    for (int it = 0; it < kBT * kBT / NT; ++it) {
+        const int e = it * NT + tid, c = e >> 6, r = e & 63;
+        if (r0 + r < m)
+            A[static_cast<int64_t>(c0 + c) * ld + r0 + r] = S[(2 * (r >> 5) + (c >> 5)) * kSub + (r & 31) * kTS + (c & 31)];
+    }
+}
+
 // lower sub-tiles (a >= b) of a 128 x 128 region, 4 x 4 of 32
 __device__ __forceinline__ int rsub(int a, int b) { return a * (a + 1) / 2 + b; }
 constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X10 (2) + colb
@@ -548,11 +567,11 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     v4d acc[2][2];
     zero_acc(acc);
     for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
-    store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, lane);           // L_i0
-    store_acc_t(acc, A, ld, kBT * i + kT * qi, c0 + kT * qj, m, lane);
-    if (!two) return;
     __syncthreads();
-    acc_to_lds(acc, W + (2 * qi + qj) * kSub, lane);
+    acc_to_lds(acc, W + (2 * qi + qj) * kSub, lane);                        // L_i0
+    __syncthreads();
+    store64_both(W, A, ld, kBT * i, c0, m, tid);
+    if (!two) return;
     tile_regs_store(l10, XS, tid);
     __syncthreads();
     for (int kc = 0; kc < 2; ++kc) mfma_tile(cc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, -1.0, lane);
@@ -562,8 +581,10 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_p
     __syncthreads();
     zero_acc(acc);
     for (int kc = 0; kc <= qj; ++kc) mfma_tile(acc, W + (2 * qi + kc) * kSub, XS + (2 * qj + kc) * kSub, 1.0, lane);
-    store_acc(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, lane);     // L_i1
-    store_acc_t(acc, A, ld, kBT * i + kT * qi, c0 + kBT + kT * qj, m, lane);
+    __syncthreads();
+    acc_to_lds(acc, W + (2 * qi + qj) * kSub, lane);                        // L_i1
+    __syncthreads();
+    store64_both(W, A, ld, kBT * i, c0 + kBT, m, tid);
 }
 
 // ---------------------------------------------------------------- 128 x 128 trailing update
