@@ -63,7 +63,10 @@ struct TLaunch {
 // sync entries of a launch list (lookahead): kind 6 records tiled event `step` on stream `strm`,
 // kind 7 makes stream `strm` wait for it
 constexpr int kTlRecord = 6, kTlWait = 7;
-constexpr int kSuper = 2;               // regions (128 columns) per super step
+#ifndef DBSLMM_SUPER
+#define DBSLMM_SUPER 2
+#endif
+constexpr int kSuper = DBSLMM_SUPER;    // regions (128 columns) per super step
 constexpr int kGramSq = 4;              // 2D tile squares per XCD of the 256-tile Gram
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -155,7 +158,7 @@ struct dbslmm_plan {
     int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
     int32_t h2f_mode = 0;                    // dbslmm_options.h2f_mode
-    double cheb_tol = 1e-13;                 // dbslmm_options.cheb_tol
+    double cheb_tol = 1e-11;                 // dbslmm_options.cheb_tol
     bool trsv_pending = false;               // a persistent substitution ran since the last error check
     bool trsv_failed = false;                // ... and one of its hand-off waits gave up (sticky until the next run)
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (DBSLMM_DIAG) only
@@ -1076,8 +1079,9 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
             hi[j] = std::max(1.0, 1.0 + ext) * (1.0 + 1e-6);
             if (!(lo[j] > 0.0)) return false;
             // Chebyshev: error <= 2 q^K x the initial error x_c - x_b, itself <= |ext| relative
-            // (the same bound); K so that the final error is 1e-13 of the solution (below the
-            // forward error of the fp64 Cholesky solve itself; dbslmm_options.cheb_tol)
+            // (the same bound); K so that the final error is 1e-11 of the solution
+            // (dbslmm_options.cheb_tol; the BASELINE bar on beta is 1e-5 relative, and the
+            // reference's own PCG stops at an absolute residual of 1e-7)
             const double kap = hi[j] / lo[j], q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
             const double e0 = std::max(std::fabs(ext), 1e-300);
             const int k = q < 1e-300 ? 1 : std::max(1, static_cast<int>(std::ceil(std::log(tol / e0) / std::log(q))));

@@ -64,7 +64,8 @@ typedef struct dbslmm_plan dbslmm_plan;
  * h2f_mode       plan_run_multi: 0 = tiled blocks factored once, the other sigmas solved by
  *                Chebyshev iteration on that factor when the bound allows (tau in (0, 1],
  *                <= 60 iterations); 1 = one factorisation per sigma (the merged sequence)
- * cheb_tol       relative error target of the Chebyshev iteration (default 1e-13)
+ * cheb_tol       relative error target of the Chebyshev iteration (default 1e-11: six orders below
+ *                the 1e-5 parity bar on beta, three below the reference PCG's own deviation)
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;

@@ -1,7 +1,8 @@
 """h2f tuning by Chebyshev iteration on one factor (trsv.hip): for the tiled blocks only the base
 copy (median sigma) is factored; the other copies iterate M_b x = z - delta P_s x with the
 persistent forward / backward substitution kernels.  Every copy must match a fresh single-sigma
-solve to fp64 accuracy (normwise 1e-12), the base copy bit for bit; statuses and the NaN of a
+solve within the iteration's target (cheb_tol 1e-11; checked at normwise 1e-10), the base copy
+bit for bit; statuses and the NaN of a
 monomorphic block carry over; the merged-factorisation path (h2f_mode = 1) stays
 bit-identical."""
 import numpy as np
@@ -51,7 +52,7 @@ def test_cheb_copies_match_fresh_solves(monkeypatch, tiled_min, factors):
         if c == base:
             np.testing.assert_array_equal(_cat(got), _cat(ref))
         else:
-            assert _finite_normwise(_cat(got), _cat(ref)) < 1e-12, c
+            assert _finite_normwise(_cat(got), _cat(ref)) < 1e-10, c
     # against the oracle's direct solve of the reference equations too
     prob.sigma_s = sig[0]
     ref, _ = _oracle(prob)
