@@ -426,14 +426,17 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 
 // ------------------------------------------------------------------------------------------
 // Kernel 2c: the Gram of the big blocks (m >= 384), 256 x 256 output tile per 512-thread
-// workgroup: wave w computes rows 64 (w & 3) .., columns 128 (w >> 2) .. (2 x 4 MFMA 32x32x32
-// i8 tiles, 128 accumulator registers).  K runs in stages of 128 individuals: every thread loads
-// one row's 8 Gp dwords (32 B, four stages ahead in registers) and expands them to 128 B of int8
-// codes in a double-buffered LDS stage (a quarter of the HBM / L2 operand traffic of an int8
-// image), raw s_barrier per stage, 32 MFMAs per wave.  LDS rows are swizzled (swz) so that both
-// the expansion writes and the operand reads are bank-conflict free.  Diagonal tiles stage one operand; waves whose 64 x 128 piece is strictly upper
-// skip the MFMAs.  Missing-call blocks:
-// exact 4-product path per 32 x 32 sub-tile.
+// workgroup: every wave computes a 64 x 128 piece (2 x 4 MFMA 32x32x32 i8 tiles, 128 accumulator
+// registers); the two waves of a SIMD hold pieces in opposite halves of the tile.  K runs in
+// stages of 128 individuals: every thread loads one row's 8 Gp dwords (32 B, four stages ahead in
+// registers) and expands them to 128 B of int8 codes in a double-buffered LDS stage (a quarter of
+// the HBM / L2 operand traffic of an int8 image), raw s_barrier per stage, 32 MFMAs per wave.
+// LDS rows are swizzled (swz) so that both the expansion writes and the operand reads are
+// bank-conflict free.  Diagonal tiles stage one operand; MFMA tiles strictly above the diagonal
+// or wholly past m (edge tiles) are skipped (config 4: 6.7 -> 6.3 ms; skipping whole waves'
+// pieces only, without the per-MFMA branches, gained nothing; keeping the 2-bit codes in LDS and
+// expanding after the operand reads, a quarter of the LDS traffic, was slower: 6.7 ms).
+// Missing-call blocks: exact 4-product path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
 namespace gram {
 constexpr int kHT = 256;                   // output tile edge
@@ -483,8 +486,14 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     // writes and reads).  Loads run four stages ahead in four register sets.
     const int64_t kw = kpad / 16;
     const int sop = tid >> 8, srow = tid & 255;
-    const bool stager = !(diag && sop == 1);
-    const uint32_t* gs = Gp + static_cast<int64_t>(row0 + kHT * (sop ? tile.tj : tile.ti) + srow) * kw;
+    // ragged edge tiles: rows / columns of the tile inside the block (the last tile row / column
+    // of a block is partly padding).  Rows past them are not expanded into LDS and their loads
+    // re-read the last valid row (an L2 hit); the MFMAs that would only produce rows or columns
+    // past m are skipped, so an edge tile costs about its valid area.
+    const int rv = min(kHT, m - kHT * tile.ti), cv = min(kHT, m - kHT * tile.tj);
+    const int svalid = sop ? cv : rv;
+    const bool stager = !(diag && sop == 1) && srow < svalid;
+    const uint32_t* gs = Gp + static_cast<int64_t>(row0 + kHT * (sop ? tile.tj : tile.ti) + min(srow, svalid - 1)) * kw;
     const int nst = static_cast<int>(kpad / kHK);   // kpad is a multiple of 128
     // unconditional loads (clamped stage, valid rows for every thread) keep the vmcnt bookkeeping
     // exact: the newer loads in flight at every use are known
@@ -502,8 +511,21 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             *reinterpret_cast<v4i*>(slot + swz(srow, 4 + c)) = expand_dose(static_cast<uint32_t>(pk.hi[c]));
         }
     };
-    const int wr = wave & 3, wc = wave >> 2;       // rows 64 wr .., columns 128 wc ..
-    const bool idle = diag && 128 * wc >= 64 * wr + 64;
+    // wave -> piece: the two waves of a SIMD (w, w + 4) hold one row group in each half of the
+    // tile and opposite column halves, so the skipped MFMAs of an edge tile leave every SIMD with
+    // about the same work.  act: bit 4 i + j = MFMA tile (i, j) produces rows / columns < m and is
+    // not strictly above a diagonal tile's diagonal (32 x 32 granularity, as dbslmm_gram_i8)
+    const int hs = wave >> 2, sw = wave & 3;
+    const int wr = (sw & 1) + 2 * hs, wc = (sw >> 1) ^ hs;   // rows 64 wr .., columns 128 wc ..
+    uint32_t act = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ri = 64 * wr + 32 * i, cj = 128 * wc + 32 * j;
+            if (ri < rv && cj < cv && !(diag && cj >= ri + 32)) act |= 1u << (4 * i + j);
+        }
+    const bool idle = act == 0;
     v16i acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -528,7 +550,8 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
+                    if (act & (1u << (4 * i + j)))
+                        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
         }
     };
     // four register sets: the loads of stage st + 4 are issued while stage st is multiplied
@@ -561,6 +584,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         const double Sj = S[row0 + lj], rj = rsd[row0 + lj];
 #pragma unroll
         for (int si = 0; si < 2; ++si) {
+            if (!(act & (1u << (4 * si + sj)))) continue;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int li = kHT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
