@@ -142,6 +142,8 @@ struct dbslmm_plan {
     std::vector<int32_t> h_m;   // per non-empty block
     std::vector<int32_t> h_tb;  // blocks on the tiled path
     std::vector<int32_t> h_empty;  // original ids of empty blocks
+    void* h_pin = nullptr;         // pinned landing buffer of the result downloads
+    size_t h_pin_bytes = 0;
     std::vector<int32_t> h_slot_out;  // slot -> small index s, large -1-l, padding INT32_MIN
     double sigma_run = 0.0;        // sigma_s of the factorisation held in d_M
     // workload figures
@@ -248,6 +250,23 @@ static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_
         if (stage[b]) (void)hipHostFree(stage[b]);
     }
     return e != hipSuccess ? e : e2;
+}
+
+// memcpy on up to 8 host threads (a result download lands in pinned memory; the caller's arrays
+// are often fresh pages, so the page faults of the copy are spread over the threads too)
+static void par_memcpy(void* dst, const void* src, size_t n) {
+    constexpr size_t kMin = size_t(2) << 20;
+    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const unsigned nt = static_cast<unsigned>(std::min<size_t>(hw, std::max<size_t>(1, n / kMin)));
+    if (nt <= 1) { if (n) memcpy(dst, src, n); return; }
+    const size_t part = (n + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; ++t) {
+        const size_t a = t * part, z = std::min(n, a + part);
+        if (a < z) th.emplace_back([=] { memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, z - a); });
+    }
+    memcpy(dst, src, std::min(n, part));
+    for (auto& t : th) t.join();
 }
 
 // The .bed image on the device: a device-to-device copy of the context's cached image when the
@@ -531,6 +550,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
         return;
     }
     (void)hipSetDevice(p->ctx->device);
+    if (p->h_pin) (void)hipHostFree(p->h_pin);
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
@@ -1408,22 +1428,49 @@ static int check_trsv(dbslmm_plan* p) {
     return DBSLMM_OK;
 }
 
-static int download_copy(dbslmm_plan* p, int c, double* beta_s, double* beta_l, int32_t* block_status) {
+// Results of factorisation copies c0 .. c0 + n - 1 (each copy's betas / status contiguous on the
+// device and in the caller's arrays): one asynchronous copy per array into the plan's pinned
+// buffer, then a threaded copy out (pageable hipMemcpy of 8 MB arrays cost ~0.3 ms each).
+static int download_copies(dbslmm_plan* p, int c0, int n, double* beta_s, double* beta_l, int32_t* block_status) {
     dbslmm_ctx* ctx = p->ctx;
     if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (const int rc = check_trsv(p)) return rc;
-    if (beta_s && p->n_s)
-        HIP_TRY(ctx, hipMemcpy(beta_s, p->d_beta_s + c * p->n_s, p->n_s * sizeof(double), hipMemcpyDeviceToHost));
-    if (beta_l && p->n_l)
-        HIP_TRY(ctx, hipMemcpy(beta_l, p->d_beta_l + c * p->n_l, p->n_l * sizeof(double), hipMemcpyDeviceToHost));
-    if (block_status && p->num_block) {
-        HIP_TRY(ctx, hipMemcpy(block_status, p->d_status + c * p->nbk, p->num_block * sizeof(int32_t),
-                               hipMemcpyDeviceToHost));
-        for (int32_t b : p->h_empty) block_status[b] = DBSLMM_BLOCK_EMPTY;
+    const size_t nbs = beta_s ? static_cast<size_t>(n) * p->n_s : 0;
+    const size_t nbl = beta_l ? static_cast<size_t>(n) * p->n_l : 0;
+    const size_t nst = block_status && p->num_block ? static_cast<size_t>(n) * p->nbk : 0;
+    const size_t bytes = (nbs + nbl) * sizeof(double) + nst * sizeof(int32_t);
+    if (bytes == 0) return DBSLMM_OK;
+    if (bytes > p->h_pin_bytes) {
+        if (p->h_pin) HIP_TRY(ctx, hipHostFree(p->h_pin));
+        p->h_pin = nullptr;
+        p->h_pin_bytes = 0;
+        HIP_TRY(ctx, hipHostMalloc(&p->h_pin, bytes, hipHostMallocDefault));
+        p->h_pin_bytes = bytes;
+    }
+    double* ps = static_cast<double*>(p->h_pin);
+    double* pl = ps + nbs;
+    int32_t* pt = reinterpret_cast<int32_t*>(pl + nbl);
+    if (nbs) HIP_TRY(ctx, hipMemcpyAsync(ps, p->d_beta_s + static_cast<int64_t>(c0) * p->n_s, nbs * sizeof(double),
+                                         hipMemcpyDeviceToHost, ctx->stream));
+    if (nbl) HIP_TRY(ctx, hipMemcpyAsync(pl, p->d_beta_l + static_cast<int64_t>(c0) * p->n_l, nbl * sizeof(double),
+                                         hipMemcpyDeviceToHost, ctx->stream));
+    if (nst) HIP_TRY(ctx, hipMemcpyAsync(pt, p->d_status + c0 * p->nbk, nst * sizeof(int32_t),
+                                         hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (nbs) par_memcpy(beta_s, ps, nbs * sizeof(double));
+    if (nbl) par_memcpy(beta_l, pl, nbl * sizeof(double));
+    for (int c = 0; c < n && nst; ++c) {
+        int32_t* out = block_status + static_cast<int64_t>(c) * p->num_block;
+        memcpy(out, pt + c * p->nbk, p->num_block * sizeof(int32_t));
+        for (int32_t b : p->h_empty) out[b] = DBSLMM_BLOCK_EMPTY;
     }
     return DBSLMM_OK;
+}
+
+static int download_copy(dbslmm_plan* p, int c, double* beta_s, double* beta_l, int32_t* block_status) {
+    return download_copies(p, c, 1, beta_s, beta_l, block_status);
 }
 
 int dbslmm_plan_run(dbslmm_plan* p) {
@@ -1456,10 +1503,7 @@ int dbslmm_plan_run_multi(dbslmm_plan* p, const double* sigmas, int32_t n_sigma,
               "blocks x sigmas must stay below 32768 (packed work items)");
     int rc = run_impl(p, true, sigmas, n_sigma);
     if (!rc) rc = dbslmm_plan_sync(p);
-    for (int i = 0; i < n_sigma && !rc; ++i)
-        rc = download_copy(p, i, beta_s ? beta_s + static_cast<int64_t>(i) * p->n_s : nullptr,
-                           beta_l ? beta_l + static_cast<int64_t>(i) * p->n_l : nullptr,
-                           block_status ? block_status + static_cast<int64_t>(i) * p->num_block : nullptr);
+    if (!rc) rc = download_copies(p, 0, n_sigma, beta_s, beta_l, block_status);
     return rc;
 }
 
