@@ -95,7 +95,7 @@ class BlockProblem:
     z_l: np.ndarray | None = None
     tau: float = 0.8
     # dbslmm_options (path-selection thresholds; missing keys = the library defaults):
-    # tiled_min, gram_big_min, gram_huge_min, h2f_mode (0 auto / 1 merged), cheb_tol
+    # tiled_min, gram_big_min, gram_huge_min, h2f_mode (0 auto / 1 merged), cheb_tol, lead_min
     opts: dict = field(default_factory=dict)
 
     def __post_init__(self):

@@ -22,7 +22,7 @@ EXPORTS = (
     "dbslmm_ctx_cache_bed",
 )
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv")
@@ -34,7 +34,7 @@ class Options(C.Structure):
     """dbslmm_options: path-selection thresholds (0 = default)."""
     _fields_ = [
         ("tiled_min", C.c_int32), ("gram_big_min", C.c_int32), ("gram_huge_min", C.c_int32),
-        ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double),
+        ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double), ("lead_min", C.c_int32),
     ]
 
 

@@ -47,6 +47,7 @@ constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-
 constexpr int kTiledMinSmall = 256;     // the same when no block reaches kTiledMinDefault
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
+constexpr int kLeadMinDefault = 2048;    // lead group: m >= max(this, m_max / 2) (dbslmm_options.lead_min)
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
@@ -58,7 +59,7 @@ struct TLaunch {
     int32_t n;
     int32_t items;    // workgroups
     int32_t nk = 1;   // trailing: K = 128 nk (regions step .. step+nk-1); region: pending panels
-    int strm = 0;     // 0: the chain stream (stream2), 1: the bulk-trailing stream (stream3)
+    int strm = 0;     // 0: the sequence's chain stream, 1: its bulk-trailing stream
 };
 // sync entries of a launch list (lookahead): kind 6 records tiled event `step` on stream `strm`,
 // kind 7 makes stream `strm` wait for it
@@ -77,7 +78,10 @@ struct dbslmm_ctx {
     hipStream_t stream = nullptr;    // main stream (unpack, gram, large-block Cholesky)
     hipStream_t stream2 = nullptr;   // tiled (multi-workgroup) Cholesky sequence, forked/joined
     hipStream_t stream3 = nullptr;   // its bulk trailing updates (lookahead), forked/joined
-    hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
+    // a plan with a lead group (dbslmm_options.lead_min) factors it on stream2 / stream3 and the
+    // other tiled blocks on stream4 / stream5 (chain / bulk trailing), concurrently
+    hipStream_t stream4 = nullptr, stream5 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr, fork2 = nullptr, join4 = nullptr;
     int n_cu = 256;                  // compute units (persistent substitution grid)
     std::string err;
     // device copy of a caller's .bed image (dbslmm_ctx_cache_bed): bed_maf and plan_create on the
@@ -116,7 +120,8 @@ struct dbslmm_plan {
     int32_t n_large = 0, n_small = 0;   // Cholesky paths (ld > 64 / ld <= 64); d_order = [large | small]
     int32_t n_tiled = 0;                // blocks on the multi-workgroup path (not in d_order)
     int32_t* d_tlist = nullptr;         // work lists of the tiled sequence
-    std::vector<TLaunch> tl;
+    std::vector<TLaunch> tl;            // the tiled sequence (of the lead group when there is one)
+    std::vector<TLaunch> tl_rest;       // the other tiled blocks' sequence (lead group only)
     hipGraphExec_t graph_exec = nullptr;   // captured tiled sequence
     int32_t *d_row0 = nullptr, *d_m = nullptr, *d_ms = nullptr, *d_ld = nullptr;
     int64_t* d_matoff = nullptr;
@@ -125,6 +130,7 @@ struct dbslmm_plan {
     int32_t n_btiles = 0;
     GramTile* d_htiles = nullptr;      // 256 x 256 tiles of the big blocks, per-XCD queues
     int32_t n_htiles = 0;
+    int32_t n_htiles_lead = 0;         // ... of which the first n_htiles_lead are the lead group's
     double* d_M = nullptr;
     double *d_beta_s = nullptr, *d_beta_l = nullptr;
     double* d_dshift = nullptr;        // 1/(sigma_s n), read by the solve kernels
@@ -152,6 +158,7 @@ struct dbslmm_plan {
     bool timing = false;
     std::vector<hipEvent_t> ev;  // kEvPerRun per run
     std::vector<hipEvent_t> tev; // dependencies between the tiled sequence's two streams
+    std::vector<hipEvent_t> tev_rest;   // ... of the rest sequence
     // h2f tuning by Chebyshev on one factor (trsv.hip): tile work lists of the tiled blocks in
     // forward / backward dependency order, tile flags (+ ticket counter, error word) and the
     // iteration vectors [Y, Z, X, R, D, S] x kMaxR x n_slots
@@ -169,6 +176,7 @@ struct dbslmm_plan {
     int32_t coef_cap = 0;
     std::vector<double> h_coef;              // the coefficients in d_coef
     std::vector<hipGraphExec_t> graph_copy;  // the single-copy tiled sequence on copy c
+    std::vector<hipGraphExec_t> graph_rest;  // ... and the rest sequence (lead group)
     int32_t cheb_base = -1;                  // base copy of the last Chebyshev run (-1: none)
     bool cheb_pending_var = false;           // copy var_copy's tiled blocks are not factored yet
     int runs_pending = 0;
@@ -476,7 +484,11 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join4, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
@@ -516,6 +528,10 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
+    if (ctx->stream4) (void)hipStreamDestroy(ctx->stream4);
+    if (ctx->stream5) (void)hipStreamDestroy(ctx->stream5);
+    if (ctx->fork2) (void)hipEventDestroy(ctx->fork2);
+    if (ctx->join4) (void)hipEventDestroy(ctx->join4);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->join3) (void)hipEventDestroy(ctx->join3);
@@ -561,9 +577,12 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : p->tev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : p->tev_rest) (void)hipEventDestroy(e);
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
     if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
     for (hipGraphExec_t g : p->graph_copy)
+        if (g) (void)hipGraphExecDestroy(g);
+    for (hipGraphExec_t g : p->graph_rest)
         if (g) (void)hipGraphExecDestroy(g);
     delete p;
 }
@@ -609,8 +628,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     // the 256-tile kernel pays once its K loop outweighs its 512 KB fp64 epilogue per tile
     const int64_t gram_huge_min = op.gram_huge_min > 0 ? op.gram_huge_min
                                   : p->kpad >= 4096 ? kGramHugeMinDefault : 2 * kGramHugeMinDefault;
-    std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd);
-    std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0);
+    std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd), lq(kXcd);
+    std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0), lload(kXcd, 0.0);
     int64_t moff = 0;
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
@@ -628,6 +647,25 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         if (mmax < kTiledMinDefault) tiled_min = kTiledMinSmall;
     }
     p->tiled_min = static_cast<int32_t>(std::min<int64_t>(tiled_min, INT32_MAX));
+    // lead group: the tiled blocks with the longest factorisation chains (m >= lead_min); their
+    // Gram tiles form the first 256-tile launch and their sequence starts right after it
+    int64_t lead_min = INT64_MAX;
+    {
+        int64_t mmax = 0, n_lead = 0, n_rest = 0;
+        for (int b = 0; b < pr->num_block; ++b)
+            mmax = std::max<int64_t>(mmax, pr->s_ptr[b + 1] - pr->s_ptr[b] +
+                                               (has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0));
+        if (op.lead_min >= 0) {
+            lead_min = op.lead_min > 0 ? op.lead_min : std::max<int64_t>(kLeadMinDefault, mmax / 2);
+            lead_min = std::max({lead_min, tiled_min, gram_huge_min});
+            for (int b = 0; b < pr->num_block; ++b) {
+                const int64_t m = pr->s_ptr[b + 1] - pr->s_ptr[b] + (has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0);
+                if (m >= lead_min) ++n_lead;
+                else if (m >= tiled_min) ++n_rest;
+            }
+            if (n_lead == 0 || n_rest == 0) lead_min = INT64_MAX;   // nothing to overlap
+        }
+    }
     std::vector<char> is_tiled;
     for (int b = 0; b < pr->num_block; ++b) {
         const int64_t s0 = pr->s_ptr[b], ms = pr->s_ptr[b + 1] - s0;
@@ -676,15 +714,17 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         }
         if (m >= gram_huge_min) {   // 256 x 256 tiles
             const int T = static_cast<int>((m + gram::kHT - 1) / gram::kHT);
+            auto& q = m >= lead_min ? lq : hq;
+            auto& ld_ = m >= lead_min ? lload : hload;
             // squares of kGramSq x kGramSq tiles (lower triangle), each on the least-loaded XCD:
             // the workgroups in flight on an XCD share kGramSq row panels of each operand
             for (int si = 0; si < T; si += kGramSq)
                 for (int sj = 0; sj <= si; sj += kGramSq) {
-                    const int x = static_cast<int>(std::min_element(hload.begin(), hload.end()) - hload.begin());
+                    const int x = static_cast<int>(std::min_element(ld_.begin(), ld_.end()) - ld_.begin());
                     for (int ti = si; ti < std::min(T, si + kGramSq); ++ti)
                         for (int tj = sj; tj < std::min(ti + 1, sj + kGramSq); ++tj) {
-                            hq[x].push_back({nb, ti, tj, 0});
-                            hload[x] += 1;
+                            q[x].push_back({nb, ti, tj, 0});
+                            ld_[x] += 1;
                         }
                 }
             ops_exec += 2.0 * p->kpad * gram::kHT * gram::kHT * (T * (T + 1) / 2);
@@ -718,15 +758,17 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             for (size_t i = 0; i < xq[x].size(); ++i) btiles[i * kXcd + x] = xq[x][i];
         p->n_btiles = static_cast<int32_t>(btiles.size());
     }
-    std::vector<GramTile> htiles;
-    {
+    std::vector<GramTile> htiles;   // [lead group's queues | the others'], entry e on XCD e % 8
+    for (const auto* qs : {&lq, &hq}) {
         size_t qmax = 0;
-        for (const auto& q : hq) qmax = std::max(qmax, q.size());
-        htiles.assign(qmax * kXcd, GramTile{-1, 0, 0, 0});
+        for (const auto& q : *qs) qmax = std::max(qmax, q.size());
+        const size_t base = htiles.size();
+        htiles.resize(base + qmax * kXcd, GramTile{-1, 0, 0, 0});
         for (int x = 0; x < kXcd; ++x)
-            for (size_t i = 0; i < hq[x].size(); ++i) htiles[i * kXcd + x] = hq[x][i];
-        p->n_htiles = static_cast<int32_t>(htiles.size());
+            for (size_t i = 0; i < (*qs)[x].size(); ++i) htiles[base + i * kXcd + x] = (*qs)[x][i];
+        if (qs == &lq) p->n_htiles_lead = static_cast<int32_t>(htiles.size());
     }
+    p->n_htiles = static_cast<int32_t>(htiles.size());
     p->M_elems = moff;
     p->h_ld = ldv;
     // Cholesky work lists: large blocks (ld > 64, one workgroup each) then small blocks (one
@@ -739,13 +781,21 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
     std::vector<int32_t> tlist;
     {
-        std::vector<int32_t> tb;
+        std::vector<int32_t> tb, tb_lead, tb_rest;
         for (int b = 0; b < p->n_nonempty; ++b)
-            if (is_tiled[b]) tb.push_back(b);
+            if (is_tiled[b]) {
+                tb.push_back(b);
+                (mv[b] >= lead_min ? tb_lead : tb_rest).push_back(b);
+            }
         p->n_tiled = static_cast<int32_t>(tb.size());
         p->h_m = mv;
         p->h_tb = tb;
-        build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist);
+        if (tb_lead.empty()) {
+            build_tiled(mv, tb, 1, p->n_nonempty, p->tl, tlist);
+        } else {
+            build_tiled(mv, tb_lead, 1, p->n_nonempty, p->tl, tlist);
+            build_tiled(mv, tb_rest, 1, p->n_nonempty, p->tl_rest, tlist);
+        }
     }
     // substitution work lists (trsv.hip): 64-row tiles of the tiled blocks; forward in order of
     // (tile, block), backward in order of (tiles from the end, block) -- every dependency of an
@@ -804,6 +854,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->wl[10] = chol_flops_tiled;
     p->wl[11] = p->n_tiled;
     p->wl[12] = static_cast<double>(std::count_if(p->tl.begin(), p->tl.end(),
+                                                  [](const TLaunch& L) { return L.kind < kTlRecord; }) +
+                                    std::count_if(p->tl_rest.begin(), p->tl_rest.end(),
                                                   [](const TLaunch& L) { return L.kind < kTlRecord; }));
     p->wl[14] = 0;
     p->wl[15] = -1;
@@ -897,11 +949,20 @@ static int collect_timing(dbslmm_plan* p) {
     return DBSLMM_OK;
 }
 
-// Enqueue a tiled launch list on stream2.
+// The stream pair and event set of a tiled sequence: the lead / only sequence runs on stream2
+// (chain, high priority) + stream3 (bulk trailing), the rest sequence on stream4 + stream5.
+struct TSeq {
+    hipStream_t chain, bulk;
+    std::vector<hipEvent_t>* tev;
+};
+static TSeq seq_main(dbslmm_plan* p) { return TSeq{p->ctx->stream2, p->ctx->stream3, &p->tev}; }
+static TSeq seq_rest(dbslmm_plan* p) { return TSeq{p->ctx->stream4, p->ctx->stream5, &p->tev_rest}; }
+
+// Enqueue a tiled launch list on its stream pair.
 // copy: the list is a single-copy list applied to factorisation copy `copy` (its matrix, sigma
 // scalar, scratch, betas and status); multi-copy lists address the copies themselves (copy 0).
 static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist,
-                         int copy = 0) {
+                         int copy, const TSeq& sq) {
     dbslmm_ctx* ctx = p->ctx;
     const int64_t c = copy;
     const chol::TiledArgs ta{p->d_M + c * p->M_elems, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff,
@@ -912,15 +973,16 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
     int nev = 0;
     for (const TLaunch& L : tl)
         if (L.kind == kTlRecord) nev = std::max(nev, L.step + 1);
-    while (static_cast<int>(p->tev.size()) < nev) {
+    std::vector<hipEvent_t>& tev = *sq.tev;
+    while (static_cast<int>(tev.size()) < nev) {
         hipEvent_t e;
         HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        p->tev.push_back(e);
+        tev.push_back(e);
     }
     for (const TLaunch& L : tl) {
-        hipStream_t st = L.strm ? ctx->stream3 : ctx->stream2;
-        if (L.kind == kTlRecord) { HIP_TRY(ctx, hipEventRecord(p->tev[L.step], st)); continue; }
-        if (L.kind == kTlWait) { HIP_TRY(ctx, hipStreamWaitEvent(st, p->tev[L.step], 0)); continue; }
+        hipStream_t st = L.strm ? sq.bulk : sq.chain;
+        if (L.kind == kTlRecord) { HIP_TRY(ctx, hipEventRecord(tev[L.step], st)); continue; }
+        if (L.kind == kTlWait) { HIP_TRY(ctx, hipStreamWaitEvent(st, tev[L.step], 0)); continue; }
         if (L.items == 0) continue;
         const int32_t* act = d_tlist + L.off;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
@@ -958,6 +1020,8 @@ static int ensure_copies(dbslmm_plan* p, int n) {
     if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
     p->graph_exec = p->graph_multi = nullptr;
     for (hipGraphExec_t& g : p->graph_copy)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    for (hipGraphExec_t& g : p->graph_rest)
         if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
     return DBSLMM_OK;
 }
@@ -1032,16 +1096,16 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     return DBSLMM_OK;
 }
 
-// Capture a launch list into a graph on stream2 (once; sigma is read from device scalars, so the
-// graph stays valid) and replay it.
+// Capture a launch list into a graph on its chain stream (once; sigma is read from device scalars,
+// so the graph stays valid) and replay it.
 static int launch_graph(dbslmm_plan* p, double isn, const std::vector<TLaunch>& tl, const int32_t* d_tlist,
-                        int copy, hipGraphExec_t& gx) {
+                        int copy, hipGraphExec_t& gx, const TSeq& sq) {
     dbslmm_ctx* ctx = p->ctx;
     if (!gx) {
         hipGraph_t gr = nullptr;
-        HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream2, hipStreamCaptureModeThreadLocal));
-        const int rc = enqueue_tiled(p, isn, tl, d_tlist, copy);
-        hipError_t ce = hipStreamEndCapture(ctx->stream2, &gr);
+        HIP_TRY(ctx, hipStreamBeginCapture(sq.chain, hipStreamCaptureModeThreadLocal));
+        const int rc = enqueue_tiled(p, isn, tl, d_tlist, copy, sq);
+        hipError_t ce = hipStreamEndCapture(sq.chain, &gr);
         if (rc != DBSLMM_OK) {
             if (gr) (void)hipGraphDestroy(gr);
             return rc;
@@ -1051,16 +1115,25 @@ static int launch_graph(dbslmm_plan* p, double isn, const std::vector<TLaunch>& 
         (void)hipGraphDestroy(gr);
         HIP_TRY(ctx, ie);
     }
-    HIP_TRY(ctx, hipGraphLaunch(gx, ctx->stream2));
+    HIP_TRY(ctx, hipGraphLaunch(gx, sq.chain));
     return DBSLMM_OK;
 }
 
-// The single-copy tiled sequence on factorisation copy `copy` (stream2, one graph per copy),
-// then its backward substitution as one persistent launch (run_pbwd).
+// The single-copy tiled sequence on factorisation copy `copy` (stream2, one graph per copy).
+// With a lead group this is the lead group's sequence; the rest sequence (run_rest_copy) runs on
+// stream4 and stream2 waits for it before the backward substitution (run_pbwd).
 static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
     if (static_cast<int>(p->graph_copy.size()) <= copy) p->graph_copy.resize(copy + 1, nullptr);
-    const int rc = launch_graph(p, isn, p->tl, p->d_tlist, copy, p->graph_copy[copy]);
-    return rc != DBSLMM_OK ? rc : run_pbwd(p, isn, copy, tgroup_all(p));
+    return launch_graph(p, isn, p->tl, p->d_tlist, copy, p->graph_copy[copy], seq_main(p));
+}
+static int run_rest_copy(dbslmm_plan* p, double isn, int copy) {
+    if (static_cast<int>(p->graph_rest.size()) <= copy) p->graph_rest.resize(copy + 1, nullptr);
+    dbslmm_ctx* ctx = p->ctx;
+    const int rc = launch_graph(p, isn, p->tl_rest, p->d_tlist, copy, p->graph_rest[copy], seq_rest(p));
+    if (rc != DBSLMM_OK) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->join4, ctx->stream4));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->join4, 0));
+    return DBSLMM_OK;
 }
 
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
@@ -1291,6 +1364,40 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         HIP_TRY(ctx, hipGetLastError());
     }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], s));
+    if (!front && n > 1)
+        return (ctx->err = "a multi-copy run needs the Gram front", DBSLMM_E_STATE);
+    const std::vector<TLaunch>& tl = n > 1 && !cheb ? p->tl_multi : p->tl;
+    // lead group (plan_create): the single-copy sequence is split in two -- the lead blocks'
+    // sequence starts on stream2 right after their Gram tiles, the rest on stream4 after the
+    // whole Gram; stream2 waits for the rest before the substitutions
+    const bool lead = !p->tl_rest.empty() && (n == 1 || cheb);
+    const int fcopy = cheb ? cp.base : 0;   // the copy the single-copy sequence factors
+    const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
+    if (p->n_nonempty > 0) {
+        for (int c = 0; c < n; ++c) {
+            const double dshift = 1.0 / (sigmas[c] * static_cast<double>(p->n_obs));
+            hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift + c, dshift);
+        }
+        if (cheb) {
+            const int rc = cheb_prepare(p, cp, s);
+            if (rc != DBSLMM_OK) return rc;
+        }
+    }
+    auto gram_huge = [&](int32_t t0, int32_t nt) {
+        hipLaunchKernelGGL(dbslmm_gram_huge, dim3(nt), dim3(512), gram::kHLdsBytes, s, p->d_G,
+                           p->kpad, p->d_htiles + t0, nt, p->d_row0, p->d_m, p->d_ld,
+                           p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
+                           static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
+                           p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
+    };
+    if (front && p->n_htiles_lead > 0) {
+        gram_huge(0, p->n_htiles_lead);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    // the lead sequence (stream2, high priority: the critical path) waits for this point of the
+    // main stream; its graph is launched after every main-stream kernel is enqueued (a graph
+    // launch of a few hundred nodes keeps the host busy for milliseconds)
+    if (lead) HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
     if (front && p->n_tiles > 0) {
         dim3 grid((p->n_tiles + 3) / 4);
         hipLaunchKernelGGL(dbslmm_gram_i8, grid, dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
@@ -1300,12 +1407,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->tiled_min, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
-    if (front && p->n_htiles > 0) {
-        hipLaunchKernelGGL(dbslmm_gram_huge, dim3(p->n_htiles), dim3(512), gram::kHLdsBytes, s, p->d_G,
-                           p->kpad, p->d_htiles, p->n_htiles, p->d_row0, p->d_m, p->d_ld,
-                           p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
-                           static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
+    if (front && p->n_htiles > p->n_htiles_lead) {
+        gram_huge(p->n_htiles_lead, p->n_htiles - p->n_htiles_lead);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_btiles > 0) {
@@ -1316,24 +1419,13 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
-    if (!front && n > 1)
-        return (ctx->err = "a multi-copy run needs the Gram front", DBSLMM_E_STATE);
     // (the factorisation overwrites its matrix: the Gram epilogues write all n copies)
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
     if (p->n_nonempty > 0) {
-        for (int c = 0; c < n; ++c) {
-            const double dshift = 1.0 / (sigmas[c] * static_cast<double>(p->n_obs));
-            hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift + c, dshift);
-        }
-        const double isn = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
-        if (cheb) {
-            const int rc = cheb_prepare(p, cp, s);
-            if (rc != DBSLMM_OK) return rc;
-        }
-        // fork: the tiled sequence runs on stream2 (high priority: the critical path) while the
-        // single-workgroup and single-wave kernels run on the main stream.
-        HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
-        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+        // fork: the tiled sequence (or, with a lead group, the rest sequence on stream4) runs
+        // beside the single-workgroup and single-wave kernels of the main stream
+        HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
         for (int c = 0; c < n && p->n_large > 0; ++c) {
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M + c * p->M_elems, p->d_order, p->n_large,
@@ -1346,7 +1438,6 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
         // single-wave blocks: concurrently on stream2 when there is no tiled sequence, else
         // behind the single-workgroup kernel (each stream keeps its own hardware queue)
-        const std::vector<TLaunch>& tl = n > 1 && !cheb ? p->tl_multi : p->tl;
         hipStream_t ss = tl.empty() ? ctx->stream2 : s;
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ss));
         for (int c = 0; c < n && p->n_small > 0; ++c) {
@@ -1360,23 +1451,31 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[5], ss));
         if (ss != s) HIP_TRY(ctx, hipEventRecord(ctx->join, ss));
-        if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
+        if (lead) {
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+            if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
+            int rc = run_tiled_copy(p, isn, fcopy);
+            if (rc == DBSLMM_OK) rc = run_rest_copy(p, isn, fcopy);
+            if (rc != DBSLMM_OK) return rc;
+        } else if (ev) {
+            HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
+        }
         if (!tl.empty()) {
             // the tiled sequence (~2.5 launches per 128 columns) is replayed from a graph
             // captured on first use (sigma is read from device scalars, so it stays valid)
-            if (n == 1) {
-                const int rc = run_tiled_copy(p, isn, 0);
-                if (rc != DBSLMM_OK) return rc;
-            } else if (cheb) {
+            if (n == 1 || cheb) {
                 // h2f: factor only the base copy, iterate the others on its factor
-                int rc = run_tiled_copy(p, isn, cp.base);
+                int rc = lead ? DBSLMM_OK : run_tiled_copy(p, isn, fcopy);
+                if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, tgroup_all(p));
                 if (rc != DBSLMM_OK) return rc;
-                if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
-                rc = run_cheb(p, isn, cp, tgroup_all(p));
-                if (rc != DBSLMM_OK) return rc;
+                if (cheb) {
+                    if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                    rc = run_cheb(p, isn, cp, tgroup_all(p));
+                    if (rc != DBSLMM_OK) return rc;
+                }
             } else {
                 // merged copies: one sequence factors every copy, then one backward launch each
-                int rc = launch_graph(p, isn, tl, p->d_tlist_multi, 0, p->graph_multi);
+                int rc = launch_graph(p, isn, tl, p->d_tlist_multi, 0, p->graph_multi, seq_main(p));
                 for (int c = 0; c < n && rc == DBSLMM_OK; ++c) rc = run_pbwd(p, isn, c, tgroup_all(p));
                 if (rc != DBSLMM_OK) return rc;
             }

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 6
+#define DBSLMM_ABI_VERSION 7
 
 enum {
     DBSLMM_OK = 0,
@@ -66,6 +66,11 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                <= 60 iterations); 1 = one factorisation per sigma (the merged sequence)
  * cheb_tol       relative error target of the Chebyshev iteration (default 1e-11: six orders below
  *                the 1e-5 parity bar on beta, three below the reference PCG's own deviation)
+ * lead_min       tiled blocks with m >= lead_min form the lead group: their Gram tiles run first
+ *                and their factorisation (the longest dependency chains) starts right after
+ *                them, beside the rest of the Gram and the other blocks' factorisation (default
+ *                max(2048, m_max / 2) when tiled blocks lie on both sides of it; < 0: no lead
+ *                group).  Scheduling only: the results are bit-identical either way.
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -73,6 +78,7 @@ typedef struct dbslmm_options {
     int32_t gram_huge_min;
     int32_t h2f_mode;
     double cheb_tol;
+    int32_t lead_min;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.

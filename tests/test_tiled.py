@@ -162,3 +162,31 @@ def test_run_multi_merged_copies_bit_identical(monkeypatch, tiled_min):
     plan.set_sigma(sig[0])
     plan.run()
     np.testing.assert_array_equal(plan.download()[0], multi[0][0])
+
+
+def test_lead_group_bit_identical():
+    """The lead group (dbslmm_options.lead_min: the biggest tiled blocks' Gram tiles first, their
+    sequence on its own streams beside the rest of the Gram and the other blocks' sequence) only
+    reorders work: single solves and h2f runs give the same betas bit for bit as one sequence."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=13)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    res = {}
+    for lead in (600, -1):
+        prob.opts.update(tiled_min=128, gram_huge_min=384, lead_min=lead)
+        plan = Plan(Context(0), prob)
+        plan.run()
+        one = plan.download()
+        multi = plan.run_multi(sig)
+        plan.run()
+        again = plan.download()
+        res[lead] = (one, multi, again)
+    (one, multi, again), (one0, multi0, _) = res[600], res[-1]
+    for x, y in zip(one, one0):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(again, one0):
+        np.testing.assert_array_equal(x, y)
+    for c in range(3):
+        for x, y in zip(multi[c], multi0[c]):
+            np.testing.assert_array_equal(x, y)
+    assert np.all(one[2] == 0)
