@@ -68,6 +68,8 @@ constexpr int kTlRecord = 6, kTlWait = 7;
 #define DBSLMM_SUPER 2
 #endif
 constexpr int kSuper = DBSLMM_SUPER;    // regions (128 columns) per super step
+constexpr int kWideSuper = 4;           // ... for blocks of m >= kWideMin (half the C traffic per
+constexpr int kWideMin = 4096;          //     flop; config 4 lead group 52.5 -> 51.8 ms/step)
 constexpr int kGramSq = 4;              // 2D tile squares per XCD of the 256-tile Gram
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -301,8 +303,9 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 
 // Launch list of the tiled sequence for the blocks `tb0` (plan block indices), each replicated over
 // `copies` independent factorisations (h2f tuning: item block id bq = b + c * nb addresses copy c).
-// A block's factorisation is a chain of super steps of R regions (128 columns each; R = 2, env
-// DBSLMM_SUPER): region(0), then per super step
+// A block's factorisation is a chain of super steps of R regions (128 columns each; R = 4 for
+// blocks of m >= kWideMin, else 2 -- a property of the block, so its factorisation does not
+// depend on the other blocks of the sequence): region(0), then per super step
 //   panel(r0) -> for r = r0+1 .. r0+R-1: region(r) [+ its pending update from panels r0 .. r-1]
 //   -> panel(r) [+ the pending update of its rows' region-r columns] -> trailing K = 128 R of
 //   everything right of the super step (the next first region included) -> region(r0 + R),
@@ -314,8 +317,8 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 // [block / tile, (local step << 8) | pending panels or K multiple].
 static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
                         int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
-    struct Blk { int32_t bq; int T64, Tz64, T2, Tz2, nr, S, off; };
-    constexpr int R = kSuper;
+    struct Blk { int32_t bq; int T64, Tz64, T2, Tz2, nr, R, S, off; };
+    int Rmax = 1;
     const int run2 = chol::kRun2;
     std::vector<Blk> bl;
     int G = 0, Kmax = 0;
@@ -328,7 +331,9 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             k.T2 = (mv[b] + 127) / 128;
             k.Tz2 = mv[b] / 128;
             k.nr = (k.T64 + 1) / 2;
-            k.S = (k.nr + R - 1) / R;
+            k.R = mv[b] >= kWideMin ? kWideSuper : kSuper;
+            Rmax = std::max(Rmax, k.R);
+            k.S = (k.nr + k.R - 1) / k.R;
             G = std::max(G, k.S);
             Kmax = std::max(Kmax, k.T64);
             bl.push_back(k);
@@ -378,15 +383,15 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
         std::vector<int32_t> v;
         for (const auto& k : bl)      // panel(r0)
             if (active(k)) {
-                const int r0 = (g - k.off) * R;
+                const int r0 = (g - k.off) * k.R;
                 for (int i = 2 * r0 + 2; i <= k.Tz64; ++i) { v.push_back((k.bq << 16) | (i << 8)); v.push_back(r0 << 8); }
             }
         panel_launch(v);
-        for (int j = 1; j < R; ++j) {
+        for (int j = 1; j < Rmax; ++j) {
             std::vector<int32_t> rv, pv;
             for (const auto& k : bl)
-                if (active(k)) {
-                    const int r = (g - k.off) * R + j;
+                if (active(k) && j < k.R) {
+                    const int r = (g - k.off) * k.R + j;
                     if (r >= k.nr) continue;
                     rv.push_back(k.bq);
                     rv.push_back((r << 8) | j);
@@ -395,16 +400,17 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             region_launch(rv);
             panel_launch(pv);
         }
-        // trailing: 128 x 128 tiles (I, J) right of the super step, rl + jlo <= J <= rl + jhi, LPT
-        // over per-XCD queues by tile row
-        auto trailing = [&](int jlo, int jhi, int strm, int run_force) {
+        // trailing: 128 x 128 tiles (I, J) right of the super step, rl + jlo <= J <= rl + jhi (near:
+        // the block's next R columns, far: the rest), LPT over per-XCD queues by tile row
+        auto trailing = [&](bool near, int strm, int run_force) {
             std::vector<std::vector<int32_t>> q(kXcd);
             std::vector<int64_t> load(kXcd, 0);
             int64_t ntiles = 0;
             for (const auto& k : bl)
                 if (active(k)) {
-                    const int r0 = (g - k.off) * R, rl = std::min(r0 + R, k.nr) - 1;
+                    const int r0 = (g - k.off) * k.R, rl = std::min(r0 + k.R, k.nr) - 1;
                     if (rl + 1 >= k.nr) continue;
+                    const int jlo = near ? 1 : k.R + 1, jhi = near ? k.R : 1 << 20;
                     for (int I = rl + jlo; I <= k.Tz2; ++I) {
                         const int jm = std::min(std::min(I, k.T2 - 1), rl + jhi);
                         if (jm >= rl + jlo) ntiles += jm - (rl + jlo) + 1;
@@ -413,8 +419,9 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
             const int run = run_force ? run_force : (ntiles >= 1024 ? run2 : 1);
             for (const auto& k : bl)
                 if (active(k)) {
-                    const int r0 = (g - k.off) * R, rl = std::min(r0 + R, k.nr) - 1;
+                    const int r0 = (g - k.off) * k.R, rl = std::min(r0 + k.R, k.nr) - 1;
                     if (rl + 1 >= k.nr) continue;
+                    const int jlo = near ? 1 : k.R + 1, jhi = near ? k.R : 1 << 20;
                     const int meta = (r0 << 8) | (rl - r0 + 1);
                     for (int I = rl + jlo; I <= k.Tz2; ++I) {
                         const int jm = std::min(std::min(I, k.T2 - 1), rl + jhi);
@@ -434,15 +441,15 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
         // regions and panels.  Tiles of near(g) were far(g-1)'s.
         sync(kTlRecord, 2 * g, 0);
         if (g > 0) sync(kTlWait, 2 * g - 1, 0);
-        trailing(1, R, 0, 1);
+        trailing(true, 0, 1);
         sync(kTlWait, 2 * g, 1);
-        trailing(R + 1, 1 << 20, 1, 0);
+        trailing(false, 1, 0);
         sync(kTlRecord, 2 * g + 1, 1);
         {   // next super step's first region; region 0 of the blocks that start at g + 1
             std::vector<int32_t> v;
             for (const auto& k : bl) {
                 if (active(k)) {
-                    const int r0 = (g - k.off) * R, rn = r0 + R;
+                    const int r0 = (g - k.off) * k.R, rn = r0 + k.R;
                     if (rn < k.nr) { v.push_back(k.bq); v.push_back(rn << 8); }
                 } else if (k.off == g + 1) {
                     v.push_back(k.bq);

@@ -12,7 +12,7 @@ from _common import normwise
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [128, 129, 159, 160, 161, 191, 192, 575, 640, 703, 1000]
+SIZES = [128, 129, 159, 160, 161, 191, 192, 575, 640, 703, 1000, 4100]   # 4100: 512-column super steps
 
 
 def _problem(seed=11, n_ref=256, with_large=True, mono_block=None):
