@@ -48,26 +48,22 @@ int main(int argc, char** argv) {
                        d_dbl, d_dbl, 1.0, d_dbl, d_dbl, d_dbl, d_i32 + 5, 1, 0, 0, 0, 0, 0};
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
                            hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(double) * chol::kTrail3Doubles));
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing2),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(double) * chol::kTrail2Doubles));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 1; k < 2; ++k) {   // (k = 0 held a measured-and-dropped variant)
         for (int w = 0; w < 2; ++w)
             if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, (int)items.size() / 2);
-            else hipLaunchKernelGGL(dbslmm_tchol_trailing2, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail2Doubles, 0, ta, run, d_items, (int)items.size() / 2);
         CK(hipEventRecord(e0));
         const int reps = 5;
         for (int r = 0; r < reps; ++r)
             if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, (int)items.size() / 2);
-            else hipLaunchKernelGGL(dbslmm_tchol_trailing2, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail2Doubles, 0, ta, run, d_items, (int)items.size() / 2);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
-        printf("%s m=%d nk=%d run=%d items=%zu  %.3f ms  %.1f TF/s (%.1f%% of 78.6)\n", k ? "trailing3(dma)" : "trailing2(regs)",
+        printf("%s m=%d nk=%d run=%d items=%zu  %.3f ms  %.1f TF/s (%.1f%% of 78.6)\n", "trailing3",
                m, nk, run, items.size() / 2, ms, flops / ms * 1e-9, flops / ms * 1e-9 / 78.6 * 100);
     }
     return 0;
