@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="dbslmm_options field (path thresholds; experiments), repeatable")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the untimed lead-group-off run that times the Gram without overlap")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end leg (PLINK files in page cache -> the dbslmm CLI -> <eff>.txt)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host threads (OMP_NUM_THREADS, else the affinity mask)")
@@ -114,7 +116,8 @@ def kernel_roofline(name, ms, wl, n_solve=1):
     return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_F64_TFLOPS, unit="TFLOP/s",
                 frac=a / PEAK_F64_TFLOPS, algorithmic=fl, ms=ms,
                 note="fp64 flops sum_b m^3/3 + 2m^2 over its blocks vs the fp64 MFMA peak"
-                     + ("; multi-workgroup sequence, %d launches" % wl["tiled_launches"]
+                     + ("; multi-workgroup sequence, %d launches; wall span from the first tiled launch (the "
+                        "lead group's sequence starts during the Gram and overlaps it)" % wl["tiled_launches"]
                         if name == "dbslmm_tchol" else "; latency-bound (sequential column chain)"))
 
 
@@ -435,6 +438,26 @@ def main():
 
     n_solve = len(sigmas) if sigmas else 1
     kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl, n_solve) for k in range(len(KERNEL_NAMES))]
+    if world == 1 and not args.no_isolated:
+        # The lead group's factorisation overlaps the rest of the Gram, so the Gram's span above
+        # includes that contention.  One untimed plan with the lead group off times the Gram
+        # launches alone (outside the timed region; reported beside the span, never as `value`).
+        import dataclasses
+        iso = Plan(ctx, dataclasses.replace(prob, opts=dict(prob.opts, lead_min=-1)))
+        run_iso = (lambda: iso.run_multi(sigmas)) if sigmas else iso.run
+        run_iso()
+        iso.sync()
+        iso.enable_timing(True)
+        for _ in range(3):
+            run_iso()
+        iso.sync()
+        iso_ms, iso_n = iso.kernel_ms()
+        del iso
+        gi = KERNEL_NAMES.index("dbslmm_gram_i8")
+        alone = kernel_roofline(KERNEL_NAMES[gi], float(iso_ms[gi]) * iso_n / 3, wl, n_solve)
+        kernels[gi].update(alone_ms=alone["ms"], alone_achieved=alone["achieved"], alone_frac=alone["frac"],
+                           span_note="ms = the Gram launches' span beside the lead group's factorisation; "
+                                     "alone_* = the same launches with the lead group off (untimed run)")
     dom = max(kernels, key=lambda r: r["ms"])
     traffic, tsrc = pmc_traffic(dom["kernel"], args, n_solve)
     roof = dict(bound=dom["bound"], achieved=dom["achieved"], peak=dom["peak"], unit=dom["unit"],
