@@ -569,7 +569,43 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     };
-    for (int st = 0; st < nst; st += 4) {
+    // waves with all 8 MFMA tiles active (every interior tile): one branch-free block per stage
+    // that issues the next stage's expansion writes between this stage's operand reads and
+    // MFMAs (every thread stores: a diagonal tile's B stagers fill the unread B slot, rows past
+    // m only feed outputs past m), so the VALU / LDS-write phase overlaps the MFMAs
+    auto step_full = [&](Pk& pk, int st) {
+        int8_t* wslot = hlds + ((st + 1) & 1) * 2 * kHOp + sop * kHOp;
+        const int8_t* A = hlds + (st & 1) * 2 * kHOp;
+        const int8_t* B = diag ? A : A + kHOp;
+#pragma unroll
+        for (int kk = 0; kk < kHK / 32; ++kk) {
+            const int c = 2 * kk + csub;
+            v4i av[2], bv[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = *reinterpret_cast<const v4i*>(A + swz(64 * wr + 32 * i + rsub, c));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const v4i*>(B + swz(128 * wc + 32 * j + rsub, c));
+            *reinterpret_cast<v4i*>(wslot + swz(srow, kk)) = expand_dose(static_cast<uint32_t>(pk.lo[kk]));
+            *reinterpret_cast<v4i*>(wslot + swz(srow, 4 + kk)) = expand_dose(static_cast<uint32_t>(pk.hi[kk]));
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+        pk = gload(st + 5);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    int st = 0;
+    if (act == 0xFFu)
+        for (; st + 4 <= nst; st += 4) {
+            step_full(p1, st);
+            step_full(p2, st + 1);
+            step_full(p3, st + 2);
+            step_full(p0, st + 3);
+        }
+    for (; st < nst; st += 4) {
         step(p1, st);
         step(p2, st + 1);
         step(p3, st + 2);
