@@ -502,7 +502,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
 // (i << 8)): L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of
 // the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).  upd: first apply
 // the pending update of A_i from the panels of regions s-upd .. s-1.
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_panel(
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_panel(
     chol::TiledArgs a0, const int32_t* __restrict__ items, int32_t n_items) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];

@@ -12,11 +12,13 @@ from _common import normwise
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [128, 129, 159, 160, 161, 191, 192, 575, 640, 703, 1000, 4100]   # 4100: 512-column super steps
+BASE_SIZES = [128, 129, 159, 160, 161, 191, 192, 575, 640, 703, 1000]
+SIZES = BASE_SIZES + [4100]   # 4100: 512-column super steps (blocks of m >= 4096)
 
 
-def _problem(seed=11, n_ref=256, with_large=True, mono_block=None):
+def _problem(seed=11, n_ref=256, with_large=True, mono_block=None, sizes=BASE_SIZES):
     from dbslmm_amd import BlockProblem, synth
+    SIZES = sizes
     total = sum(SIZES)
     p = synth.simulate(total + 50, n_ref, pop="EUR", chroms=[1, 2], seed=seed, miss_rate=0.002,
                        large_every=0)
@@ -68,7 +70,7 @@ def _oracle(prob):
 
 @pytest.mark.parametrize("with_large", [True, False])
 def test_tiled_matches_oracle_and_single_workgroup(monkeypatch, with_large):
-    prob = _problem(with_large=with_large)
+    prob = _problem(with_large=with_large, sizes=SIZES)
     ref, _ = _oracle(prob)
     tiled, st_t = _solve(prob, 64, monkeypatch)          # every block on the tiled path
     single, st_s = _solve(prob, 10 ** 9, monkeypatch)    # none
@@ -102,7 +104,7 @@ def test_tiled_monomorphic_block_is_nan(monkeypatch):
 
 def test_tiled_plan_rerun_bit_identical(monkeypatch):
     from dbslmm_amd import Context, Plan
-    prob = _problem(seed=3)
+    prob = _problem(seed=3, sizes=SIZES)
     prob.opts["tiled_min"] = 128
     plan = Plan(Context(0), prob)
     wl = plan.workload()
@@ -169,7 +171,7 @@ def test_lead_group_bit_identical():
     sequence on its own streams beside the rest of the Gram and the other blocks' sequence) only
     reorders work: single solves and h2f runs give the same betas bit for bit as one sequence."""
     from dbslmm_amd import Context, Plan
-    prob = _problem(seed=13)
+    prob = _problem(seed=13, sizes=SIZES)
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     res = {}
     for lead in (600, -1):
