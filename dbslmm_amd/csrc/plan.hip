@@ -21,6 +21,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -73,6 +74,11 @@ constexpr int kWideMin = 4096;          //     flop; config 4 lead group 52.5 ->
 constexpr int kGramSq = 4;              // 2D tile squares per XCD of the 256-tile Gram
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+// Graph capture (launch_graph) vs the device-synchronising setup calls of another host thread
+// (multi-device plans run one thread per shard; several shards may share a device): a
+// hipDeviceSynchronize / synchronous memset or copy while another thread's stream is capturing
+// invalidates that capture.  Both sides hold this lock.
+std::mutex g_capture_mu;
 }  // namespace
 
 struct dbslmm_ctx {
@@ -132,7 +138,10 @@ struct dbslmm_plan {
     int32_t n_btiles = 0;
     GramTile* d_htiles = nullptr;      // 256 x 256 tiles of the big blocks, per-XCD queues
     int32_t n_htiles = 0;
-    int32_t n_htiles_lead = 0;         // ... of which the first n_htiles_lead are the lead group's
+    int32_t n_htiles_lead = 0;         // ... of which the first n_htiles_lead are the lead group's,
+    int32_t n_htiles_tiled = 0;        //     the first n_htiles_tiled the tiled blocks' (then the rest)
+    bool early_fork = false;           // every tiled block's Gram is in those: the tiled sequences
+                                       // may start before the other blocks' Gram
     double* d_M = nullptr;
     double *d_beta_s = nullptr, *d_beta_l = nullptr;
     double* d_dshift = nullptr;        // 1/(sigma_s n), read by the solve kernels
@@ -637,8 +646,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     // the 256-tile kernel pays once its K loop outweighs its 512 KB fp64 epilogue per tile
     const int64_t gram_huge_min = op.gram_huge_min > 0 ? op.gram_huge_min
                                   : p->kpad >= 4096 ? kGramHugeMinDefault : 2 * kGramHugeMinDefault;
-    std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd), lq(kXcd);
-    std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0), lload(kXcd, 0.0);
+    std::vector<std::vector<GramTile>> xq(kXcd), hq(kXcd), lq(kXcd), nq(kXcd);
+    std::vector<double> xload(kXcd, 0.0), hload(kXcd, 0.0), lload(kXcd, 0.0), nload(kXcd, 0.0);
     int64_t moff = 0;
     double ops_alg = 0, ops_exec = 0, chol_flops_large = 0, chol_flops_small = 0, chol_flops_tiled = 0;
     int64_t tiled_min = kTiledMinDefault;
@@ -723,8 +732,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         }
         if (m >= gram_huge_min) {   // 256 x 256 tiles
             const int T = static_cast<int>((m + gram::kHT - 1) / gram::kHT);
-            auto& q = m >= lead_min ? lq : hq;
-            auto& ld_ = m >= lead_min ? lload : hload;
+            auto& q = m >= lead_min ? lq : tiled ? hq : nq;
+            auto& ld_ = m >= lead_min ? lload : tiled ? hload : nload;
             // squares of kGramSq x kGramSq tiles (lower triangle), each on the least-loaded XCD:
             // the workgroups in flight on an XCD share kGramSq row panels of each operand
             for (int si = 0; si < T; si += kGramSq)
@@ -767,8 +776,9 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             for (size_t i = 0; i < xq[x].size(); ++i) btiles[i * kXcd + x] = xq[x][i];
         p->n_btiles = static_cast<int32_t>(btiles.size());
     }
-    std::vector<GramTile> htiles;   // [lead group's queues | the others'], entry e on XCD e % 8
-    for (const auto* qs : {&lq, &hq}) {
+    // [lead group's queues | the other tiled blocks' | the non-tiled blocks'], entry e on XCD e % 8
+    std::vector<GramTile> htiles;
+    for (const auto* qs : {&lq, &hq, &nq}) {
         size_t qmax = 0;
         for (const auto& q : *qs) qmax = std::max(qmax, q.size());
         const size_t base = htiles.size();
@@ -776,6 +786,16 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         for (int x = 0; x < kXcd; ++x)
             for (size_t i = 0; i < (*qs)[x].size(); ++i) htiles[base + i * kXcd + x] = (*qs)[x][i];
         if (qs == &lq) p->n_htiles_lead = static_cast<int32_t>(htiles.size());
+        if (qs == &hq) p->n_htiles_tiled = static_cast<int32_t>(htiles.size());
+    }
+    {
+        // (without tiled blocks stream2 runs chol_small, which needs the whole Gram)
+        bool all_huge = true, any_tiled = false;
+        for (size_t b = 0; b < mv.size(); ++b) {
+            any_tiled = any_tiled || is_tiled[b];
+            if (is_tiled[b] && mv[b] < gram_huge_min) all_huge = false;
+        }
+        p->early_fork = all_huge && any_tiled;
     }
     p->n_htiles = static_cast<int32_t>(htiles.size());
     p->M_elems = moff;
@@ -1009,6 +1029,7 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
 static int ensure_copies(dbslmm_plan* p, int n) {
     dbslmm_ctx* ctx = p->ctx;
     if (n <= p->n_copies) return DBSLMM_OK;
+    std::lock_guard<std::mutex> lk(g_capture_mu);   // device-wide sync + synchronous memset
     HIP_TRY(ctx, hipDeviceSynchronize());
     void* old[] = {p->d_M, p->d_dshift, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
     for (void* q : old)
@@ -1063,7 +1084,10 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     dbslmm_ctx* ctx = p->ctx;
     hipStream_t st = grp.st;
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
-    if (!p->d_cheb) HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    if (!p->d_cheb) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
+        HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    }
     const int64_t c = copy;
     trsv::Args a{};
     a.M = p->d_M + c * p->M_elems;
@@ -1111,6 +1135,7 @@ static int launch_graph(dbslmm_plan* p, double isn, const std::vector<TLaunch>& 
                         int copy, hipGraphExec_t& gx, const TSeq& sq) {
     dbslmm_ctx* ctx = p->ctx;
     if (!gx) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
         hipGraph_t gr = nullptr;
         HIP_TRY(ctx, hipStreamBeginCapture(sq.chain, hipStreamCaptureModeThreadLocal));
         const int rc = enqueue_tiled(p, isn, tl, d_tlist, copy, sq);
@@ -1224,12 +1249,15 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
 static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
     dbslmm_ctx* ctx = p->ctx;
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
-    if (!p->d_cheb)
+    if (!p->d_cheb) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
         HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    }
     // the coefficients depend only on the sigmas: uploaded when they change, synchronously (the
     // host vector is a temporary of the run; an asynchronous copy from pageable memory may still
     // be pending when it is freed) after every earlier run that reads d_coef has finished
     if (cp.coef == p->h_coef) return DBSLMM_OK;
+    std::lock_guard<std::mutex> lk(g_capture_mu);   // synchronous copy below
     HIP_TRY(ctx, hipStreamSynchronize(st));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream2));
     if (p->coef_cap < static_cast<int32_t>(cp.coef.size())) {
@@ -1332,6 +1360,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         const int rc = ensure_copies(p, n);
         if (rc) return rc;
         if (p->multi_n != n) {
+            std::lock_guard<std::mutex> lk(g_capture_mu);   // synchronous upload below
             std::vector<int32_t> tlist;
             p->tl_multi.clear();
             build_tiled(p->h_m, p->h_tb, n, p->n_nonempty, p->tl_multi, tlist);
@@ -1407,6 +1436,17 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     // main stream; its graph is launched after every main-stream kernel is enqueued (a graph
     // launch of a few hundred nodes keeps the host busy for milliseconds)
     if (lead) HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
+    // the other tiled blocks' Gram tiles next: with early_fork their sequence (and the single
+    // sequence without a lead group) forks here, before the non-tiled blocks' Gram
+    if (front && p->n_htiles_tiled > p->n_htiles_lead) {
+        gram_huge(p->n_htiles_lead, p->n_htiles_tiled - p->n_htiles_lead);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    const bool early = p->early_fork && p->n_nonempty > 0;
+    if (early) {
+        HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
+    }
     if (front && p->n_tiles > 0) {
         dim3 grid((p->n_tiles + 3) / 4);
         hipLaunchKernelGGL(dbslmm_gram_i8, grid, dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
@@ -1416,8 +1456,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->tiled_min, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
-    if (front && p->n_htiles > p->n_htiles_lead) {
-        gram_huge(p->n_htiles_lead, p->n_htiles - p->n_htiles_lead);
+    if (front && p->n_htiles > p->n_htiles_tiled) {
+        gram_huge(p->n_htiles_tiled, p->n_htiles - p->n_htiles_tiled);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_btiles > 0) {
@@ -1433,8 +1473,10 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     if (p->n_nonempty > 0) {
         // fork: the tiled sequence (or, with a lead group, the rest sequence on stream4) runs
         // beside the single-workgroup and single-wave kernels of the main stream
-        HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
-        HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
+        if (!early) {
+            HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
+            HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
+        }
         for (int c = 0; c < n && p->n_large > 0; ++c) {
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M + c * p->M_elems, p->d_order, p->n_large,
