@@ -439,9 +439,9 @@ def main():
     n_solve = len(sigmas) if sigmas else 1
     kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl, n_solve) for k in range(len(KERNEL_NAMES))]
     if world == 1 and not args.no_isolated:
-        # The lead group's factorisation overlaps the rest of the Gram, so the Gram's span above
-        # includes that contention.  One untimed plan with the lead group off times the Gram
-        # launches alone (outside the timed region; reported beside the span, never as `value`).
+        # The lead group's unpack, Gram and factorisation overlap the others', so the phase spans
+        # above include that contention.  One untimed plan with the lead group off times every
+        # phase without it (outside the timed region; reported beside the spans, never as `value`).
         import dataclasses
         iso = Plan(ctx, dataclasses.replace(prob, opts=dict(prob.opts, lead_min=-1)))
         run_iso = (lambda: iso.run_multi(sigmas)) if sigmas else iso.run
@@ -453,11 +453,11 @@ def main():
         iso.sync()
         iso_ms, iso_n = iso.kernel_ms()
         del iso
-        gi = KERNEL_NAMES.index("dbslmm_gram_i8")
-        alone = kernel_roofline(KERNEL_NAMES[gi], float(iso_ms[gi]) * iso_n / 3, wl, n_solve)
-        kernels[gi].update(alone_ms=alone["ms"], alone_achieved=alone["achieved"], alone_frac=alone["frac"],
-                           span_note="ms = the Gram launches' span beside the lead group's factorisation; "
-                                     "alone_* = the same launches with the lead group off (untimed run)")
+        for k in range(len(KERNEL_NAMES)):
+            alone = kernel_roofline(KERNEL_NAMES[k], float(iso_ms[k]) * iso_n / 3, wl, n_solve)
+            kernels[k].update(alone_ms=alone["ms"], alone_achieved=alone["achieved"], alone_frac=alone["frac"],
+                              span_note="ms = the phase's wall span in the timed (overlapped) schedule; "
+                                        "alone_* = the same phase with the lead group off (untimed run)")
     dom = max(kernels, key=lambda r: r["ms"])
     traffic, tsrc = pmc_traffic(dom["kernel"], args, n_solve)
     roof = dict(bound=dom["bound"], achieved=dom["achieved"], peak=dom["peak"], unit=dom["unit"],

@@ -91,16 +91,19 @@ __device__ __forceinline__ v4i expand_dose(uint32_t w) {
 //                  1/sd with the N-1 divisor (nomalizeVec), sum of observed dosages.
 //   maf (optional) min(af, 1-af), af = mu/2 (dtpr.cpp:361-362).
 //   block_flags    bit 0 set when a slot of the block has a missing call.
+//   slot_list      optional: unpack only these n_slots slots (the plan unpacks its lead group first)
 // ------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
     const uint8_t* __restrict__ bed, int32_t n_ref, int64_t bytes_per_snp,
     const int32_t* __restrict__ slot_pos, const int32_t* __restrict__ slot_block, int32_t n_slots,
     uint32_t* __restrict__ Gp, int64_t kpad,
     double* __restrict__ S_out, double* __restrict__ mu_out, double* __restrict__ rsd_out,
-    double* __restrict__ maf_out, int32_t* __restrict__ block_flags) {
+    double* __restrict__ maf_out, int32_t* __restrict__ block_flags,
+    const int32_t* __restrict__ slot_list) {
     const int lane = threadIdx.x & (kWave - 1);
-    const int slot = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-    if (slot >= n_slots) return;
+    const int k = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    if (k >= n_slots) return;
+    const int slot = slot_list ? slot_list[k] : k;   // a subset of the slots (n_slots of them)
     const int32_t pos = slot_pos[slot];
     const int64_t n_words = kpad / 16;          // 16 individuals per lane-word
     uint32_t* grow = Gp ? Gp + static_cast<int64_t>(slot) * n_words : nullptr;

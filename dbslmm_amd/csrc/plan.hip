@@ -39,7 +39,7 @@ namespace {
 // events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large,
 // [4] / [5] around chol_small (main stream), [6] / [8] around the tiled factorisation sequence,
 // [8] / [7] around the h2f Chebyshev iterations (stream2)
-constexpr int kEvPerRun = 9;
+constexpr int kEvPerRun = 11;   // 9, 10: around the lead group's Gram (between the unpack halves)
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
@@ -140,6 +140,8 @@ struct dbslmm_plan {
     int32_t n_htiles = 0;
     int32_t n_htiles_lead = 0;         // ... of which the first n_htiles_lead are the lead group's,
     int32_t n_htiles_tiled = 0;        //     the first n_htiles_tiled the tiled blocks' (then the rest)
+    int32_t* d_slot_order = nullptr;   // lead group: [its slots | the others'] (unpacked in that order)
+    int32_t n_slots_lead = 0;
     bool early_fork = false;           // every tiled block's Gram is in those: the tiled sequences
                                        // may start before the other blocks' Gram
     double* d_M = nullptr;
@@ -590,7 +592,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
-                    p->d_cheb, p->d_coef, p->d_stamps};
+                    p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -826,6 +828,20 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             build_tiled(mv, tb_rest, 1, p->n_nonempty, p->tl_rest, tlist);
         }
     }
+    // lead group: its slots are unpacked first, so its Gram (and sequence) need not wait for the
+    // whole unpack
+    std::vector<int32_t> slot_order;
+    if (!p->tl_rest.empty()) {
+        std::vector<char> in_lead(p->n_nonempty, 0);
+        for (int32_t b = 0; b < p->n_nonempty; ++b) in_lead[b] = mv[b] >= lead_min;
+        for (int32_t b = 0; b < p->n_nonempty; ++b)
+            if (in_lead[b])
+                for (int32_t r = row0[b]; r < row0[b] + ldv[b]; ++r) slot_order.push_back(r);
+        p->n_slots_lead = static_cast<int32_t>(slot_order.size());
+        for (int32_t b = 0; b < p->n_nonempty; ++b)
+            if (!in_lead[b])
+                for (int32_t r = row0[b]; r < row0[b] + ldv[b]; ++r) slot_order.push_back(r);
+    }
     // substitution work lists (trsv.hip): 64-row tiles of the tiled blocks; forward in order of
     // (tile, block), backward in order of (tiles from the end, block) -- every dependency of an
     // item comes earlier in its list
@@ -922,6 +938,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_tri_b, tri_b)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_foff, foff)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_tb, p->h_tb)) != hipSuccess) return fail("upload trsv lists");
+    if (!slot_order.empty() && (e = dev_upload(&p->d_slot_order, slot_order)) != hipSuccess) return fail("upload slot order");
     // [tile flags | ticket counter | error word | spare]
     if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
     if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
@@ -972,6 +989,11 @@ static int collect_timing(dbslmm_plan* p) {
             HIP_TRY(ctx, hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
             p->ms_acc[k] += ms;
         }
+        // the lead group's Gram (9 -> 10) sits between the two unpack launches (0 -> 1)
+        float lg = 0.f;
+        HIP_TRY(ctx, hipEventElapsedTime(&lg, e[9], e[10]));
+        p->ms_acc[0] -= lg;
+        p->ms_acc[1] += lg;
         p->ms_runs++;
     }
     p->runs_pending = 0;
@@ -1393,15 +1415,21 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     if (front) HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
     HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, n * nbk * sizeof(int32_t), s));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], s));
-    if (front && p->n_slots > 0) {
+    auto unpack = [&](const int32_t* list, int32_t n_sl) {
         const int wpb = 4;
-        dim3 grid((p->n_slots + wpb - 1) / wpb);
+        dim3 grid((n_sl + wpb - 1) / wpb);
         hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, s, p->d_bed, p->n_ref,
-                           p->bytes_per_snp, p->d_slot_pos, p->d_slot_block, p->n_slots, p->d_G,
-                           p->kpad, p->d_S, p->d_mu, p->d_rsd, nullptr, p->d_flags);
+                           p->bytes_per_snp, p->d_slot_pos, p->d_slot_block, n_sl, p->d_G,
+                           p->kpad, p->d_S, p->d_mu, p->d_rsd, nullptr, p->d_flags, list);
+    };
+    // a lead group's slots first: its Gram and sequence start after ~2 % of the unpack
+    const bool split_unpack = front && p->n_slots_lead > 0;
+    if (front && p->n_slots > 0) {
+        if (split_unpack) unpack(p->d_slot_order, p->n_slots_lead);
+        else unpack(nullptr, p->n_slots);
         HIP_TRY(ctx, hipGetLastError());
     }
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], s));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[9], s));
     if (!front && n > 1)
         return (ctx->err = "a multi-copy run needs the Gram front", DBSLMM_E_STATE);
     const std::vector<TLaunch>& tl = n > 1 && !cheb ? p->tl_multi : p->tl;
@@ -1432,10 +1460,16 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         gram_huge(0, p->n_htiles_lead);
         HIP_TRY(ctx, hipGetLastError());
     }
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[10], s));
     // the lead sequence (stream2, high priority: the critical path) waits for this point of the
     // main stream; its graph is launched after every main-stream kernel is enqueued (a graph
     // launch of a few hundred nodes keeps the host busy for milliseconds)
     if (lead) HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
+    if (split_unpack) {   // the other slots
+        unpack(p->d_slot_order + p->n_slots_lead, p->n_slots - p->n_slots_lead);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], s));
     // the other tiled blocks' Gram tiles next: with early_fork their sequence (and the single
     // sequence without a lead group) forks here, before the non-tiled blocks' Gram
     if (front && p->n_htiles_tiled > p->n_htiles_lead) {
@@ -1813,7 +1847,7 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
                                dim3(256), 0, st, d_tbed, tbps, d_tpos, p->n_slots, d_sel, n_test, cbps, d_cbed);
             hipLaunchKernelGGL(dbslmm_unpack_stats, dim3(static_cast<unsigned>((p->n_slots + 3) / 4)), dim3(256), 0,
                                st, d_cbed, n_test, cbps, d_cpos, d_cpos, p->n_slots, nullptr,
-                               nt_pad, nullptr, d_mu, d_rsd, nullptr, nullptr);
+                               nt_pad, nullptr, d_mu, d_rsd, nullptr, nullptr, nullptr);
             hipLaunchKernelGGL(dbslmm_variance, dim3(static_cast<unsigned>(nt_pad / 64), p->n_nonempty),
                                dim3(256), 0, st, p->d_M + p->var_copy * p->M_elems, p->d_row0, p->d_m,
                                p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_status + p->var_copy * p->nbk,
@@ -1863,7 +1897,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
         hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, ctx->stream, cached ? ctx->d_bed_cache : d_bed,
                            n_ref, bps,
                            d_pos, d_pos, static_cast<int32_t>(n_snp), nullptr, round_up(n_ref, 64),
-                           nullptr, nullptr, nullptr, d_maf, nullptr);
+                           nullptr, nullptr, nullptr, d_maf, nullptr, nullptr);
         if ((e = hipGetLastError()) != hipSuccess ||
             (e = hipStreamSynchronize(ctx->stream)) != hipSuccess ||
             (e = hipMemcpy(maf, d_maf, n_snp * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) {
@@ -1909,7 +1943,7 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
         }
         hipLaunchKernelGGL(dbslmm_unpack_stats, dim3((n_rows + 3) / 4), dim3(256), 0, ctx->stream,
                            d_bed, n_ref, bps, d_pos, d_pos, n_rows, nullptr, round_up(n_ref, 64),
-                           nullptr, d_mu, d_rsd, d_maf, nullptr);
+                           nullptr, d_mu, d_rsd, d_maf, nullptr, nullptr);
         hipLaunchKernelGGL(dbslmm_std_columns, dim3(static_cast<unsigned>((n_out + 255) / 256)),
                            dim3(256), 0, ctx->stream, d_bed, n_ref, bps, d_pos, n_rows, d_mu, d_rsd,
                            d_out);
@@ -1980,7 +2014,7 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
         if (n_rows > 0)
             hipLaunchKernelGGL(dbslmm_unpack_stats, dim3(static_cast<unsigned>((n_rows + 3) / 4)), dim3(256), 0,
                                ctx->stream, d_bed, n_ref, bps, d_pos, d_pos, static_cast<int32_t>(n_rows),
-                               nullptr, round_up(n_ref, 64), nullptr, d_mu, d_rsd, nullptr, nullptr);
+                               nullptr, round_up(n_ref, 64), nullptr, d_mu, d_rsd, nullptr, nullptr, nullptr);
         hipLaunchKernelGGL(dbslmm_valid_partial, dim3(n_chunks, num_block), dim3(256), 0, ctx->stream,
                            d_bed, n_ref, bps, d_ptr, d_pos, d_z1, d_mu, d_rsd, d_part, n_chunks);
         hipLaunchKernelGGL(dbslmm_valid_reduce, dim3((num_block + 255) / 256), dim3(256), 0, ctx->stream,
