@@ -797,7 +797,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             any_tiled = any_tiled || is_tiled[b];
             if (is_tiled[b] && mv[b] < gram_huge_min) all_huge = false;
         }
-        p->early_fork = all_huge && any_tiled;
+        // (lead_min < 0: no overlap of the Gram and the factorisation at all)
+        p->early_fork = all_huge && any_tiled && op.lead_min >= 0;
     }
     p->n_htiles = static_cast<int32_t>(htiles.size());
     p->M_elems = moff;

@@ -70,7 +70,9 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                and their factorisation (the longest dependency chains) starts right after
  *                them, beside the rest of the Gram and the other blocks' factorisation (default
  *                max(2048, m_max / 2) when tiled blocks lie on both sides of it; < 0: no lead
- *                group).  Scheduling only: the results are bit-identical either way.
+ *                group, and the tiled sequence starts after the whole Gram instead of right
+ *                after the tiled blocks' Gram tiles).  Scheduling only: the results are
+ *                bit-identical either way.
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;

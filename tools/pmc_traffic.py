@@ -7,7 +7,8 @@ coalesced streaming read (MI355X_MICROARCH.md, HBM section): the read side is do
 Also records launches per kernel and, for the composite phases the bench times as one slot --
 the tiled Cholesky (dbslmm_tchol_* launches plus the persistent backward substitution
 dbslmm_trsv_bwd<1>) and the h2f Chebyshev substitutions (dbslmm_trsv_fwd/bwd<2>) -- the summed
-HBM bytes per run (= per bench step; runs = launches of dbslmm_unpack_stats) under
+HBM bytes per run (= per bench step; runs = launches of dbslmm_gram_i8, one per run -- the unpack
+is two launches per run with a lead group) under
 "dbslmm_tchol" and "dbslmm_trsv" (key "hbm_bytes_per_step").
 """
 import collections
@@ -33,7 +34,7 @@ def main(src, dst, bench_args=""):
                      f"`python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline {bench_args}`".rstrip(),
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
            "kernels": {}}
-    runs = f.get("dbslmm_unpack_stats", (0, 0))[1]
+    runs = f.get("dbslmm_gram_i8", (0, 0))[1]
     seq = trsv = 0.0
     for k in sorted(set(f) | set(w)):
         name = k[5:] if k.startswith("void ") else k
