@@ -388,9 +388,14 @@ def main():
         gather = ShardGather(full.n_s, full.n_l, s_idx, l_idx, k=len(sigmas) if sigmas else 1,
                              device=cdev)
 
+    outs = None
+    if sigmas:   # the caller's result buffers, reused every step (as an application would)
+        outs = (np.zeros((len(sigmas), prob.n_s)), np.zeros((len(sigmas), prob.n_l)),
+                np.zeros((len(sigmas), prob.num_block), dtype=np.int32))
+
     def step():
         if sigmas:
-            res = plan.run_multi(sigmas)      # one Gram, len(sigmas) solves (synchronous)
+            res = plan.run_multi(sigmas, out=outs)   # one Gram, len(sigmas) solves (synchronous)
             if gather:
                 gather([(r[0], r[1]) for r in res])
         elif gather:

@@ -153,14 +153,23 @@ class Plan:
     def set_sigma(self, sigma_s: float):
         self.ctx.check(self.ctx.lib.dbslmm_plan_set_sigma(self.h, float(sigma_s)), "plan_set_sigma")
 
-    def run_multi(self, sigmas):
-        """h2f tuning: one unpack + Gram, one solve per sigma_s -> [(beta_s, beta_l, status)]."""
+    def run_multi(self, sigmas, out=None):
+        """h2f tuning: one unpack + Gram, one solve per sigma_s -> [(beta_s, beta_l, status)].
+        out: optional (beta_s, beta_l, status) arrays of shapes (n, n_s), (n, n_l), (n, num_block)
+        to write into (a caller that solves repeatedly reuses its buffers)."""
         p = self.prob
         sig = np.ascontiguousarray(sigmas, dtype=np.float64)
         n = len(sig)
-        bs = np.zeros((n, p.n_s))
-        bl = np.zeros((n, p.n_l))
-        st = np.zeros((n, p.num_block), dtype=np.int32)
+        if out is not None:
+            bs, bl, st = out
+            if (bs.shape != (n, p.n_s) or bl.shape != (n, p.n_l) or st.shape != (n, p.num_block)
+                    or bs.dtype != np.float64 or bl.dtype != np.float64 or st.dtype != np.int32
+                    or not all(a.flags.c_contiguous for a in out)):
+                raise ValueError("out: C-contiguous float64 (n, n_s), (n, n_l) and int32 (n, num_block)")
+        else:
+            bs = np.zeros((n, p.n_s))
+            bl = np.zeros((n, p.n_l))
+            st = np.zeros((n, p.num_block), dtype=np.int32)
         self.ctx.check(self.ctx.lib.dbslmm_plan_run_multi(self.h, _ptr(sig), n, _ptr(bs), _ptr(bl),
                                                           _ptr(st)), "plan_run_multi")
         return [(bs[i], bl[i], st[i]) for i in range(n)]

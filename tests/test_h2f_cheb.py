@@ -87,3 +87,22 @@ def test_cheb_repeatable_and_followed_by_plain_run(monkeypatch):
     got = plan.download()
     ref = _fresh(prob, sig[:1])[0]
     np.testing.assert_array_equal(_cat(got), _cat(ref))
+
+
+def test_run_multi_into_caller_buffers():
+    """Plan.run_multi(out=...) writes the same results into the caller's (reused) arrays."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=7)
+    prob.opts["tiled_min"] = 256
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    plan = Plan(Context(0), prob)
+    ref = plan.run_multi(sig)
+    out = (np.full((3, prob.n_s), 7.0), np.full((3, prob.n_l), 7.0), np.full((3, prob.num_block), 9, dtype=np.int32))
+    for _ in range(2):
+        got = plan.run_multi(sig, out=out)
+        for (a, b, c), (x, y, z) in zip(got, ref):
+            np.testing.assert_array_equal(a, x)
+            np.testing.assert_array_equal(b, y)
+            np.testing.assert_array_equal(c, z)
+    with pytest.raises(ValueError):
+        plan.run_multi(sig, out=(out[0][:2], out[1], out[2]))
