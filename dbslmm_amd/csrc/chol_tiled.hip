@@ -498,9 +498,9 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     }
 }
 
-// panel of outer step s, one workgroup per 64-row tile i below region s (item (block << 16) |
-// (i << 8)): L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of
-// the region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).  upd: first apply
+// panel of outer step s, one workgroup per 64-row tile i below region s (item (block << 16) | i):
+// L_i0 = A_i0 X00^T, then L_i1 = (A_i1 - L_i0 L10^T) X11^T (X00, X11: the inverses of the
+// region's two 64 x 64 diagonal tiles; L10 its off-diagonal 64 x 64 block).  upd: first apply
 // the pending update of A_i from the panels of regions s-upd .. s-1.
 extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_panel(
     chol::TiledArgs a0, const int32_t* __restrict__ items, int32_t n_items) {
@@ -510,7 +510,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tcho
     const int32_t it = items[2 * blockIdx.x];
     const int32_t meta = items[2 * blockIdx.x + 1];
     const int s = meta >> 8, upd = meta & 255;
-    const int i = (it >> 8) & 255;
+    const int i = it & 0xFFFF;
     int b;
     const TiledArgs a = a0.view(it >> 16, b);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qi = wave >> 1, qj = wave & 1;

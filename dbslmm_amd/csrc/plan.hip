@@ -70,7 +70,8 @@ constexpr int kTlRecord = 6, kTlWait = 7;
 #endif
 constexpr int kSuper = DBSLMM_SUPER;    // regions (128 columns) per super step
 constexpr int kWideSuper = 4;           // ... for blocks of m >= kWideMin (half the C traffic per
-constexpr int kWideMin = 4096;          //     flop; config 4 lead group 52.5 -> 51.8 ms/step)
+constexpr int kWideMin = 4096;          //     flop; config 5 35.4 -> 34.3 ms/step)
+constexpr int kTiledMaxM = 255 * 128;   // tiled path: 128-row tile and region indices < 256
 constexpr int kGramSq = 4;              // 2D tile squares per XCD of the 256-tile Gram
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -395,7 +396,7 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
         for (const auto& k : bl)      // panel(r0)
             if (active(k)) {
                 const int r0 = (g - k.off) * k.R;
-                for (int i = 2 * r0 + 2; i <= k.Tz64; ++i) { v.push_back((k.bq << 16) | (i << 8)); v.push_back(r0 << 8); }
+                for (int i = 2 * r0 + 2; i <= k.Tz64; ++i) { v.push_back((k.bq << 16) | i); v.push_back(r0 << 8); }
             }
         panel_launch(v);
         for (int j = 1; j < Rmax; ++j) {
@@ -406,7 +407,7 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
                     if (r >= k.nr) continue;
                     rv.push_back(k.bq);
                     rv.push_back((r << 8) | j);
-                    for (int i = 2 * r + 2; i <= k.Tz64; ++i) { pv.push_back((k.bq << 16) | (i << 8)); pv.push_back((r << 8) | j); }
+                    for (int i = 2 * r + 2; i <= k.Tz64; ++i) { pv.push_back((k.bq << 16) | i); pv.push_back((r << 8) | j); }
                 }
             region_launch(rv);
             panel_launch(pv);
@@ -695,8 +696,9 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         if (m == 0) { p->h_empty.push_back(b); continue; }
         const int nb = static_cast<int>(row0.size());
         const bool tiled = m >= tiled_min;
-        if (tiled && (m / chol::kBT > 254 || nb >= 32767)) {   // packed (block, I, J) trailing items
-            ctx->err = "LD block too large for the tiled path (m must be < 16320 SNPs)";
+        // packed work items: 128-row tile / region indices in 8 bits, block (x copies) in 15
+        if (tiled && (m >= kTiledMaxM || nb >= 32767)) {
+            ctx->err = "LD block too large for the tiled path (m must be < 32640 SNPs)";
             dbslmm_plan_destroy(p);
             return DBSLMM_E_ARG;
         }

@@ -192,3 +192,30 @@ def test_lead_group_bit_identical():
         for x, y in zip(multi[c], multi0[c]):
             np.testing.assert_array_equal(x, y)
     assert np.all(one[2] == 0)
+
+
+def test_block_beyond_16k_snps():
+    """One LD block of 17,000 SNPs (above round 1's 16,320 cap; the tiled path now takes
+    m < 32,640): the h2f copies and a plain run against the direct fp64 solve (NumPy Cholesky on
+    the host cores, as tests/test_fullscale.py)."""
+    from dbslmm_amd import Context, Plan
+    from test_fullscale import _block_ref, _threads
+    prob = _problem(seed=17, n_ref=128, sizes=[17000])
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    thr = _threads()
+    O.use_blas(True)
+    O.blas_threads(thr)
+    try:
+        ref = _block_ref(prob, 0, sig, thr, pcg=False)["chol"]
+    finally:
+        O.blas_threads(1)
+    plan = Plan(Context(0), prob)
+    multi = plan.run_multi(sig)
+    for c in range(3):
+        assert np.all(multi[c][2] == 0)
+        assert normwise(np.concatenate([multi[c][0], multi[c][1]]), ref[c]) < 1e-9, c
+    plan.set_sigma(sig[1])
+    plan.run()
+    bs, bl, st = plan.download()
+    assert np.all(st == 0)
+    assert normwise(np.concatenate([bs, bl]), ref[1]) < 1e-9
