@@ -65,10 +65,7 @@ struct TLaunch {
 // sync entries of a launch list (lookahead): kind 6 records tiled event `step` on stream `strm`,
 // kind 7 makes stream `strm` wait for it
 constexpr int kTlRecord = 6, kTlWait = 7;
-#ifndef DBSLMM_SUPER
-#define DBSLMM_SUPER 2
-#endif
-constexpr int kSuper = DBSLMM_SUPER;    // regions (128 columns) per super step
+constexpr int kSuper = 2;               // regions (128 columns) per super step
 constexpr int kWideSuper = 4;           // ... for blocks of m >= kWideMin (half the C traffic per
 constexpr int kWideMin = 4096;          //     flop; config 5 35.4 -> 34.3 ms/step)
 constexpr int kTiledMaxM = 255 * 128;   // tiled path: 128-row tile and region indices < 256
@@ -321,11 +318,10 @@ static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
 //   panel(r0) -> for r = r0+1 .. r0+R-1: region(r) [+ its pending update from panels r0 .. r-1]
 //   -> panel(r) [+ the pending update of its rows' region-r columns] -> trailing K = 128 R of
 //   everything right of the super step (the next first region included) -> region(r0 + R),
-// then the backward steps (64-row tiles, descending).  Every launch of a given slot holds the
+// then one persistent backward substitution (run_pbwd).  Every launch of a given slot holds the
 // same kind of work for all blocks, each at its OWN local step (work items carry it): blocks are
-// left-aligned (all start at launch 0); env DBSLMM_ALIGN=1 right-aligns them (a block with fewer
-// super steps starts later, so its heavy first steps overlap the largest block's latency-bound
-// last steps -- no gain measured at configs 3-5).  Each work item is two int32:
+// left-aligned (all start at launch 0; right alignment -- a block with fewer super steps starting
+// later -- measured no gain at configs 3-5).  Each work item is two int32:
 // [block / tile, (local step << 8) | pending panels or K multiple].
 static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_t>& tb0, int copies,
                         int nb, std::vector<TLaunch>& tl, std::vector<int32_t>& tlist) {
