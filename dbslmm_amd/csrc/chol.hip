@@ -575,11 +575,16 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_la
     const double* __restrict__ z_slot, const int32_t* __restrict__ slot_out,
     const double* __restrict__ rsd, const double* __restrict__ dshift_p, double inv_sqrt_n,
     double* __restrict__ y, double* __restrict__ beta_s, double* __restrict__ beta_l,
-    int32_t* __restrict__ status) {
-    const double dshift = *dshift_p;
+    int32_t* __restrict__ status, int32_t n_copies, int64_t m_stride, int64_t y_stride,
+    int64_t bs_stride, int64_t bl_stride, int64_t st_stride) {
+    // workgroup g: block order[g / n_copies] of factorisation copy g % n_copies (h2f tuning: all
+    // copies in one launch, each block's copies next to each other, largest blocks first)
+    const int g = static_cast<int>(blockIdx.x);
+    if (g >= n_blocks * n_copies) return;
+    const int c = g % n_copies;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const chol::BlockArgs a{blk_row0, blk_m, blk_ms, blk_ld, blk_matoff, blk_id, z_slot, slot_out,
-                            rsd, dshift, inv_sqrt_n, beta_s, beta_l, status};
-    if (static_cast<int>(blockIdx.x) >= n_blocks) return;
-    chol::large_block(a, M, y, order[blockIdx.x], lds);
+                            rsd, dshift_p[c], inv_sqrt_n, beta_s + c * bs_stride,
+                            beta_l + c * bl_stride, status + c * st_stride};
+    chol::large_block(a, M + c * m_stride, y + c * y_stride, order[g / n_copies], lds);
 }

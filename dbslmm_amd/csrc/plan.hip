@@ -1510,13 +1510,13 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
             HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
         }
-        for (int c = 0; c < n && p->n_large > 0; ++c) {
-            hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads),
-                               kCholLargeLds, s, p->d_M + c * p->M_elems, p->d_order, p->n_large,
+        if (p->n_large > 0) {   // every copy in one launch
+            hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large * n), dim3(chol::kLargeThreads),
+                               kCholLargeLds, s, p->d_M, p->d_order, p->n_large,
                                p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
-                               p->d_slot_out, p->d_rsd, p->d_dshift + c, isn, p->d_y + c * p->n_slots,
-                               p->d_beta_s + c * p->n_s, p->d_beta_l + c * p->n_l,
-                               p->d_status + c * p->nbk);
+                               p->d_slot_out, p->d_rsd, p->d_dshift, isn, p->d_y, p->d_beta_s, p->d_beta_l,
+                               p->d_status, n, p->M_elems, static_cast<int64_t>(p->n_slots), p->n_s, p->n_l,
+                               p->nbk);
             HIP_TRY(ctx, hipGetLastError());
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
