@@ -58,7 +58,7 @@ __device__ __forceinline__ bool factor_pipe(double* T, double* Xo, double* colb,
         // step j's column for columns j + 2 .. into LDS: one wave, so its LDS operations execute
         // in issue order, and the compiler keeps the store / loads (possibly aliasing addresses)
         // in program order
-        if (j + 2 < kT && !xlane) colb[kT * (j & 1) + r] = v[j];
+        if (j + 2 < kT) colb[kT * (j & 1) + r + (xlane ? 4 * kT : 0)] = v[j];   // X lanes: spare slots, no divergent store
         vjp = vj;
     }
     if (!xlane) {
@@ -75,7 +75,7 @@ __device__ __forceinline__ bool factor_pipe(double* T, double* Xo, double* colb,
 }
 __global__ void probe(const double* in, double* outT, double* outX, int* fl, int jmax, int pipe) {
     using namespace chol;
-    __shared__ double T[kT * kTS], X[kT * kTS], colb[2 * kT + 8];
+    __shared__ double T[kT * kTS], X[kT * kTS], colb[6 * kT + 8];
     const int lane = threadIdx.x;
     for (int e = lane; e < kT * kTS; e += 64) { T[e] = in[e]; X[e] = 0.0; }
     __syncthreads();
