@@ -8,15 +8,25 @@ beta in HBM.  Default workload = the configuration BASELINE.json's metric is quo
 EUR LD blocks, DBSLMM (large + small effects), h2 = 0.5 tuned over h2f in {0.8, 1.0, 1.2} (one
 Gram + three factorisations and solves per step).  --config 2 is the small configs[1] case.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--devices 0,0]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Multi-GPU (strong scaling, the default): ONE problem -- the same workload as N=1 -- with its LD
-blocks sharded over the ranks (longest processing time first on n_ref m(m+1) + m^3/3, each rank
-holding only its blocks' .bed rows, dbslmm_amd/dist.py); every step each rank solves its shard and
-the betas are gathered to rank 0 with one RCCL `gather` (the path's only exchange).  value = the
-problem's SNPs / the max-over-ranks time.  --replicas: N independent copies of the workload
-(seed = 1 + rank, no exchange) -> weak scaling.  Rank 0 prints ONE JSON line.
+blocks sharded over the GPUs (longest processing time first on n_ref m(m+1) + m^3/3, each GPU
+holding only its blocks' .bed rows).  Two launch modes:
+
+* one process (`python bench.py --gpus N`, no WORLD_SIZE): the product's own multi-device context
+  (dbslmm_ctx_create_multi through dbslmm_amd.Context(list of devices)): one host thread per
+  device, every shard's betas copied straight into the caller's arrays.  --devices a,b,.. names
+  the device list (repeats allowed: `--gpus 2 --devices 0,0` rehearses two shards on one GPU);
+* one process per GPU under torch.distributed.run (WORLD_SIZE = N; implied --dist): each rank
+  solves its shard (dbslmm_amd/dist.py) and the betas are gathered to rank 0 with one RCCL
+  `gather` per step (the path's only exchange); value uses the max-over-ranks time.
+
+value = the problem's SNPs x steps / time.  For N > 1 the merged betas of the last step are checked
+against the oracle's direct solve on every block >= 2000 SNPs (max_dbeta_vs_cpu_ref.big_blocks).
+--replicas (torchrun): N independent copies of the workload (seed = 1 + rank, no exchange) -> weak
+scaling.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -46,6 +56,12 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--devices", default=None,
+                    help="one process, N > 1: device ordinals of the multi-device context, e.g. 0,1 or "
+                         "0,0 (a rehearsal on one GPU); default 0..gpus-1")
+    ap.add_argument("--dist", action="store_true",
+                    help="one process per GPU over torch.distributed (implied by a torchrun launch, "
+                         "WORLD_SIZE > 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS),
@@ -259,7 +275,21 @@ def cpu_leg(args, prob, res, sigmas, wl):
     dbeta = dict(max_abs=mx, normwise=nw, snps_compared=ncmp,
                  vs="CPU reference-faithful PCG (oracle) on the timed sample" +
                     (", every h2f solve" if sigmas else ""))
-    # beta check 2: every block >= 2000 SNPs vs the direct solve (all host cores per block)
+    dbeta["big_blocks"] = big_block_check(prob, res, sigmas)
+    return cpu, dbeta
+
+
+def big_block_check(prob, res, sigmas):
+    """beta check on every block >= 2000 SNPs vs the oracle's direct fp64 solve of the reference
+    equations (all host cores per block), every h2f solve; res = the full problem's results."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import ref_numpy as R
+    O.use_blas(True)
+    hi = host_info()
+    sig_list = sigmas if sigmas else [prob.sigma_s]
+    m_b = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
     big = np.flatnonzero(m_b >= 2000)
     O.blas_threads(hi["threads_all"])
     bmx, bnw, bsn = 0.0, 0.0, 0
@@ -289,11 +319,10 @@ def cpu_leg(args, prob, res, sigmas, wl):
                 bsn += ref.size
     finally:
         O.blas_threads(1)
-    dbeta["big_blocks"] = dict(blocks=int(big.size), max_m=int(m_b.max()), snps_compared=bsn,
-                               max_abs=bmx, normwise_per_block_max=bnw, seconds=time.perf_counter() - t0,
-                               vs="oracle direct fp64 solve (Cholesky) of the reference equations, "
-                                  "every block >= 2000 SNPs" + (", every h2f solve" if sigmas else ""))
-    return cpu, dbeta
+    return dict(blocks=int(big.size), max_m=int(m_b.max()), snps_compared=bsn,
+                max_abs=bmx, normwise_per_block_max=bnw, seconds=time.perf_counter() - t0,
+                vs="oracle direct fp64 solve (Cholesky) of the reference equations, "
+                   "every block >= 2000 SNPs" + (", every h2f solve" if sigmas else ""))
 
 
 def e2e_leg(args, panel):
@@ -349,12 +378,17 @@ def main():
     dist = None
     if args.rank_device is not None:
         local = args.rank_device
+    # one process: the product's multi-device context over `devices` (N = len(devices))
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
     if world > 1:
+        devices = [local]
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
     else:
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(devices[0])
+    in_proc = world == 1 and len(devices) > 1
+    n_gpus = world if world > 1 else len(devices)
     cdev = "cuda" if args.dist_backend == "nccl" else "cpu"    # collective tensors
 
     from dbslmm_amd import Context, KERNEL_NAMES, Plan, synth
@@ -364,14 +398,18 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def sync_all():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
     sharded = world > 1 and not args.replicas
     panel = synth.simulate(args.snps, args.n_ref, pop=args.pop, seed=1 if sharded else 1 + rank,
-                           engine=args.gen, device=local if world > 1 else 0)
+                           engine=args.gen, device=devices[0])
     full = synth.make_problem(panel, lmm_only=args.lmm_only)
     for kv in args.opt:
         k, v = kv.split("=", 1)
         full.opts[k] = float(v) if k == "cheb_tol" else int(v)
-    if world > 1 or args.no_e2e:
+    if world > 1 or in_proc or args.no_e2e:
         del panel
     sigmas = [full.sigma_s * f for f in args.h2f] if args.h2f else None
     gather = None
@@ -381,7 +419,7 @@ def main():
         prob, s_idx, l_idx = sub_problem(full, shards[rank], compact=True)
     else:
         prob = full
-    ctx = Context(local if world > 1 else 0)
+    ctx = Context(devices if in_proc else devices[0])
     plan = Plan(ctx, prob)
     wl = plan.workload()
     if sharded:
@@ -397,37 +435,45 @@ def main():
         if sigmas:
             res = plan.run_multi(sigmas, out=outs)   # one Gram, len(sigmas) solves (synchronous)
             if gather:
-                gather([(r[0], r[1]) for r in res])
-        elif gather:
+                return gather([(r[0], r[1]) for r in res])
+            return res
+        if gather:
             plan.run()
             bs, bl, _ = plan.download()
-            gather([(bs, bl)])
-        else:
-            plan.run()
+            return gather([(bs, bl)])
+        plan.run()
+        return None
 
     for _ in range(args.warmup):
         step()
     plan.sync()
-    torch.cuda.synchronize()
+    sync_all()
     barrier()
-    torch.cuda.synchronize()
+    sync_all()
     plan.enable_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     plan.sync()
-    torch.cuda.synchronize()
+    sync_all()
     barrier()
-    torch.cuda.synchronize()
+    sync_all()
     elapsed = time.perf_counter() - t0
     wl = plan.workload()                      # + the h2f iteration count of the runs
     kms, nlaunch = plan.kernel_ms()
     kms = kms * nlaunch / args.steps          # per step (a tuning step is len(h2f) runs)
-    if sigmas:   # every h2f solve of the last step is compared with the CPU reference
+    # the results of one more step, compared with the CPU reference below (every h2f solve)
+    if sigmas:
         res = plan.run_multi(sigmas)
     else:
+        plan.run()
         res = [plan.download()]
     status = res[0][2]
+    full_res = res if world == 1 else None    # the full problem's betas (rank 0)
+    if gather:
+        merged = gather([(r[0], r[1]) for r in res])
+        if rank == 0:
+            full_res = [(bs, bl, None) for bs, bl in merged]
     st = torch.tensor([int(np.sum((status != 0) & (status != 1)))], dtype=torch.int64, device=cdev)
     if dist is not None:
         dist.all_reduce(st, op=dist.ReduceOp.SUM)
@@ -443,7 +489,7 @@ def main():
 
     n_solve = len(sigmas) if sigmas else 1
     kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl, n_solve) for k in range(len(KERNEL_NAMES))]
-    if world == 1 and not args.no_isolated:
+    if n_gpus == 1 and not args.no_isolated:
         # The lead group's unpack, Gram and factorisation overlap the others', so the phase spans
         # above include that contention.  One untimed plan with the lead group off times every
         # phase without it (outside the timed region; reported beside the spans, never as `value`).
@@ -464,22 +510,40 @@ def main():
                               span_note="ms = the phase's wall span in the timed (overlapped) schedule; "
                                         "alone_* = the same phase with the lead group off (untimed run)")
     dom = max(kernels, key=lambda r: r["ms"])
-    traffic, tsrc = pmc_traffic(dom["kernel"], args, n_solve)
+    traffic, tsrc = pmc_traffic(dom["kernel"], args, n_solve) if n_gpus == 1 else (None, None)
     roof = dict(bound=dom["bound"], achieved=dom["achieved"], peak=dom["peak"], unit=dom["unit"],
-                frac=dom["frac"], traffic=traffic, kernel=dom["kernel"], traffic_source=tsrc)
+                frac=dom["frac"], traffic=traffic, kernel=dom["kernel"], traffic_source=tsrc,
+                ms=dom["ms"], alone_ms=dom.get("alone_ms"), alone_achieved=dom.get("alone_achieved"),
+                alone_frac=dom.get("alone_frac"),
+                note="achieved / frac on the phase's wall span in the timed schedule (overlapped with "
+                     "other phases); alone_* = the same phase timed without the lead-group overlap")
 
     cpu = None
     dbeta = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         cpu, dbeta = cpu_leg(args, prob, res, sigmas, wl)
+    elif rank == 0 and full_res is not None and not args.replicas and not args.no_cpu_baseline:
+        dbeta = dict(big_blocks=big_block_check(full, full_res, sigmas),
+                     note=f"merged betas of the {n_gpus}-GPU solve (cpu_baseline is timed at N = 1 only)")
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and n_gpus == 1 and not args.no_e2e:
         e2e = e2e_leg(args, panel)
         del panel
 
     if rank == 0:
+        if in_proc:
+            par = (f"LD blocks of one problem sharded over {n_gpus} GPU(s) {devices} by the product's "
+                   f"multi-device context (dbslmm_ctx_create_multi: LPT shards, one host thread per "
+                   f"device, betas copied from each device to the caller's arrays)")
+        elif args.replicas:
+            par = f"{world} independent replicas (no exchange)"
+        elif world > 1:
+            par = (f"LD blocks of one problem sharded over {world} GPU(s) (LPT, one process per GPU), "
+                   f"betas gathered to rank 0 by one RCCL gather per step")
+        else:
+            par = "1 GPU"
         line = {
-            "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": world,
+            "metric": METRIC, "value": value, "unit": "SNPs/s", "n_gpus": n_gpus,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak" if args.replicas else "strong", "vs_baseline": None, "dtype": "f64",
@@ -489,16 +553,13 @@ def main():
                                    f"h2=0.5 (BASELINE configs[{args.config - 1}])", "generator": args.gen,
                        "h2f": args.h2f, "options": dict(full.opts),
                        "snps_rank0": wl["snps"], "snps_total": total_snps, "n_ref": args.n_ref,
-                       "blocks_rank0": wl["blocks"],
+                       "blocks_rank0": wl["blocks"], "devices": devices if world == 1 else None,
                        "gram": "exact int8 dosages on v_mfma_i32_32x32x32_i8, fp64 epilogue",
                        "solve": "fp64 Cholesky of the joint per-block matrix" + (
                            "; h2f: tiled blocks factored once (base h2f), the other h2f solves by "
                            "%d Chebyshev iterations on that factor" % wl["cheb_iters"]
                            if wl["cheb_iters"] > 0 else ""),
-                       "parallelism": (f"{world} independent replicas (no exchange)" if args.replicas else
-                                       f"LD blocks of one problem sharded over {world} GPU(s) (LPT), "
-                                       f"betas gathered to rank 0 by one RCCL gather per step"
-                                       if world > 1 else "1 GPU")},
+                       "parallelism": par},
             "roofline": roof,
             "kernels": kernels,
             "cpu_baseline": cpu,

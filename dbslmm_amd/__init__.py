@@ -54,7 +54,9 @@ class Context:
 
     def cache_bed(self, bed):
         """Keep a device copy of this .bed image (dbslmm_ctx_cache_bed); bed_maf / plan_create on
-        the same array then skip their upload.  None releases it."""
+        the same array then skip their upload (a plan reads the cached image in place).  The
+        array is matched by address and length only: do not modify it while it is cached (call
+        cache_bed again after a change).  None releases it."""
         if bed is None:
             self._cached_bed = None
             self.check(self.lib.dbslmm_ctx_cache_bed(self.h, None, 0), "ctx_cache_bed")

@@ -211,6 +211,14 @@ static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diag
     ARG_CHECK(ctx, diags, "null diags");
     std::fill(diags, diags + static_cast<size_t>(n_test) * p->num_block, 0.0);
     auto& S = p->mp->shards;
+    // every shard's pending single-sigma re-run (graph captures) first, drained, then the variances
+    const int rc0 = fan_out(ctx, static_cast<int>(S.size()), [&](int d) -> int {
+        dbslmm_plan* q = S[d].plan;
+        if (S[d].blocks.empty() || !q->cheb_pending_var) return DBSLMM_OK;
+        const int r = variance_factor(q);
+        return r == DBSLMM_OK ? dbslmm_plan_sync(q) : r;
+    });
+    if (rc0 != DBSLMM_OK) return rc0;
     return fan_out(ctx, static_cast<int>(S.size()), [&](int d) -> int {
         DeviceShard& sh = S[d];
         if (sh.blocks.empty()) return DBSLMM_OK;

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -91,10 +92,12 @@ struct dbslmm_ctx {
     int n_cu = 256;                  // compute units (persistent substitution grid)
     std::string err;
     // device copy of a caller's .bed image (dbslmm_ctx_cache_bed): bed_maf and plan_create on the
-    // same host range (pointer and length) read it instead of uploading again
+    // same host range (pointer and length) read it instead of uploading again; a plan created from
+    // it shares the buffer (freed when the context and every such plan have released it)
     const uint8_t* bed_host = nullptr;
     int64_t bed_host_len = 0;
-    uint8_t* d_bed_cache = nullptr;
+    std::shared_ptr<uint8_t> bed_cache;
+    uint8_t* d_bed_cache = nullptr;    // bed_cache.get()
     std::vector<dbslmm_ctx*> subs;   // multi-device context (multi.hip): one context per device,
                                      // device = -1 and no streams of its own
 };
@@ -118,7 +121,8 @@ struct dbslmm_plan {
     int32_t n_slots = 0, n_nonempty = 0, n_tiles = 0;
     int64_t M_elems = 0;
     // device
-    uint8_t* d_bed = nullptr;
+    uint8_t* d_bed = nullptr;          // own upload, or the context's cached image (bed_shared)
+    std::shared_ptr<uint8_t> bed_shared;
     uint32_t* d_G = nullptr;   // Gp: 2-bit dosage codes, kpad / 16 dwords per slot
     int32_t *d_slot_pos = nullptr, *d_slot_block = nullptr, *d_slot_out = nullptr;
     double *d_z = nullptr, *d_S = nullptr, *d_mu = nullptr, *d_rsd = nullptr, *d_y = nullptr;
@@ -541,7 +545,7 @@ void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
         return;
     }
     (void)hipSetDevice(ctx->device);
-    if (ctx->d_bed_cache) (void)hipFree(ctx->d_bed_cache);
+    ctx->bed_cache.reset();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
@@ -562,14 +566,21 @@ int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len) {
     if (!ctx->subs.empty()) return DBSLMM_OK;   // multi-device: each device gets its own rows
     ARG_CHECK(ctx, (bed == nullptr) == (bed_len == 0) && bed_len >= 0, "bed / bed_len");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (ctx->d_bed_cache) HIP_TRY(ctx, hipFree(ctx->d_bed_cache));
+    ctx->bed_cache.reset();      // plans created from the old image keep their reference
     ctx->d_bed_cache = nullptr;
     ctx->bed_host = nullptr;
     ctx->bed_host_len = 0;
     if (!bed) return DBSLMM_OK;
-    HIP_TRY(ctx, hipMalloc(&ctx->d_bed_cache, bed_len + 16));
-    HIP_TRY(ctx, hipMemset(ctx->d_bed_cache + bed_len, 0, 16));
-    HIP_TRY(ctx, upload_staged(ctx->d_bed_cache, bed, bed_len, ctx->stream));
+    uint8_t* d = nullptr;
+    HIP_TRY(ctx, hipMalloc(&d, bed_len + 16));
+    const int dev = ctx->device;
+    ctx->bed_cache = std::shared_ptr<uint8_t>(d, [dev](uint8_t* q) {
+        (void)hipSetDevice(dev);
+        (void)hipFree(q);
+    });
+    HIP_TRY(ctx, hipMemset(d + bed_len, 0, 16));
+    HIP_TRY(ctx, upload_staged(d, bed, bed_len, ctx->stream));
+    ctx->d_bed_cache = d;
     ctx->bed_host = bed;
     ctx->bed_host_len = bed_len;
     return DBSLMM_OK;
@@ -584,6 +595,8 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     }
     (void)hipSetDevice(p->ctx->device);
     if (p->h_pin) (void)hipHostFree(p->h_pin);
+    if (p->bed_shared) p->d_bed = nullptr;      // the context's cached image: not ours to free
+    p->bed_shared.reset();
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
                     p->d_S, p->d_mu, p->d_rsd, p->d_y, p->d_flags, p->d_status, p->d_order,
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
@@ -912,8 +925,13 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         return DBSLMM_E_HIP;
     };
     if (e != hipSuccess) return fail("hipSetDevice");
-    if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
-    if ((e = bed_to_device(ctx, p->d_bed, pr->bed, pr->bed_len)) != hipSuccess) return fail("upload bed");
+    if (ctx->d_bed_cache && pr->bed == ctx->bed_host && pr->bed_len == ctx->bed_host_len) {
+        p->bed_shared = ctx->bed_cache;          // read-only: the cached image itself, no copy
+        p->d_bed = p->bed_shared.get();
+    } else {
+        if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
+        if ((e = bed_to_device(ctx, p->d_bed, pr->bed, pr->bed_len)) != hipSuccess) return fail("upload bed");
+    }
     // + kHT spare rows: a 256-row Gram tile may read past the last slot (results discarded)
     const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kHT) * (p->kpad / 4);
     if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
@@ -1598,6 +1616,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
 static int check_trsv(dbslmm_plan* p) {
     dbslmm_ctx* ctx = p->ctx;
     if (p->trsv_pending) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);   // synchronous copy / memset below
         int32_t werr = 0;
         HIP_TRY(ctx, hipMemcpy(&werr, p->d_tflags + p->n_tflags + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
         if (werr) HIP_TRY(ctx, hipMemset(p->d_tflags + p->n_tflags + 1, 0, sizeof(int32_t)));
@@ -1772,6 +1791,17 @@ int dbslmm_est(dbslmm_ctx* ctx, const dbslmm_problem* pr, double* beta_s, double
     return rc;
 }
 
+// The last h2f run iterated the last sigma's tiled blocks on another copy's factor and wrote no
+// matrix for them: re-run that sigma alone (Gram + factorisation) so the variance has its factor.
+// A multi-device plan does this for every shard (and waits) before any shard's variance starts,
+// so no shard captures a graph while another runs the variance's synchronous calls.
+static int variance_factor(dbslmm_plan* p) {
+    if (!p->cheb_pending_var) return DBSLMM_OK;
+    const double sg = p->sigma_run;
+    p->cheb_pending_var = false;
+    return run_impl(p, true, &sg, 1);
+}
+
 // Test-set variance: compact the test panel to the plan's slots and the
 // indicator-1 individuals, standardise (readSNPIm + nomalizeVec over n_test), then one
 // forward-substitution pass per block against the factor the solve left in d_M.
@@ -1782,14 +1812,7 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     if (!p->ran) { ctx->err = "plan_variance before plan_run"; return DBSLMM_E_STATE; }
     if (p->mp) return mp_variance(p, tp, diags, n_test_out);
     ARG_CHECK(ctx, tp && tp->bed && tp->indicator && tp->n_total > 0, "bad test panel");
-    if (p->cheb_pending_var) {
-        // the last h2f run iterated the last sigma's tiled blocks on another copy's factor and
-        // wrote no matrix for them: re-run that sigma alone (Gram + factorisation) for its factor
-        const double sg = p->sigma_run;
-        p->cheb_pending_var = false;
-        const int rc = run_impl(p, true, &sg, 1);
-        if (rc != DBSLMM_OK) return rc;
-    }
+    if (const int rc = variance_factor(p)) return rc;
     ARG_CHECK(ctx, p->n_s == 0 || tp->s_pos, "test panel s_pos missing");
     ARG_CHECK(ctx, p->n_l == 0 || tp->l_pos, "test panel l_pos missing");
     std::vector<int32_t> sel;
@@ -1823,6 +1846,9 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     for (int32_t s = 0; s < p->n_slots; ++s) cpos[s] = tpos[s] >= 0 ? s : -1;
     const size_t ndiag = static_cast<size_t>(n_test) * p->num_block;
     int rc = DBSLMM_OK;
+    // synchronous allocations and copies: ordered against other host threads' graph captures
+    // (several shards of a multi-device plan on one device)
+    std::lock_guard<std::mutex> lk(g_capture_mu);
     do {
         hipError_t e;
         if ((e = hipMalloc(&d_tbed, tp->bed_len + 16)) != hipSuccess ||

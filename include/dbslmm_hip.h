@@ -158,8 +158,12 @@ const char* dbslmm_last_error(const dbslmm_ctx* ctx);
  * buffers): dbslmm_bed_maf and dbslmm_plan_create calls that pass the same host range (bed,
  * bed_len) then read it instead of uploading again -- the reference reads the .bed once for the
  * MAF pass (IO::readBim, dtpr.cpp:93-102) and again per block in calcBlock (dbslmmfit.cpp:
- * 384-387).  The caller must not modify the buffer while it is cached.  bed == NULL releases the
- * copy.  A multi-device context ignores the call (each device holds only its shard's rows). */
+ * 384-387).  The cached image is matched by host pointer and length only: the caller must not
+ * modify the buffer, or free it and pass a new one at the same address, while it is cached
+ * (call this again, or with bed == NULL, after any change).  A plan created from the cached image
+ * reads it in place (no second device copy) and keeps it alive until the plan is destroyed, even
+ * if the context releases or replaces it.  bed == NULL releases the context's reference.  A
+ * multi-device context ignores the call (each device holds only its shard's rows). */
 int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len);
 
 /* DBSLMMFIT::est replacement: upload, solve, download, free.  beta_s has s_ptr[num_block]

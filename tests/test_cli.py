@@ -170,6 +170,125 @@ def test_cli_gpu_ids_shards_match_single_gpu(tmp_path):
     assert outs[0] == outs[1]
 
 
+def _filtered_panel(tmp_path, layout, seed=5):
+    """3-chromosome synthetic panel whose GEMMA summaries exercise every host filter of BatchRun:
+    swapped alleles and a wrong a2 (matchRef compares a1/a2 strictly, no strand flips:
+    scr/dtpr.cpp:387-392), SNPs absent from the .bim, summary MAFs that differ from the .bed MAF by
+    more than -mafMax and by exactly -mafMax (strict `<`, :389), plus SNPs outside the LD blocks
+    (addBlock's sequential [start, end) scan, :455-481): layout "tail" cuts the last block short
+    (its last SNPs are never assigned), "gap" removes a block in the middle of chromosome 20 (the
+    scan stalls there and nothing after it is assigned)."""
+    from dbslmm_amd import synth
+    panel = synth.simulate(7000, 250, pop="EUR", chroms=[19, 20, 21], seed=seed, large_every=3,
+                           miss_rate=0.002)
+    f = synth.write_plink(panel, str(tmp_path / "p"))
+    bim = R.read_bim(f["ref"], panel.n_ref, True)         # .bed MAF (IO::readBim, constr)
+    rng = np.random.default_rng(seed)
+    for key in ("s", "l"):
+        out = []
+        for line in open(f[key]).read().splitlines():
+            t = line.split("\t")
+            u = rng.random()
+            if u < 0.03:
+                t[5], t[6] = t[6], t[5]                       # allele flip: rejected
+            elif u < 0.04:
+                t[6] = "T"                                    # a2 mismatch
+            elif u < 0.07:
+                maf = bim[t[1]][3]                            # |maf_bim - maf| = 0.25: rejected
+                t[7] = "%.17g" % (maf + 0.25 if maf < 0.25 else maf - 0.25)
+            elif u < 0.09:
+                t[7] = "%.17g" % (bim[t[1]][3] + 0.2)         # boundary of the strict <
+            elif u < 0.10:
+                t[1] += "_absent"                             # not in the .bim
+            out.append("\t".join(t))
+        open(f[key], "w").write("\n".join(out) + "\n")
+    blocks = [list(b) for b in panel.blocks]
+    if layout == "tail":
+        bmax = int(panel.block.max())
+        last = np.flatnonzero(panel.block == bmax)
+        blocks[bmax][2] = int(panel.ps[last[-min(12, last.size - 1)]])   # its last SNPs fall outside
+    else:
+        c20 = [i for i, b in enumerate(blocks) if b[0] == 20]
+        del blocks[c20[len(c20) // 2]]
+    with open(f["b"], "w") as fb:
+        for c, s, e in blocks:
+            fb.write(f"chr{c}\t{s}\t{e}\n")
+    return panel, f, bim
+
+
+def _oracle_host(f, bim, maf_max):
+    """ref_numpy restatement of BatchRun's host steps (scr/dbslmm.cpp:252-317)."""
+    blocks = R.read_block(f["b"])
+    summ_s, summ_l = R.read_summ(f["s"]), R.read_summ(f["l"])
+    inter_s, good_s = R.match_ref(summ_s, bim, maf_max)
+    inter_l, good_l = R.match_ref(summ_l, bim, maf_max)
+    info_s, info_l = R.add_block(inter_s, blocks), R.add_block(inter_l, blocks)
+    bad = [f"{x.snp} 0" for x, g in zip(summ_s, good_s) if not g] + \
+          [f"{x.snp} 1" for x, g in zip(summ_l, good_l) if not g]
+    return blocks, inter_s, inter_l, info_s, info_l, bad
+
+
+@pytest.mark.parametrize("layout", ["tail", "gap"])
+def test_dry_run_filters_match_oracle_multichrom(tmp_path, layout):
+    """CPU: the CLI's host pipeline (-mafMax 1: no MAF pass) on the 3-chromosome panel with
+    allele mismatches, absent SNPs and out-of-block SNPs: block / SNP counts and .badsnps equal
+    the restatement's."""
+    panel, f, bim = _filtered_panel(tmp_path, layout)
+    bim1 = {k: (v[0], v[1], v[2], 0.0) for k, v in bim.items()}      # constr = false: maf 0
+    blocks, inter_s, inter_l, info_s, info_l, bad = _oracle_host(f, bim1, 1.0)
+    eff = str(tmp_path / "o")
+    r = run(["-s", f["s"], "-l", f["l"], "-r", f["ref"], "-b", f["b"], "-n", str(f["n"]), "-nsnp",
+             str(f["nsnp"]), "-h", "0.5", "-mafMax", "1", "-eff", eff, "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    assert f"dry-run: blocks {len(blocks)} small {len(info_s)} large {len(info_l)}" in r.stdout
+    assert len(info_s) < len(inter_s)                     # out-of-block SNPs were dropped
+    assert open(eff + ".badsnps").read().splitlines() == bad
+    assert len(bad) > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["tail", "gap"])
+def test_cli_filters_multichrom_match_oracle(tmp_path, layout):
+    """The drop-in CLI on the filtered 3-chromosome panel vs the oracle, row for row
+    (VERDICT r02 item 1a): the GPU MAF pass + matchRef (-mafMax 0.2, strict <), addBlock,
+    DBSLMMFIT::est and the writer (scr/dbslmm.cpp:252-364).  <eff>.txt: identical SNP / allele /
+    flag columns in the reference's order (large rows, then small), betas within 1e-10 normwise of
+    the oracle's direct fp64 solve; the default 6-digit file equals the precise file's values
+    through C's %g; .badsnps identical."""
+    panel, f, bim = _filtered_panel(tmp_path, layout)
+    blocks, inter_s, inter_l, info_s, info_l, bad = _oracle_host(f, bim, 0.2)
+    nb = len(blocks)
+    res = R.est(panel.bed, panel.n_ref, f["n"], 0.5 / f["nsnp"], nb, info_s, info_l, tau=0.8,
+                method="chol")
+    exp = R.format_eff(res)
+    base = ["-s", f["s"], "-l", f["l"], "-r", f["ref"], "-b", f["b"], "-n", str(f["n"]), "-nsnp",
+            str(f["nsnp"]), "-h", "0.5", "-mafMax", "0.2"]
+    precise, plain = str(tmp_path / "precise"), str(tmp_path / "plain")
+    r = run(base + ["-eff", precise, "--precise-out"], cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert f"After filtering, {len(inter_s)} small effect SNPs are selected." in r.stdout
+    r = run(base + ["-eff", plain], cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert open(plain + ".badsnps").read().splitlines() == bad
+    rows_p = [x.split() for x in open(precise + ".txt").read().splitlines()]
+    rows_g = [x.split() for x in open(plain + ".txt").read().splitlines()]
+    rows_e = [x.split() for x in exp]
+    assert len(rows_e) == len(info_s) + len(info_l) > 3000
+    key = lambda rows: [(x[0], x[1], x[4]) for x in rows]
+    assert key(rows_p) == key(rows_e) == key(rows_g)
+    got = np.array([float(x[2]) for x in rows_p])
+    ref = np.concatenate([res.beta_l, res.beta_s])
+    assert np.max(np.abs(got - ref)) <= 1e-10 * np.max(np.abs(ref))
+    noscl = np.array([float(x[3]) for x in rows_p])
+    maf = np.array([e["maf"] for e in info_l + info_s])
+    assert np.allclose(noscl, got / np.sqrt(2 * maf * (1 - maf)), rtol=1e-15, atol=0)
+    # the default writer is C's %g at precision 6 of the same doubles
+    assert [(x[2], x[3]) for x in rows_g] == [(R.format_g(float(x[2])), R.format_g(float(x[3])))
+                                              for x in rows_p]
+    # and the oracle's %g rows agree up to one unit in the 6th digit (beta differences ~1e-13)
+    assert sum(not rows_close(" ".join(a), " ".join(b)) for a, b in zip(rows_g, rows_e)) == 0
+
+
 @pytest.mark.gpu
 def test_cli_timing_and_mafmax_multichrom(tmp_path):
     """--timing prints the phase wall times as one JSON line on stderr; the run goes through the

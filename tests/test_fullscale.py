@@ -37,9 +37,9 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
 
 
-def _gpu_solve(prob, factors):
+def _gpu_solve(prob, factors, devices=0):
     from dbslmm_amd import Context, Plan
-    plan = Plan(Context(0), prob)
+    plan = Plan(Context(devices), prob)
     sig = [prob.sigma_s * f for f in factors]
     if len(sig) > 1:
         out = plan.run_multi(sig)
@@ -83,14 +83,22 @@ def _got(prob, res, b):
     return np.concatenate([s, bl[prob.l_ptr[b]:prob.l_ptr[b + 1]]])
 
 
-@pytest.mark.parametrize("cfg", sorted(CONFIGS))
-def test_fullscale_blocks_match_oracle(cfg):
+@pytest.mark.parametrize("cfg,devices", [(3, 0), (4, 0), (5, 0), (3, [0, 0])],
+                         ids=["3", "4", "5", "3-multi"])
+def test_fullscale_blocks_match_oracle(cfg, devices):
+    """devices = [0, 0]: the product's multi-device context (dbslmm_ctx_create_multi, LPT block
+    shards with compact per-device .bed images, one host thread per shard) on the test GPU twice;
+    its betas must also equal the one-device solve bit for bit."""
     from dbslmm_amd import synth
     snps, n_ref, pop, lmm, factors = CONFIGS[cfg]
     panel = synth.simulate(snps, n_ref, pop=pop, seed=1, engine="gpu")
     prob = synth.make_problem(panel, lmm_only=lmm)
     del panel
-    sig, out, wl = _gpu_solve(prob, factors)
+    sig, out, wl = _gpu_solve(prob, factors, devices)
+    if isinstance(devices, list):
+        _, one, _ = _gpu_solve(prob, factors, 0)
+        for (bs, bl, st), (bs1, bl1, st1) in zip(out, one):
+            assert np.array_equal(bs, bs1) and np.array_equal(bl, bl1) and np.array_equal(st, st1)
     m_b = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
     for bs, bl, st in out:
         assert np.all((st == 0) | ((st == 1) & (m_b == 0))), np.flatnonzero((st != 0) & (m_b > 0))

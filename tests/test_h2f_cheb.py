@@ -106,3 +106,28 @@ def test_run_multi_into_caller_buffers():
             np.testing.assert_array_equal(c, z)
     with pytest.raises(ValueError):
         plan.run_multi(sig, out=(out[0][:2], out[1], out[2]))
+
+
+@pytest.mark.parametrize("cheb_tol", [1e-7, 1e-9, 1e-11])
+def test_cheb_error_within_target(cheb_tol):
+    """The iteration count is fixed on the host from dbslmm_options.cheb_tol (error <= 2 q^K x the
+    initial error): every iterated copy must land within 10 x cheb_tol of
+    a fresh single-sigma solve, normwise (a bound tied to the target, so a change of
+    cheb_tol or of the iteration bounds cannot drift unnoticed), and a tighter target must not
+    take fewer iterations."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=9)
+    prob.opts.update(tiled_min=64, cheb_tol=cheb_tol)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    plan = Plan(Context(0), prob)
+    multi = plan.run_multi(sig)
+    iters = plan.workload()["cheb_iters"]
+    assert iters > 0
+    for c, (got, ref) in enumerate(zip(multi, _fresh(prob, sig))):
+        assert _finite_normwise(_cat(got), _cat(ref)) <= 10 * cheb_tol, (c, iters)
+    if cheb_tol < 1e-7:
+        loose = dict(prob.opts, cheb_tol=cheb_tol * 100)
+        prob.opts = loose
+        p2 = Plan(Context(0), prob)
+        p2.run_multi(sig)
+        assert p2.workload()["cheb_iters"] < iters

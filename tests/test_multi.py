@@ -76,18 +76,33 @@ def test_sharded_plan_run_multi_and_shards():
     assert n == 1 and ms[1] > 0
 
 
-def test_sharded_variance_matches_single():
+@pytest.mark.parametrize("h2f", [False, True])
+def test_sharded_variance_matches_single(h2f):
+    """h2f: the variance follows an h2f run_multi whose last sigma was solved by Chebyshev
+    iteration, so every shard re-runs that sigma (a graph capture) before its variance; the
+    shards share device 0, where one shard's capture must not meet another's synchronous
+    variance setup."""
     from test_variance import synth_variance_case
     from dbslmm_amd import Context, Plan
     prob, tbed, ind, tsp, tlp = synth_variance_case()
     prob.opts["tiled_min"] = 64
-    out = []
-    for dev in (0, [0, 0]):
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    out, betas = [], []
+    for dev in (0, [0, 0], [0, 0, 0]):
         plan = Plan(Context(dev), prob)
-        plan.run()
-        plan.sync()
+        if h2f:
+            betas.append(plan.run_multi(sig))
+            assert plan.workload()["cheb_iters"] > 0
+        else:
+            plan.run()
+            plan.sync()
         out.append(plan.variance(tbed, ind, tsp, tlp))
-    np.testing.assert_array_equal(out[0], out[1])
+    for o in out[1:]:
+        np.testing.assert_array_equal(out[0], o)
+    for b in betas[1:]:
+        for x, y in zip(betas[0], b):
+            for u, v in zip(x, y):
+                np.testing.assert_array_equal(u, v)
 
 
 def test_sharded_bed_maf_and_tools():

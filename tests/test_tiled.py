@@ -219,3 +219,33 @@ def test_block_beyond_16k_snps():
     bs, bl, st = plan.download()
     assert np.all(st == 0)
     assert normwise(np.concatenate([bs, bl]), ref[1]) < 1e-9
+
+
+def test_block_at_tiled_size_cap():
+    """One LD block of 32,639 SNPs, the largest the tiled path takes (m < 32,640 = 255 x 128):
+    the 128-row tile / region indices reach 254 and the substitution's 64-row tile count 510, at
+    the edges of the packed work-item fields.  Chebyshev h2f copies vs the direct
+    fp64 solve; one SNP more is rejected at plan creation with the stated error."""
+    from dbslmm_amd import Context, DbslmmError, Plan
+    from test_fullscale import _block_ref, _threads
+    cap = 255 * 128
+    prob = _problem(seed=19, n_ref=128, sizes=[cap - 1])
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    ctx = Context(0)
+    plan = Plan(ctx, prob)
+    multi = plan.run_multi(sig)
+    assert plan.workload()["cheb_iters"] > 0
+    plan.close()
+    thr = _threads()
+    O.use_blas(True)
+    O.blas_threads(thr)
+    try:
+        ref = _block_ref(prob, 0, sig, thr, pcg=False)["chol"]
+    finally:
+        O.blas_threads(1)
+    for c in range(3):
+        assert np.all(multi[c][2] == 0)
+        assert normwise(np.concatenate([multi[c][0], multi[c][1]]), ref[c]) < 1e-9, c
+    over = _problem(seed=19, n_ref=128, sizes=[cap])
+    with pytest.raises(DbslmmError, match="m must be < 32640"):
+        Plan(ctx, over)

@@ -331,3 +331,38 @@ def test_cli_writes_variance_txt(tmp_path, drop):
     assert np.array_equal(np.isnan(got), np.isnan(D))
     fin = np.isfinite(D)
     assert _colwise(np.where(fin, got, 0.0), np.where(fin, D, 0.0)) < TOL
+
+
+@pytest.mark.gpu
+def test_cli_h2f_sharded_variance_matches_one_gpu(tmp_path):
+    """-h2f 0.8,1,1.2 with -dat_str/-test_indicator_file: the variance of the last factor after a
+    Chebyshev h2f run (the shards re-run that sigma before the variance).  --gpu-ids 0,0 (two
+    shards on the test GPU, one of them idle: test_dat is one LD block) writes the same
+    variance.txt and <eff> files byte for byte as one GPU."""
+    import subprocess
+    from _common import ROOT
+    from test_cli import REF, SUMM, split_summary
+    v = td_variance_problem(False, drop_test_mono=True)
+    summ = str(tmp_path / "summ.txt")
+    with open(SUMM) as f, open(summ, "w") as o:
+        for line in f:
+            if line.split("\t")[1] not in v["dropped"]:
+                o.write(line)
+    s, l = split_summary(tmp_path, summ)
+    ind = str(tmp_path / "ind.txt")
+    open(ind, "w").write("".join(f"{x}\n" for x in v["ind"]))
+    cli = os.path.join(ROOT, "dbslmm_amd", "bin", "dbslmm")
+    outs = []
+    for name, extra in (("one", []), ("two", ["--gpu-ids", "0,0"])):
+        d = tmp_path / name
+        d.mkdir()
+        r = subprocess.run([cli, "-s", s, "-l", l, "-r", REF, "-b", BLOCKS_EUR1, "-n", "2400", "-nsnp",
+                            "996", "-h", "0.5", "-h2f", "0.8,1,1.2", "-mafMax", "0.2", "-eff",
+                            str(d / "o.dbslmm"), "-dat_str", os.path.join(TD, "test_chr1"),
+                            "-test_indicator_file", ind] + extra,
+                           capture_output=True, text=True, cwd=str(d), timeout=300)
+        assert r.returncode == 0, r.stderr
+        outs.append([open(d / f).read() for f in ("variance.txt", "o_h2f0.8.dbslmm.txt",
+                                                  "o_h2f1.dbslmm.txt", "o_h2f1.2.dbslmm.txt")])
+    assert outs[0] == outs[1]
+    assert read_arma_ascii(str(tmp_path / "one" / "variance.txt")).size > 0
