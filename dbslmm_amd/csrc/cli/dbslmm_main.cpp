@@ -21,6 +21,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -55,9 +58,16 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
 };
 
-struct Allele { int64_t pos; string a1, a2; double maf; };                 // ALLELE
-struct Summ { string snp; long ps; string a1, a2; double maf, z; };        // SUMM (P unused)
-struct Info { string snp; long ps; int64_t pos; int block; string a1; double maf, z; };  // INFO
+// The host rows keep string_views into the mmap'd input files (no per-SNP allocation).
+struct Bim {                        // map<string, ALLELE> of IO::readBim: line index = .bed row
+    vector<string_view> snp, a1, a2;
+    vector<char> bad;               // fewer than 6 fields: not inserted (the row still counts)
+    vector<double> maf;             // GPU MAF pass (constr), else empty (0.0)
+    StrIndex idx;                   // snp -> first line with it (std::map::insert keeps the first)
+};
+struct Summ { string_view snp, a1, a2; long ps; double maf, z; };         // SUMM (P unused)
+struct Pos { int32_t summ; long ps; int64_t pos; };                       // POS: row of the summary
+struct Info { int32_t summ; long ps; int64_t pos; int block; };           // INFO (fields via summ)
 
 double walltime() {
     struct timeval tv;
@@ -136,94 +146,100 @@ void assign(int argc, char** argv, Param& p) {
     }
 }
 
-// IO::readBim (scr/dtpr.cpp:83-123): maf from the GPU MAF pass when constr.  Lines are split on
-// several threads; the map keeps the first occurrence of a SNP id, as std::map::insert does.
-bool read_bim(const string& ref, const vector<double>& maf, std::unordered_map<string, Allele>& bim,
-              vector<string>& order) {
-    const string text = read_file(ref + ".bim");
-    if (text.empty()) { std::ifstream f(ref + ".bim"); return static_cast<bool>(f); }
-    const vector<string_view> lines = lines_of(text);
+// IO::readBim (scr/dtpr.cpp:83-123): fields 1 (SNP), 4 (a1), 5 (a2) of each tab-separated line,
+// parsed on several threads into views of the mapped file; the SNP index is built concurrently.
+bool read_bim(const MappedText& f, Bim& bim) {
+    if (!f.ok) return false;
+    const unsigned T = host_threads();
     struct Row { string_view snp, a1, a2; bool ok; };
-    vector<Row> rows(lines.size());
-    parallel_chunks(lines.size(), host_threads(), [&](size_t lo, size_t hi) {
-        vector<string_view> t;
-        for (size_t i = lo; i < hi; ++i) {
-            split_view(lines[i], '\t', t);
-            rows[i] = t.size() < 6 ? Row{{}, {}, {}, false} : Row{t[1], t[4], t[5], true};
-        }
+    vector<vector<Row>> part(T);
+    const vector<size_t> cnt = parallel_lines(f.text, T, [&](unsigned t, string_view line) {
+        string_view fl[6];
+        part[t].push_back(tab_fields(line, fl, 6) < 6 ? Row{{}, {}, {}, false} : Row{fl[1], fl[4], fl[5], true});
     });
-    bim.reserve(rows.size());
-    for (size_t count = 0; count < rows.size(); ++count) {
-        const Row& r = rows[count];
-        if (!r.ok) continue;
-        const double m = count < maf.size() ? maf[count] : 0.0;
-        auto ins = bim.emplace(string(r.snp), Allele{static_cast<int64_t>(count), string(r.a1), string(r.a2), m});
-        if (ins.second) order.push_back(ins.first->first);
-    }
+    size_t n = 0;
+    for (size_t c : cnt) n += c;
+    bim.snp.resize(n);
+    bim.a1.resize(n);
+    bim.a2.resize(n);
+    bim.bad.assign(n, 0);
+    vector<size_t> off(part.size() + 1, 0);
+    for (size_t t = 0; t < part.size(); ++t) off[t + 1] = off[t] + part[t].size();
+    parallel_chunks(part.size(), static_cast<unsigned>(part.size()), [&](size_t lo, size_t hi) {
+        for (size_t t = lo; t < hi; ++t)
+            for (size_t k = 0; k < part[t].size(); ++k) {
+                const Row& r = part[t][k];
+                const size_t i = off[t] + k;
+                bim.snp[i] = r.snp;
+                bim.a1[i] = r.a1;
+                bim.a2[i] = r.a2;
+                bim.bad[i] = !r.ok;
+            }
+    });
+    bim.idx.build(n, T, [&](size_t i) { return bim.snp[i]; }, &bim.bad);
     return true;
+}
+size_t bim_size(const Bim& bim) {             // distinct SNP ids (std::map size)
+    size_t n = 0;
+    for (const auto& s : bim.idx.slot) n += s.load(std::memory_order_relaxed) >= 0;
+    return n;
 }
 
 // IO::readSumm (scr/dtpr.cpp:178-220): GEMMA, no header; z = beta/se when se starts with a digit
-// and > 1e-20, else 0.  Parsed in contiguous line chunks on several threads, kept in file order.
-vector<Summ> read_summ(const string& path) {
-    const string text = read_file(path);
-    const vector<string_view> lines = lines_of(text);
-    vector<Summ> rows(lines.size());
-    vector<char> ok(lines.size(), 0);
-    parallel_chunks(lines.size(), host_threads(), [&](size_t lo, size_t hi) {
-        vector<string_view> t;
-        for (size_t i = lo; i < hi; ++i) {
-            split_view(lines[i], '\t', t);
-            if (t.size() < 11) continue;
-            Summ& s = rows[i];
-            s.z = 0.0;
-            const string se_s(t[9]), b_s(t[8]), ps_s(t[2]), af_s(t[7]);
-            if (isdigit(static_cast<unsigned char>(se_s.c_str()[0]))) {
-                const double se = atof(se_s.c_str());
-                if (se - 0.0 > 1e-20) s.z = atof(b_s.c_str()) / se;
-            }
-            s.snp = string(t[1]);
-            s.ps = atol(ps_s.c_str());
-            s.a1 = string(t[5]);
-            s.a2 = string(t[6]);
-            const double af = atof(af_s.c_str());
-            s.maf = std::min(af, 1.0 - af);
-            ok[i] = 1;
+// and > 1e-20, else 0.  Parsed in line chunks on several threads, kept in file order.
+vector<Summ> read_summ(const MappedText& f) {
+    const unsigned T = host_threads();
+    vector<vector<Summ>> part(T);
+    parallel_lines(f.text, T, [&](unsigned t, string_view line) {
+        string_view fl[11];
+        if (tab_fields(line, fl, 11) < 11) return;
+        Summ s;
+        s.z = 0.0;
+        if (!fl[9].empty() && isdigit(static_cast<unsigned char>(fl[9][0]))) {
+            const double se = field_atof(fl[9]);
+            if (se - 0.0 > 1e-20) s.z = field_atof(fl[8]) / se;
         }
+        s.snp = fl[1];
+        s.ps = field_atol(fl[2]);
+        s.a1 = fl[5];
+        s.a2 = fl[6];
+        const double af = field_atof(fl[7]);
+        s.maf = std::min(af, 1.0 - af);
+        part[t].push_back(s);
     });
     vector<Summ> out;
-    out.reserve(rows.size());
-    for (size_t i = 0; i < rows.size(); ++i)
-        if (ok[i]) out.push_back(std::move(rows[i]));
+    size_t n = 0;
+    for (const auto& v : part) n += v.size();
+    out.reserve(n);
+    for (const auto& v : part) out.insert(out.end(), v.begin(), v.end());
     return out;
 }
-
-struct Pos { string snp; long ps; int64_t pos; string a1; double maf, z; };
 
 // SNPPROC::matchRef (scr/dtpr.cpp:383-408): strict allele equality, |maf_ref - maf| < mafMax.
 // A SNP absent from the .bim compares against a default ALLELE ("", "", 0.0) as the reference's
 // operator[] does, and is never kept.
-vector<Pos> match_ref(const vector<Summ>& summ, const std::unordered_map<string, Allele>& bim,
-                      double maf_max, vector<char>& good) {
+vector<Pos> match_ref(const vector<Summ>& summ, const Bim& bim, double maf_max, vector<char>& good) {
     good.assign(summ.size(), 0);
-    static const Allele empty{0, "", "", 0.0};
     const unsigned T = host_threads();
     vector<vector<Pos>> part(T);
     vector<int> dis_t(T, 0), maf_t(T, 0);
     vector<size_t> lo_t(T + 1, 0);
     for (unsigned t = 0; t <= T; ++t) lo_t[t] = summ.size() * t / T;
+    auto key = [&](size_t i) { return bim.snp[i]; };
     vector<std::thread> th;
     for (unsigned t = 0; t < T; ++t)
         th.emplace_back([&, t] {
             for (size_t i = lo_t[t]; i < lo_t[t + 1]; ++i) {
-                auto it = bim.find(summ[i].snp);
-                const Allele& b = it == bim.end() ? empty : it->second;
-                const bool a1 = b.a1 == summ[i].a1, a2 = b.a2 == summ[i].a2;
-                const bool mb = std::fabs(b.maf - summ[i].maf) < maf_max;
+                const Summ& s = summ[i];
+                const int32_t r = bim.idx.find(s.snp, key);
+                const string_view b1 = r >= 0 ? bim.a1[r] : string_view(), b2 = r >= 0 ? bim.a2[r] : string_view();
+                const double bm = r >= 0 && !bim.maf.empty() ? bim.maf[r] : 0.0;
+                const bool a1 = b1 == s.a1, a2 = b2 == s.a2;
+                const bool mb = std::fabs(bm - s.maf) < maf_max;
                 if (!a1 || !a2) ++dis_t[t];
                 if (!mb) ++maf_t[t];
-                if (a1 && a2 && mb && it != bim.end()) {
-                    part[t].push_back({summ[i].snp, summ[i].ps, b.pos, summ[i].a1, summ[i].maf, summ[i].z});
+                if (a1 && a2 && mb && r >= 0) {
+                    part[t].push_back({static_cast<int32_t>(i), s.ps, static_cast<int64_t>(r)});
                     good[i] = 1;
                 }
             }
@@ -231,10 +247,13 @@ vector<Pos> match_ref(const vector<Summ>& summ, const std::unordered_map<string,
     for (auto& x : th) x.join();
     vector<Pos> inter;
     int dis = 0, mafc = 0;
+    size_t n = 0;
+    for (unsigned t = 0; t < T; ++t) n += part[t].size();
+    inter.reserve(n);
     for (unsigned t = 0; t < T; ++t) {
         dis += dis_t[t];
         mafc += maf_t[t];
-        for (auto& e : part[t]) inter.push_back(std::move(e));
+        inter.insert(inter.end(), part[t].begin(), part[t].end());
     }
     std::cout << "Number of allele discrepency: " << dis << "\n";
     std::cout << "Number of maf discrepency:    " << mafc << "\n";
@@ -245,12 +264,12 @@ vector<Pos> match_ref(const vector<Summ>& summ, const std::unordered_map<string,
 // dropped.
 vector<Info> add_block(const vector<Pos>& inter, const vector<Block>& blocks) {
     vector<Info> out;
+    out.reserve(inter.size());
     size_t count = 0;
     for (size_t i = 0; i < blocks.size(); ++i) {
         for (size_t j = count; j < inter.size(); ++j) {
             if (inter[j].ps >= blocks[i].start && inter[j].ps < blocks[i].end) {
-                out.push_back({inter[j].snp, inter[j].ps, inter[j].pos, static_cast<int>(i),
-                               inter[j].a1, inter[j].maf, inter[j].z});
+                out.push_back({inter[j].summ, inter[j].ps, inter[j].pos, static_cast<int>(i)});
                 ++count;
             } else {
                 break;
@@ -260,7 +279,8 @@ vector<Info> add_block(const vector<Pos>& inter, const vector<Block>& blocks) {
     return out;
 }
 
-void to_csr(const vector<Info>& info, int nb, vector<int64_t>& ptr, vector<int32_t>& pos, vector<double>& z) {
+void to_csr(const vector<Info>& info, const vector<Summ>& summ, int nb, vector<int64_t>& ptr,
+            vector<int32_t>& pos, vector<double>& z) {
     ptr.assign(nb + 1, 0);
     for (const auto& e : info) ptr[e.block + 1]++;
     for (int b = 0; b < nb; ++b) ptr[b + 1] += ptr[b];
@@ -268,7 +288,7 @@ void to_csr(const vector<Info>& info, int nb, vector<int64_t>& ptr, vector<int32
     z.resize(info.size());
     for (size_t i = 0; i < info.size(); ++i) {   // info is in block order (addBlock)
         pos[i] = static_cast<int32_t>(info[i].pos);
-        z[i] = info[i].z;
+        z[i] = summ[info[i].summ].z;
     }
 }
 
@@ -312,8 +332,8 @@ vector<int32_t> read_indicator(const string& path) {
 // calcBlock pairs the i-th SNP of a block with the i-th test SNP of the same block
 // (test_info_s_block[i].pos, scr/dbslmmfit.cpp:394-396); a block with fewer test SNPs is an
 // out-of-range read in the reference and an error here.
-bool align_test_pos(const vector<Info>& info, const vector<Info>& t_info, int nb, vector<int32_t>& out,
-                    string& err) {
+bool align_test_pos(const vector<Info>& info, const vector<Info>& t_info, const vector<Summ>& summ, int nb,
+                    vector<int32_t>& out, string& err) {
     vector<vector<int64_t>> per(nb);
     for (const auto& e : t_info) per[e.block].push_back(e.pos);
     vector<size_t> used(nb, 0);
@@ -321,7 +341,8 @@ bool align_test_pos(const vector<Info>& info, const vector<Info>& t_info, int nb
     for (size_t i = 0; i < info.size(); ++i) {
         const int b = info[i].block;
         if (used[b] >= per[b].size()) {
-            err = "block " + std::to_string(b) + ": SNP " + info[i].snp + " has no counterpart in the test .bim";
+            err = "block " + std::to_string(b) + ": SNP " + string(summ[info[i].summ].snp) +
+                  " has no counterpart in the test .bim";
             return false;
         }
         out[i] = static_cast<int32_t>(per[b][used[b]++]);
@@ -362,11 +383,14 @@ int fail(const string& msg) {
 struct Phases {
     double t0 = walltime(), last = t0;
     string json;
+    void put(const char* name, double sec) {
+        char buf[96];
+        snprintf(buf, sizeof(buf), "%s\"%s\": %.6f", json.empty() ? "" : ", ", name, sec);
+        json += buf;
+    }
     void mark(const char* name) {
         const double t = walltime();
-        char buf[96];
-        snprintf(buf, sizeof(buf), "%s\"%s\": %.6f", json.empty() ? "" : ", ", name, t - last);
-        json += buf;
+        put(name, t - last);
         last = t;
     }
     void print(int64_t n_snp) const {
@@ -374,6 +398,106 @@ struct Phases {
                 static_cast<long long>(n_snp));
     }
 };
+
+namespace {
+// getRow (scr/dtpr.cpp:71-80) of a mapped text: the number of getline lines
+int64_t count_lines(string_view t) {
+    std::atomic<int64_t> total{0};
+    parallel_chunks(t.size(), host_threads(), [&](size_t lo, size_t hi) {
+        int64_t n = 0;
+        for (size_t i = lo; i < hi;) {
+            const void* e = memchr(t.data() + i, '\n', hi - i);
+            if (!e) break;
+            ++n;
+            i = static_cast<size_t>(static_cast<const char*>(e) - t.data()) + 1;
+        }
+        total += n;
+    });
+    return total + (!t.empty() && t.back() != '\n' ? 1 : 0);
+}
+
+// One <eff>.txt per h2f factor (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small
+// rows, "snp a1 beta beta_noscl flag"; ostream's default double format = printf %g at precision 6
+// (17 with --precise-out), produced by std::to_chars (the same digits, ~3x faster than snprintf).
+// All files and row chunks are formatted on the host threads, then written at their offsets.
+struct EffList { const vector<Info>* info; const vector<Summ>* summ; const double* beta; int flag; };
+bool write_eff_files(const vector<string>& names, const vector<std::array<EffList, 2>>& lists, int prec) {
+    const unsigned T = host_threads();
+    struct Task { size_t file; int list; size_t lo, hi; string out; };
+    vector<Task> tasks;
+    for (size_t f = 0; f < names.size(); ++f)
+        for (int l = 0; l < 2; ++l) {
+            const size_t n = lists[f][l].info->size();
+            const size_t k = std::max<size_t>(1, std::min<size_t>(T, n / 2048 + 1));
+            for (size_t c = 0; c < k; ++c) tasks.push_back({f, l, n * c / k, n * (c + 1) / k, {}});
+        }
+    std::atomic<size_t> next{0};
+    auto fmt = [&] {
+        char num[64];
+        for (size_t t; (t = next.fetch_add(1)) < tasks.size();) {
+            Task& k = tasks[t];
+            const EffList& L = lists[k.file][k.list];
+            string& o = k.out;
+            o.reserve((k.hi - k.lo) * 56);
+            for (size_t i = k.lo; i < k.hi; ++i) {
+                const Summ& s = (*L.summ)[(*L.info)[i].summ];
+                const double b = L.beta[i];
+                const double noscl = b / std::sqrt(2 * s.maf * (1 - s.maf));
+                if (std::isinf(noscl)) continue;
+                o.append(s.snp.data(), s.snp.size());
+                o += ' ';
+                o.append(s.a1.data(), s.a1.size());
+                o += ' ';
+                o.append(num, std::to_chars(num, num + sizeof(num), b, std::chars_format::general, prec).ptr);
+                o += ' ';
+                o.append(num, std::to_chars(num, num + sizeof(num), noscl, std::chars_format::general, prec).ptr);
+                o += L.flag ? " 1\n" : " 0\n";
+            }
+        }
+    };
+    {
+        vector<std::thread> th;
+        for (unsigned t = 1; t < T; ++t) th.emplace_back(fmt);
+        fmt();
+        for (auto& x : th) x.join();
+    }
+    vector<int> fd(names.size(), -1);
+    vector<off_t> off(tasks.size(), 0);
+    bool ok = true;
+    for (size_t f = 0; f < names.size(); ++f) {
+        fd[f] = ::open((names[f] + ".txt").c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        ok = ok && fd[f] >= 0;
+    }
+    off_t pos = 0;
+    for (size_t t = 0; t < tasks.size(); ++t) {
+        if (t > 0 && tasks[t].file != tasks[t - 1].file) pos = 0;
+        off[t] = pos;
+        pos += static_cast<off_t>(tasks[t].out.size());
+    }
+    std::atomic<bool> wok{true};
+    if (ok) {
+        next = 0;
+        auto wr = [&] {
+            for (size_t t; (t = next.fetch_add(1)) < tasks.size();) {
+                const string& o = tasks[t].out;
+                size_t done = 0;
+                while (done < o.size()) {
+                    const ssize_t w = pwrite(fd[tasks[t].file], o.data() + done, o.size() - done, off[t] + done);
+                    if (w <= 0) { wok = false; break; }
+                    done += static_cast<size_t>(w);
+                }
+            }
+        };
+        vector<std::thread> th;
+        for (unsigned t = 1; t < std::min<unsigned>(T, 8); ++t) th.emplace_back(wr);
+        wr();
+        for (auto& x : th) x.join();
+    }
+    for (int d : fd)
+        if (d >= 0) ok = (::close(d) == 0) && ok;
+    return ok && wok;
+}
+}  // namespace
 
 int main(int argc, char** argv) {
     Phases ph;
@@ -398,67 +522,109 @@ int main(int argc, char** argv) {
     if (p.t > 100 || p.t < 1) return fail("-t is not correct (1, 100)!");
     if (p.eff.empty()) return fail("-eff is no parameter!");
     if (p.nsnp <= 0 || p.n <= 0) return fail("-n and -nsnp must be positive!");
+    const bool has_lfile = static_cast<bool>(lf);
+    sf.close();
+    lf.close();
+    rf.close();
+    bf.close();
 
     std::cout << "Reading reference PLINK FAM file from [" << p.r << ".fam]\n";
     const int n_ref = get_row(p.r + ".fam");
     std::cout << n_ref << " individuals to be included from reference FAM file.\n";
     std::cout << "Reading reference PLINK BIM file from [" << p.r << ".bim]\n";
-    const int n_snp_bim = get_row(p.r + ".bim");
+    MappedText bim_txt;
+    bim_txt.open(p.r + ".bim");
+    const int64_t n_snp_bim = count_lines(bim_txt.text);
     const bool constr = !(std::fabs(p.mafMax - 1.0) < 1e-10);
 
+    // The GPU side runs on its own host thread while this one parses the text inputs: HIP context
+    // (device initialisation), one staged upload of the .bed cached on the context (it serves the
+    // MAF pass and the plan), the MAF pass of readBim.
     dbslmm_ctx* ctx = nullptr;
     Mapped bed;
+    vector<double> maf;
+    vector<int32_t> ids;
+    string gpu_err;
+    double t_ctx = 0.0, t_up = 0.0, t_maf = 0.0;
+    std::thread gpu;
     if (!p.dry_run) {
         if (!bed.open(p.r + ".bed")) return fail(p.r + ".bed cannot be opened");
-        if (p.gpu_ids.empty()) {
-            if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) return fail("no usable HIP device (dbslmm_ctx_create)");
-            ph.mark("ctx");
-            // one staged upload of the .bed serves both the MAF pass and the plan
-            if (dbslmm_ctx_cache_bed(ctx, bed.p, static_cast<int64_t>(bed.n)) != DBSLMM_OK)
-                return fail(string("uploading the .bed: ") + dbslmm_last_error(ctx));
-            ph.mark("bed_upload");
-        } else {
-            vector<int32_t> ids;
+        if (!p.gpu_ids.empty())
             for (const string& t : split(p.gpu_ids, ',')) ids.push_back(atoi(t.c_str()));
-            if (ids.empty() || dbslmm_ctx_create_multi(static_cast<int32_t>(ids.size()), ids.data(), &ctx) != DBSLMM_OK)
-                return fail("no usable HIP devices (dbslmm_ctx_create_multi, --gpus / --gpu-ids)");
-            std::cout << "Sharding the LD blocks over " << ids.size() << " GPUs.\n";
-        }
+        gpu = std::thread([&] {
+            double t = walltime();
+            if (ids.empty()) {
+                if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) { gpu_err = "no usable HIP device (dbslmm_ctx_create)"; return; }
+                t_ctx = walltime() - t;
+                t = walltime();
+                if (dbslmm_ctx_cache_bed(ctx, bed.p, static_cast<int64_t>(bed.n)) != DBSLMM_OK) {
+                    gpu_err = string("uploading the .bed: ") + dbslmm_last_error(ctx);
+                    return;
+                }
+                t_up = walltime() - t;
+            } else {
+                if (dbslmm_ctx_create_multi(static_cast<int32_t>(ids.size()), ids.data(), &ctx) != DBSLMM_OK) {
+                    gpu_err = "no usable HIP devices (dbslmm_ctx_create_multi, --gpus / --gpu-ids)";
+                    return;
+                }
+                t_ctx = walltime() - t;
+            }
+            if (constr) {
+                t = walltime();
+                maf.resize(n_snp_bim);
+                if (dbslmm_bed_maf(ctx, bed.p, static_cast<int64_t>(bed.n), n_ref, n_snp_bim, maf.data()) != DBSLMM_OK) {
+                    gpu_err = string("MAF pass: ") + dbslmm_last_error(ctx);
+                    return;
+                }
+                t_maf = walltime() - t;
+            }
+        });
     } else if (constr) {
         return fail("--dry-run needs -mafMax 1 (the MAF pass runs on the GPU)");
     }
-    vector<double> maf;
-    if (constr) {
-        std::cout << "Calculating MAF of reference panel ...\n";
-        maf.resize(n_snp_bim);
-        if (dbslmm_bed_maf(ctx, bed.p, static_cast<int64_t>(bed.n), n_ref, n_snp_bim, maf.data()) != DBSLMM_OK)
-            return fail(string("MAF pass: ") + dbslmm_last_error(ctx));
-        ph.mark("maf");
-    } else {
-        std::cout << "[WARNING] Do not consider the difference between reference panel and summary data ...\n";
-    }
-    std::unordered_map<string, Allele> bim;
-    vector<string> bim_order;
-    read_bim(p.r, maf, bim, bim_order);
-    std::cout << bim.size() << " SNPs to be included from reference BIM file.\n";
+
+    // host parsing (overlaps the GPU thread)
+    Bim bim;
+    read_bim(bim_txt, bim);
+    const double t_bim = walltime() - ph.t0;
     const vector<Block> blocks = read_block(p.b);
+    MappedText s_txt, l_txt;
+    s_txt.open(p.s);
+    const vector<Summ> summ_s = read_summ(s_txt);
+    vector<Summ> summ_l;
+    if (has_lfile) {
+        l_txt.open(p.l);
+        summ_l = read_summ(l_txt);
+    }
+    const double t_parse = walltime() - ph.t0;
+    if (gpu.joinable()) gpu.join();
+    if (!gpu_err.empty()) return fail(gpu_err);
+    if (!ids.empty()) std::cout << "Sharding the LD blocks over " << ids.size() << " GPUs.\n";
+    if (constr) std::cout << "Calculating MAF of reference panel ...\n";
+    else std::cout << "[WARNING] Do not consider the difference between reference panel and summary data ...\n";
+    bim.maf = std::move(maf);
+    ph.put("ctx", t_ctx);
+    ph.put("bed_upload", t_up);
+    ph.put("maf", t_maf);
+    ph.put("parse", t_parse);
+    ph.put("parse_bim", t_bim);
+    ph.mark("gpu_wait");      // wall time from the start to here (parse and GPU set-up overlap)
+    std::cout << bim_size(bim) << " SNPs to be included from reference BIM file.\n";
 
     std::cout << "Reading summary data of small effect SNPs from [" << p.s << "]\n";
-    const vector<Summ> summ_s = read_summ(p.s);
     vector<char> good_s;
     const vector<Pos> inter_s = match_ref(summ_s, bim, p.mafMax, good_s);
     std::cout << "After filtering, " << inter_s.size() << " small effect SNPs are selected.\n";
     const vector<Info> info_s = add_block(inter_s, blocks);
-    std::ofstream bad(p.eff + ".badsnps");
+    string badtxt;
     for (size_t i = 0; i < summ_s.size(); ++i)
-        if (!good_s[i]) bad << summ_s[i].snp << " " << 0 << "\n";
+        if (!good_s[i]) { badtxt.append(summ_s[i].snp.data(), summ_s[i].snp.size()); badtxt += " 0\n"; }
 
     vector<Info> info_l;
     vector<Pos> inter_l;
     bool has_l = false;
-    if (lf) {
+    if (has_lfile) {
         std::cout << "Reading summary data of large effect SNPs from [" << p.l << "]\n";
-        const vector<Summ> summ_l = read_summ(p.l);
         vector<char> good_l;
         inter_l = match_ref(summ_l, bim, p.mafMax, good_l);
         if (!inter_l.empty()) {
@@ -469,9 +635,15 @@ int main(int argc, char** argv) {
             std::cout << "After filtering, no large effect SNP is selected.\n";
         }
         for (size_t i = 0; i < summ_l.size(); ++i)
-            if (!good_l[i]) bad << summ_l[i].snp << " " << 1 << "\n";
+            if (!good_l[i]) { badtxt.append(summ_l[i].snp.data(), summ_l[i].snp.size()); badtxt += " 1\n"; }
     }
-    bad.close();
+    {
+        FILE* bad = fopen((p.eff + ".badsnps").c_str(), "wb");
+        if (bad) {
+            fwrite(badtxt.data(), 1, badtxt.size(), bad);
+            fclose(bad);
+        }
+    }
     // test panel of the variance output (scr/dbslmm.cpp:264-320)
     const bool want_var = !p.dat_str.empty() && !p.test_indicator_file.empty();
     if (!want_var && (!p.dat_str.empty() || !p.test_indicator_file.empty()))
@@ -480,9 +652,9 @@ int main(int argc, char** argv) {
     if (want_var) {
         const vector<long> base = read_test_bim(p.dat_str + ".bim");
         string err;
-        if (!align_test_pos(info_s, add_block(make_pos_for_test_bim(base, inter_s), blocks),
+        if (!align_test_pos(info_s, add_block(make_pos_for_test_bim(base, inter_s), blocks), summ_s,
                             static_cast<int>(blocks.size()), ts_pos, err) ||
-            (has_l && !align_test_pos(info_l, add_block(make_pos_for_test_bim(base, inter_l), blocks),
+            (has_l && !align_test_pos(info_l, add_block(make_pos_for_test_bim(base, inter_l), blocks), summ_l,
                                       static_cast<int>(blocks.size()), tl_pos, err)))
             return fail("test panel " + p.dat_str + ": " + err);
         indicator = read_indicator(p.test_indicator_file);
@@ -493,14 +665,16 @@ int main(int argc, char** argv) {
     vector<int64_t> s_ptr, l_ptr;
     vector<int32_t> s_pos, l_pos;
     vector<double> z_s, z_l;
-    to_csr(info_s, nb, s_ptr, s_pos, z_s);
-    if (has_l) to_csr(info_l, nb, l_ptr, l_pos, z_l);
+    to_csr(info_s, summ_s, nb, s_ptr, s_pos, z_s);
+    if (has_l) to_csr(info_l, summ_l, nb, l_ptr, l_pos, z_l);
+    ph.mark("match");
     if (p.dry_run) {
         std::cout << "dry-run: blocks " << nb << " small " << info_s.size() << " large " << info_l.size() << "\n";
-        return 0;
+        if (p.timing) ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));
+        std::cout.flush();
+        std::_Exit(0);
     }
 
-    ph.mark("parse");
     const double sigma_s = p.h / static_cast<double>(p.nsnp);                 // dbslmm.cpp:332
     dbslmm_problem prob{};
     prob.bed = bed.p;
@@ -572,6 +746,8 @@ int main(int argc, char** argv) {
     std::cout << "Fitting time: " << walltime() - t0 << " seconds.\n";
     ph.mark("variance");
 
+    vector<string> names;
+    vector<std::array<EffList, 2>> lists;
     for (int f = 0; f < nf; ++f) {
         int n_bad = 0;
         for (int b = 0; b < nb; ++b) {
@@ -590,46 +766,16 @@ int main(int argc, char** argv) {
             else
                 name += string("_h2f") + hh;
         }
-        // output writer (scr/dbslmm.cpp:353-364, 391-395): large rows first, then small rows;
-        // ostream's default double format is printf %g at precision 6 (17 with --precise-out),
-        // formatted in parallel chunks and written in order
-        FILE* out = fopen((name + ".txt").c_str(), "wb");
-        if (!out) return fail(name + ".txt cannot be written");
-        const double* bs = beta_s.data() + static_cast<size_t>(f) * info_s.size();
-        const double* bl = beta_l.data() + static_cast<size_t>(f) * info_l.size();
-        const int prec = p.precise ? 17 : 6;
-        auto emit = [&](const vector<Info>& info, const double* beta, int flag) {
-            const unsigned T = host_threads();
-            vector<string> buf(T);
-            vector<std::thread> th;
-            for (unsigned t = 0; t < T; ++t)
-                th.emplace_back([&, t] {
-                    const size_t lo = info.size() * t / T, hi = info.size() * (t + 1) / T;
-                    string& o = buf[t];
-                    o.reserve((hi - lo) * 48);
-                    char num[64];
-                    for (size_t i = lo; i < hi; ++i) {
-                        const double noscl = beta[i] / std::sqrt(2 * info[i].maf * (1 - info[i].maf));
-                        if (std::isinf(noscl)) continue;
-                        o += info[i].snp;
-                        o += ' ';
-                        o += info[i].a1;
-                        o += ' ';
-                        o.append(num, static_cast<size_t>(snprintf(num, sizeof(num), "%.*g", prec, beta[i])));
-                        o += ' ';
-                        o.append(num, static_cast<size_t>(snprintf(num, sizeof(num), "%.*g", prec, noscl)));
-                        o += flag ? " 1\n" : " 0\n";
-                    }
-                });
-            for (auto& x : th) x.join();
-            for (const string& o : buf) fwrite(o.data(), 1, o.size(), out);
-        };
-        emit(info_l, bl, 1);
-        emit(info_s, bs, 0);
-        fclose(out);
+        names.push_back(name);
+        lists.push_back({EffList{&info_l, &summ_l, beta_l.data() + static_cast<size_t>(f) * info_l.size(), 1},
+                         EffList{&info_s, &summ_s, beta_s.data() + static_cast<size_t>(f) * info_s.size(), 0}});
     }
+    if (!write_eff_files(names, lists, p.precise ? 17 : 6)) return fail(names[0] + ".txt cannot be written");
     ph.mark("write");
     dbslmm_ctx_destroy(ctx);
     if (p.timing) ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));
-    return 0;
+    // the parsed inputs (views of the mappings, hash index, host arrays) need no teardown
+    std::cout.flush();
+    fflush(stderr);
+    std::_Exit(0);
 }

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -123,6 +124,160 @@ struct Mapped {
     ~Mapped() {
         if (p) munmap(const_cast<uint8_t*>(p), n);
         if (fd >= 0) close(fd);
+    }
+};
+
+// ---------------------------------------------------------------- fast text ingest (dbslmm CLI)
+// A page-cached text file mapped read-only; the parsers keep string_views into it (no per-field
+// allocation), so the mapping lives as long as the parsed rows.
+struct MappedText {
+    Mapped m;
+    string_view text;
+    bool ok = false;
+    bool open(const string& path) {
+        struct stat st;
+        if (::stat(path.c_str(), &st) != 0) return false;
+        ok = true;
+        if (st.st_size == 0) return true;
+        if (!m.open(path)) return ok = false;
+        text = string_view(reinterpret_cast<const char*>(m.p), m.n);
+        return true;
+    }
+};
+
+// Lines of `text` on up to `threads` threads, in order: thread t owns the lines that START in its
+// byte range and calls f(t, line) for each (std::getline semantics: the last line may lack its
+// '\n').  Returns the number of lines each thread saw (their prefix sum gives global line numbers).
+template <typename F>
+inline vector<size_t> parallel_lines(string_view text, unsigned threads, F f) {
+    const size_t n = text.size();
+    threads = std::max(1u, std::min<unsigned>(threads, static_cast<unsigned>(n / (1 << 16) + 1)));
+    vector<size_t> count(threads, 0);
+    auto run = [&](unsigned t) {
+        size_t lo = n * t / threads, hi = n * (t + 1) / threads;
+        // the first line starting at or after lo (a line starts after a '\n', or at 0)
+        if (lo > 0) {
+            const void* e = memchr(text.data() + lo - 1, '\n', n - (lo - 1));
+            lo = e ? static_cast<size_t>(static_cast<const char*>(e) - text.data()) + 1 : n;
+        }
+        size_t i = lo, c = 0;
+        while (i < hi && i < n) {
+            const void* e = memchr(text.data() + i, '\n', n - i);
+            const size_t j = e ? static_cast<size_t>(static_cast<const char*>(e) - text.data()) : n;
+            f(t, text.substr(i, j - i));
+            ++c;
+            i = j + 1;
+        }
+        count[t] = c;
+    };
+    vector<std::thread> th;
+    for (unsigned t = 1; t < threads; ++t) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+    return count;
+}
+
+// the first k tab-separated fields of a line (fewer if the line has fewer); returns the count
+inline int tab_fields(string_view line, string_view* out, int k) {
+    int c = 0;
+    size_t i = 0;
+    while (c < k && i < line.size()) {
+        const void* e = memchr(line.data() + i, '\t', line.size() - i);
+        const size_t j = e ? static_cast<size_t>(static_cast<const char*>(e) - line.data()) : line.size();
+        out[c++] = line.substr(i, j - i);
+        i = j + 1;
+    }
+    return c;
+}
+
+// atof / atol of a field that is not NUL-terminated, with the C library's semantics (leading
+// white space, sign, longest valid prefix, 0 when there is none): strtod / strtol on a copy
+inline double field_atof(string_view s) {
+    char buf[64];
+    if (s.size() < sizeof(buf)) {
+        memcpy(buf, s.data(), s.size());
+        buf[s.size()] = 0;
+        return strtod(buf, nullptr);
+    }
+    return strtod(string(s).c_str(), nullptr);
+}
+inline long field_atol(string_view s) {
+    // fast path: plain decimal digits (bp positions)
+    if (!s.empty() && s.size() < 19) {
+        long v = 0;
+        size_t i = 0;
+        for (; i < s.size() && s[i] >= '0' && s[i] <= '9'; ++i) v = v * 10 + (s[i] - '0');
+        if (i == s.size() && i > 0) return v;
+    }
+    char buf[64];
+    if (s.size() < sizeof(buf)) {
+        memcpy(buf, s.data(), s.size());
+        buf[s.size()] = 0;
+        return strtol(buf, nullptr, 10);
+    }
+    return strtol(string(s).c_str(), nullptr, 10);
+}
+
+inline uint64_t hash_sv(string_view s) {          // FNV-1a, 64 bit
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    return h ^ (h >> 29);
+}
+
+// Open-addressing index of n keys (key(i) -> string_view), built on several threads: every slot
+// holds the SMALLEST i among equal keys (std::map::insert keeps the first occurrence).  Slots only
+// go from empty to full, so equal keys always meet in one slot whatever the interleaving.
+struct StrIndex {
+    vector<std::atomic<int32_t>> slot;
+    vector<uint64_t> hash;
+    size_t mask = 0;
+    template <typename K>
+    void build(size_t n, unsigned threads, K key, const vector<char>* skip = nullptr) {
+        size_t cap = 16;
+        while (cap < 2 * n + 16) cap <<= 1;
+        mask = cap - 1;
+        slot = vector<std::atomic<int32_t>>(cap);
+        hash.assign(n, 0);
+        parallel_chunks(cap, threads, [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; ++i) slot[i].store(-1, std::memory_order_relaxed);
+        });
+        parallel_chunks(n, threads, [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; ++i) {
+                if (skip && (*skip)[i]) continue;
+                const string_view k = key(i);
+                const uint64_t h = hash_sv(k);
+                hash[i] = h;
+                size_t p = h & mask;
+                const int32_t me = static_cast<int32_t>(i);
+                for (;;) {
+                    int32_t cur = slot[p].load(std::memory_order_acquire);
+                    if (cur < 0) {
+                        if (slot[p].compare_exchange_strong(cur, me, std::memory_order_acq_rel)) break;
+                        // another key took the slot: re-examine it
+                    }
+                    if (cur >= 0) {
+                        if (hash[cur] == h && key(cur) == k) {   // equal key: keep the smaller index
+                            while (me < cur && !slot[p].compare_exchange_weak(cur, me, std::memory_order_acq_rel)) {
+                            }
+                            break;
+                        }
+                        p = (p + 1) & mask;
+                    }
+                }
+            }
+        });
+    }
+    // index of key k, or -1
+    template <typename K>
+    int32_t find(string_view k, K key) const {
+        const uint64_t h = hash_sv(k);
+        size_t p = h & mask;
+        for (;;) {
+            const int32_t cur = slot[p].load(std::memory_order_relaxed);
+            if (cur < 0) return -1;
+            if (hash[cur] == h && key(cur) == k) return cur;
+            p = (p + 1) & mask;
+        }
     }
 };
 

@@ -89,7 +89,6 @@ __device__ __forceinline__ v4i expand_dose(uint32_t w) {
 //   stat_*         exact integer statistics over the n_ref individuals.
 //   mu, rsd, S     fp64: mean over observed calls (= the imputation value, dtpr.cpp:358),
 //                  1/sd with the N-1 divisor (nomalizeVec), sum of observed dosages.
-//   maf (optional) min(af, 1-af), af = mu/2 (dtpr.cpp:361-362).
 //   block_flags    bit 0 set when a slot of the block has a missing call.
 //   slot_list      optional: unpack only these n_slots slots (the plan unpacks its lead group first)
 // ------------------------------------------------------------------------------------------
@@ -98,8 +97,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
     const int32_t* __restrict__ slot_pos, const int32_t* __restrict__ slot_block, int32_t n_slots,
     uint32_t* __restrict__ Gp, int64_t kpad,
     double* __restrict__ S_out, double* __restrict__ mu_out, double* __restrict__ rsd_out,
-    double* __restrict__ maf_out, int32_t* __restrict__ block_flags,
-    const int32_t* __restrict__ slot_list) {
+    int32_t* __restrict__ block_flags, const int32_t* __restrict__ slot_list) {
     const int lane = threadIdx.x & (kWave - 1);
     const int k = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (k >= n_slots) return;
@@ -114,7 +112,6 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
             if (S_out) S_out[slot] = 0.0;
             if (mu_out) mu_out[slot] = 0.0;
             if (rsd_out) rsd_out[slot] = 0.0;
-            if (maf_out) maf_out[slot] = 0.0;
         }
         return;
     }
@@ -150,12 +147,43 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
         if (S_out) S_out[slot] = ds;
         if (mu_out) mu_out[slot] = mu;
         if (rsd_out) rsd_out[slot] = 1.0 / sd;                      // +inf when monomorphic
-        if (maf_out) {
-            const double af = 0.5 * mu;
-            maf_out[slot] = af < 1.0 - af ? af : 1.0 - af;
-        }
         if (nmiss > 0 && block_flags) atomicOr(block_flags + slot_block[slot], 1);
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// MAF of IO::readSNPIm as the reference rounds it (dtpr.cpp:356-362): missing calls take the
+// mean of the observed calls (mu, exact S / count from dbslmm_unpack_stats), sum(geno) runs in
+// Armadillo's arrayops::accumulate order -- two sequential accumulators over the even / odd
+// individuals -- and af = 0.5 * sum / n.  Once a (non-integer) mean has been added, each later add
+// rounds, so the order decides the last bits, and the MAF filter of matchRef (|maf_ref - maf| <
+// mafMax, strict) can flip on them.  One thread per row: a sequential chain of n_ref fp64 adds,
+// rounded exactly like the host's (no reassociation).
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void dbslmm_maf_arma(
+    const uint8_t* __restrict__ bed, int32_t n_ref, int64_t bytes_per_snp,
+    const int32_t* __restrict__ pos, int32_t n_rows, const double* __restrict__ mu,
+    double* __restrict__ maf_out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_rows) return;
+    const int64_t row_off = 3 + static_cast<int64_t>(pos[k]) * bytes_per_snp;
+    const double m = mu[k];
+    double a1 = 0.0, a2 = 0.0;
+    for (int32_t i0 = 0; i0 < n_ref; i0 += 16) {
+        const uint32_t word = load_u32_any(bed, row_off + i0 / 4);
+        const int nv = min(16, n_ref - i0);
+        for (int j = 0; j < nv; j += 2) {          // i0 is even: j even = even individual
+            const uint32_t c0 = (word >> (2 * j)) & 3u;
+            // PLINK 2-bit code (low bit first): 00 -> 2, 10 -> 1, 11 -> 0, 01 -> missing (mean)
+            a1 += c0 == 0u ? 2.0 : c0 == 2u ? 1.0 : c0 == 3u ? 0.0 : m;
+            if (j + 1 < nv) {
+                const uint32_t c1 = (word >> (2 * j + 2)) & 3u;
+                a2 += c1 == 0u ? 2.0 : c1 == 2u ? 1.0 : c1 == 3u ? 0.0 : m;
+            }
+        }
+    }
+    const double af = 0.5 * (a1 + a2) / static_cast<double>(n_ref);
+    maf_out[k] = (1.0 - af) < af ? 1.0 - af : af;   // std::min(af, 1.0 - af)
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1437,7 +1437,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         dim3 grid((n_sl + wpb - 1) / wpb);
         hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, s, p->d_bed, p->n_ref,
                            p->bytes_per_snp, p->d_slot_pos, p->d_slot_block, n_sl, p->d_G,
-                           p->kpad, p->d_S, p->d_mu, p->d_rsd, nullptr, p->d_flags, list);
+                           p->kpad, p->d_S, p->d_mu, p->d_rsd, p->d_flags, list);
     };
     // a lead group's slots first: its Gram and sequence start after ~2 % of the unpack
     const bool split_unpack = front && p->n_slots_lead > 0;
@@ -1872,7 +1872,7 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
                                dim3(256), 0, st, d_tbed, tbps, d_tpos, p->n_slots, d_sel, n_test, cbps, d_cbed);
             hipLaunchKernelGGL(dbslmm_unpack_stats, dim3(static_cast<unsigned>((p->n_slots + 3) / 4)), dim3(256), 0,
                                st, d_cbed, n_test, cbps, d_cpos, d_cpos, p->n_slots, nullptr,
-                               nt_pad, nullptr, d_mu, d_rsd, nullptr, nullptr, nullptr);
+                               nt_pad, nullptr, d_mu, d_rsd, nullptr, nullptr);
             hipLaunchKernelGGL(dbslmm_variance, dim3(static_cast<unsigned>(nt_pad / 64), p->n_nonempty),
                                dim3(256), 0, st, p->d_M + p->var_copy * p->M_elems, p->d_row0, p->d_m,
                                p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_status + p->var_copy * p->nbk,
@@ -1903,7 +1903,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     uint8_t* d_bed = nullptr;
     int32_t* d_pos = nullptr;
-    double* d_maf = nullptr;
+    double *d_maf = nullptr, *d_mu = nullptr;
     std::vector<int32_t> pos(n_snp);
     std::iota(pos.begin(), pos.end(), 0);
     int rc = DBSLMM_OK;
@@ -1913,16 +1913,19 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
         if ((!cached && ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
                          (e = bed_to_device(ctx, d_bed, bed, bed_len)) != hipSuccess)) ||
             (e = dev_upload(&d_pos, pos)) != hipSuccess ||
+            (e = hipMalloc(&d_mu, n_snp * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_maf, n_snp * sizeof(double))) != hipSuccess) {
             ctx->err = std::string("bed_maf alloc/upload: ") + hipGetErrorString(e);
             rc = DBSLMM_E_HIP;
             break;
         }
+        const uint8_t* db = cached ? ctx->d_bed_cache : d_bed;
         dim3 grid(static_cast<unsigned>((n_snp + 3) / 4));
-        hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, ctx->stream, cached ? ctx->d_bed_cache : d_bed,
-                           n_ref, bps,
+        hipLaunchKernelGGL(dbslmm_unpack_stats, grid, dim3(256), 0, ctx->stream, db, n_ref, bps,
                            d_pos, d_pos, static_cast<int32_t>(n_snp), nullptr, round_up(n_ref, 64),
-                           nullptr, nullptr, nullptr, d_maf, nullptr, nullptr);
+                           nullptr, d_mu, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(dbslmm_maf_arma, dim3(static_cast<unsigned>((n_snp + 255) / 256)), dim3(256), 0,
+                           ctx->stream, db, n_ref, bps, d_pos, static_cast<int32_t>(n_snp), d_mu, d_maf);
         if ((e = hipGetLastError()) != hipSuccess ||
             (e = hipStreamSynchronize(ctx->stream)) != hipSuccess ||
             (e = hipMemcpy(maf, d_maf, n_snp * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess) {
@@ -1932,6 +1935,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
     } while (0);
     (void)hipFree(d_bed);
     (void)hipFree(d_pos);
+    (void)hipFree(d_mu);
     (void)hipFree(d_maf);
     return rc;
 }
@@ -1968,7 +1972,9 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
         }
         hipLaunchKernelGGL(dbslmm_unpack_stats, dim3((n_rows + 3) / 4), dim3(256), 0, ctx->stream,
                            d_bed, n_ref, bps, d_pos, d_pos, n_rows, nullptr, round_up(n_ref, 64),
-                           nullptr, d_mu, d_rsd, d_maf, nullptr, nullptr);
+                           nullptr, d_mu, d_rsd, nullptr, nullptr);
+        hipLaunchKernelGGL(dbslmm_maf_arma, dim3(static_cast<unsigned>((n_rows + 255) / 256)), dim3(256), 0,
+                           ctx->stream, d_bed, n_ref, bps, d_pos, n_rows, d_mu, d_maf);
         hipLaunchKernelGGL(dbslmm_std_columns, dim3(static_cast<unsigned>((n_out + 255) / 256)),
                            dim3(256), 0, ctx->stream, d_bed, n_ref, bps, d_pos, n_rows, d_mu, d_rsd,
                            d_out);
@@ -2039,7 +2045,7 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
         if (n_rows > 0)
             hipLaunchKernelGGL(dbslmm_unpack_stats, dim3(static_cast<unsigned>((n_rows + 3) / 4)), dim3(256), 0,
                                ctx->stream, d_bed, n_ref, bps, d_pos, d_pos, static_cast<int32_t>(n_rows),
-                               nullptr, round_up(n_ref, 64), nullptr, d_mu, d_rsd, nullptr, nullptr, nullptr);
+                               nullptr, round_up(n_ref, 64), nullptr, d_mu, d_rsd, nullptr, nullptr);
         hipLaunchKernelGGL(dbslmm_valid_partial, dim3(n_chunks, num_block), dim3(256), 0, ctx->stream,
                            d_bed, n_ref, bps, d_ptr, d_pos, d_z1, d_mu, d_rsd, d_part, n_chunks);
         hipLaunchKernelGGL(dbslmm_valid_reduce, dim3((num_block + 255) / 256), dim3(256), 0, ctx->stream,

@@ -65,7 +65,7 @@ def read_snp_im(bed: bytes | np.ndarray, pos: int, indicator: np.ndarray):
     miss = np.isnan(g)
     mean = g[~miss].sum() / float(g.size - miss.sum())   # dtpr.cpp:358 (NaN if all missing)
     g[miss] = mean
-    af = 0.5 * g.sum() / g.size                           # dtpr.cpp:361
+    af = 0.5 * _arma_accumulate(g) / g.size               # dtpr.cpp:361 (sum(geno): Armadillo order)
     return g, min(af, 1.0 - af)
 
 

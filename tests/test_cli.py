@@ -182,8 +182,15 @@ def _filtered_panel(tmp_path, layout, seed=5):
     panel = synth.simulate(7000, 250, pop="EUR", chroms=[19, 20, 21], seed=seed, large_every=3,
                            miss_rate=0.002)
     f = synth.write_plink(panel, str(tmp_path / "p"))
-    bim = R.read_bim(f["ref"], panel.n_ref, True)         # .bed MAF (IO::readBim, constr)
     rng = np.random.default_rng(seed)
+    # duplicate SNP ids in the .bim: std::map::insert keeps the first line (dtpr.cpp:108-118)
+    lines = open(f["ref"] + ".bim").read().splitlines()
+    for k in rng.choice(np.arange(100, len(lines)), size=8, replace=False):
+        t = lines[k].split("\t")
+        t[1] = lines[k - 37].split("\t")[1]
+        lines[k] = "\t".join(t)
+    open(f["ref"] + ".bim", "w").write("\n".join(lines) + "\n")
+    bim = R.read_bim(f["ref"], panel.n_ref, True)         # .bed MAF (IO::readBim, constr)
     for key in ("s", "l"):
         out = []
         for line in open(f[key]).read().splitlines():

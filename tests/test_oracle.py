@@ -95,11 +95,17 @@ def test_c_oracle_synth_small_golden(lmm):
 
 
 def test_bed_maf_matches_read_snp_im():
-    bed = load_bed(os.path.join(TD, "ref_chr1.bed"))
-    maf = O.bed_maf(bed, 400, 723, threads=2)
-    idv = np.ones(400, dtype=np.int32)
-    for pos in (0, 5, 722):
-        assert maf[pos] == R.read_snp_im(bed, pos, idv)[1]
+    """Both restatements compute readSNPIm's af = 0.5 * sum(geno) / n with sum() in Armadillo's
+    accumulate order (dtpr.cpp:361; the order decides the last bits once mean-imputed calls are
+    added, and matchRef's strict |maf_ref - maf| < mafMax can flip on them): bit for bit, on
+    test_dat and on the synthetic panel with missing calls."""
+    for path, n_ref, n_snp in ((os.path.join(TD, "ref_chr1.bed"), 400, 723),
+                               (os.path.join(GOLD, "synth_small", "ref.bed"), 203, 600)):
+        bed = load_bed(path)
+        maf = O.bed_maf(bed, n_ref, n_snp, threads=2)
+        idv = np.ones(n_ref, dtype=np.int32)
+        ref = np.array([R.read_snp_im(bed, pos, idv)[1] for pos in range(n_snp)])
+        np.testing.assert_array_equal(maf, ref)
 
 
 def test_joint_solve_identity():
