@@ -457,29 +457,46 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 
 // ------------------------------------------------------------------------------------------
 // Kernel 2c: the Gram of the big blocks (m >= 384), 256 x 256 output tile per 512-thread
-// workgroup: every wave computes a 64 x 128 piece (2 x 4 MFMA 32x32x32 i8 tiles, 128 accumulator
-// registers); the two waves of a SIMD hold pieces in opposite halves of the tile.  K runs in
-// stages of 128 individuals: every thread loads one row's 8 Gp dwords (32 B, four stages ahead in
-// registers) and expands them to 128 B of int8 codes in a double-buffered LDS stage (a quarter of
-// the HBM / L2 operand traffic of an int8 image), raw s_barrier per stage, 32 MFMAs per wave.
-// LDS rows are swizzled (swz) so that both the expansion writes and the operand reads are
-// bank-conflict free.  Diagonal tiles stage one operand; MFMA tiles strictly above the diagonal
-// or wholly past m (edge tiles) are skipped (config 4: 6.7 -> 6.3 ms; skipping whole waves'
-// pieces only, without the per-MFMA branches, gained nothing; keeping the 2-bit codes in LDS and
-// expanding after the operand reads, a quarter of the LDS traffic, was slower: 6.7 ms).
-// Missing-call blocks: exact 4-product path per 32 x 32 sub-tile.
+// workgroup, on the FP4 matrix cores.  Dosages 0 / 1 / 2 are exact e2m1 values (0.0, 1.0, 2.0),
+// every product is exact and every partial sum an integer below 4 n_ref < 2^24, so
+// v_mfma_scale_f32_32x32x64_f8f6f4 (unit E8M0 scales) gives the integer Gram bit for bit -- at
+// twice the MACs per clock of v_mfma_i32_32x32x32_i8 and with half its operand bytes in LDS.
+// A Gp dword (16 two-bit codes) becomes two FP4 dwords with one shift and one mask each:
+// (w << 1) & 0x66666666 holds the even-numbered codes, (w >> 1) & 0x66666666 the odd ones (a
+// fixed permutation of the individuals, the same on both operands).  Every wave computes a
+// 64 x 128 piece (2 x 4 MFMA tiles, 128 accumulator registers); the two waves of a SIMD hold
+// pieces in opposite halves of the tile.  K runs in stages of 256 individuals: every thread loads
+// one row's 16 Gp dwords (64 B, two stages ahead in registers) and expands them to 128 B of FP4
+// codes in a double-buffered LDS stage, raw s_barrier per stage, 32 MFMAs per wave.  LDS rows are
+// swizzled (swz) so that both the expansion writes and the operand reads are bank-conflict free.
+// Diagonal tiles stage one operand; MFMA tiles strictly above the diagonal or wholly past m (edge
+// tiles) are skipped.  Missing-call blocks: exact 4-product i8 path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 namespace gram {
 constexpr int kHT = 256;                   // output tile edge
-constexpr int kHK = 128;                   // individuals (bytes) per K stage = one row chunk set
-constexpr int kHOp = kHT * kHK;            // one operand stage (32 KiB)
+constexpr int kHK = 256;                   // individuals per K stage
+constexpr int kHRow = kHK / 2;             // LDS bytes per row and stage (FP4 codes)
+constexpr int kHOp = kHT * kHRow;          // one operand stage (32 KiB)
 constexpr int kHSlots = 2;                 // LDS double buffer
 constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 128 KiB
+constexpr int kKpadAlign = kHK;            // kpad: a multiple of the FP4 stage
+constexpr int kE8M0One = 0x7F7F7F7F;       // E8M0 scale 2^0 in every byte
 // logical 16-B chunk c of row r at position c ^ f(r), f(r) = (r ^ r >> 2 ^ r >> 3) & 7: conflict-free
 // for the expansion writes (ds_write_b128: 8-lane groups of consecutive rows, 32 banks) and the
 // MFMA operand reads (ds_read_b128: 16-lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}
 // of 32 rows, 64 banks) -- MI355X_MICROARCH.md LDS table; (r >> 2) & 3 left the writes 2-way
-__device__ __forceinline__ int swz(int r, int c) { return r * kHK + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 7)); }
+__device__ __forceinline__ int swz(int r, int c) { return r * kHRow + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 7)); }
+// 16-B LDS chunk c of a row (32 individuals) from Gp dwords 2c, 2c + 1
+__device__ __forceinline__ v4i fp4_chunk(uint32_t w0, uint32_t w1) {
+    return v4i{static_cast<int>((w0 << 1) & 0x66666666u), static_cast<int>((w0 >> 1) & 0x66666666u),
+               static_cast<int>((w1 << 1) & 0x66666666u), static_cast<int>((w1 >> 1) & 0x66666666u)};
+}
+__device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
+    const v8i a8{a[0], a[1], a[2], a[3], 0, 0, 0, 0}, b8{b[0], b[1], b[2], b[3], 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
+}
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
@@ -512,9 +529,9 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         }
         return;
     }
-    // staging: thread t -> operand t >> 8, row t & 255; per stage (128 individuals) two 16-B
-    // loads of 8 Gp dwords, expanded on the way into LDS (8 ds_write_b128 at swz: conflict-free
-    // writes and reads).  Loads run four stages ahead in four register sets.
+    // staging: thread t -> operand t >> 8, row t & 255; per stage (256 individuals) four 16-B
+    // loads of 16 Gp dwords, expanded on the way into LDS (8 ds_write_b128 at swz).  Loads run two
+    // stages ahead in two register sets.
     const int64_t kw = kpad / 16;
     const int sop = tid >> 8, srow = tid & 255;
     // ragged edge tiles: rows / columns of the tile inside the block (the last tile row / column
@@ -525,22 +542,26 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     const int svalid = sop ? cv : rv;
     const bool stager = !(diag && sop == 1) && srow < svalid;
     const uint32_t* gs = Gp + static_cast<int64_t>(row0 + kHT * (sop ? tile.tj : tile.ti) + min(srow, svalid - 1)) * kw;
-    const int nst = static_cast<int>(kpad / kHK);   // kpad is a multiple of 128
+    const int nst = static_cast<int>(kpad / kHK);   // kpad is a multiple of kHK
     // unconditional loads (clamped stage, valid rows for every thread) keep the vmcnt bookkeeping
     // exact: the newer loads in flight at every use are known
-    struct Pk { v4i lo, hi; };                       // a stage of one row: 8 Gp dwords
+    struct Pk { v4i q[4]; };                         // a stage of one row: 16 Gp dwords
     auto gload = [&](int st) -> Pk {
-        const uint32_t* q = gs + 8 * min(st, nst - 1);
-        return Pk{*reinterpret_cast<const v4i*>(q), *reinterpret_cast<const v4i*>(q + 4)};
+        const uint32_t* g = gs + (kHK / 16) * min(st, nst - 1);
+        Pk pk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk.q[i] = *reinterpret_cast<const v4i*>(g + 4 * i);
+        return pk;
+    };
+    auto chunk = [](const Pk& pk, int c) {           // Gp dwords 2c, 2c + 1
+        return fp4_chunk(static_cast<uint32_t>(pk.q[c >> 1][2 * (c & 1)]),
+                         static_cast<uint32_t>(pk.q[c >> 1][2 * (c & 1) + 1]));
     };
     auto lstore = [&](const Pk& pk, int st) {
         if (!stager) return;
         int8_t* slot = hlds + (st & 1) * 2 * kHOp + sop * kHOp;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            *reinterpret_cast<v4i*>(slot + swz(srow, c)) = expand_dose(static_cast<uint32_t>(pk.lo[c]));
-            *reinterpret_cast<v4i*>(slot + swz(srow, 4 + c)) = expand_dose(static_cast<uint32_t>(pk.hi[c]));
-        }
+        for (int c = 0; c < 8; ++c) *reinterpret_cast<v4i*>(slot + swz(srow, c)) = chunk(pk, c);
     };
     // wave -> piece: the two waves of a SIMD (w, w + 4) hold one row group in each half of the
     // tile and opposite column halves, so the skipped MFMAs of an edge tile leave every SIMD with
@@ -557,18 +578,18 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             if (ri < rv && cj < cv && !(diag && cj >= ri + 32)) act |= 1u << (4 * i + j);
         }
     const bool idle = act == 0;
-    v16i acc[2][4];
+    v16f acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0};
+        for (int j = 0; j < 4; ++j) acc[i][j] = v16f{0.0f};
     const int rsub = lane & 31, csub = lane >> 5;   // row in a 32-row group, 16-B half of a k-step
     auto compute = [&](int st) {
         if (idle) return;
         const int8_t* A = hlds + (st & 1) * 2 * kHOp;
         const int8_t* B = diag ? A : A + kHOp;
 #pragma unroll
-        for (int kk = 0; kk < kHK / 32; ++kk) {
+        for (int kk = 0; kk < 4; ++kk) {              // 64 individuals per k-step
             const int c = 2 * kk + csub;
             v4i av[2], bv[4];
 #pragma unroll
@@ -581,21 +602,20 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if (act & (1u << (4 * i + j)))
-                        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
+                    if (act & (1u << (4 * i + j))) acc[i][j] = mfma_fp4(av[i], bv[j], acc[i][j]);
         }
     };
-    // four register sets: the loads of stage st + 4 are issued while stage st is multiplied
-    Pk p0 = gload(0), p1 = gload(1), p2 = gload(2), p3 = gload(3);
+    // two register sets: the loads of stage st + 3 are issued while stage st is multiplied
+    Pk p0 = gload(0), p1 = gload(1);
     lstore(p0, 0);
-    p0 = gload(4);
+    p0 = gload(2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // raw barriers: a __syncthreads() would also drain the loads in flight.  Expansions past the
     // last stage land in the slot no later stage reads; every wave runs the same barriers.
     auto step = [&](Pk& pk, int st) {     // stage st is in slot st & 1; pk holds stage st + 1
         lstore(pk, st + 1);
-        pk = gload(st + 5);
+        pk = gload(st + 3);
         if (st < nst) compute(st);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -609,38 +629,33 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         const int8_t* A = hlds + (st & 1) * 2 * kHOp;
         const int8_t* B = diag ? A : A + kHOp;
 #pragma unroll
-        for (int kk = 0; kk < kHK / 32; ++kk) {
+        for (int kk = 0; kk < 4; ++kk) {
             const int c = 2 * kk + csub;
             v4i av[2], bv[4];
 #pragma unroll
             for (int i = 0; i < 2; ++i) av[i] = *reinterpret_cast<const v4i*>(A + swz(64 * wr + 32 * i + rsub, c));
 #pragma unroll
             for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const v4i*>(B + swz(128 * wc + 32 * j + rsub, c));
-            *reinterpret_cast<v4i*>(wslot + swz(srow, kk)) = expand_dose(static_cast<uint32_t>(pk.lo[kk]));
-            *reinterpret_cast<v4i*>(wslot + swz(srow, 4 + kk)) = expand_dose(static_cast<uint32_t>(pk.hi[kk]));
+            *reinterpret_cast<v4i*>(wslot + swz(srow, 2 * kk)) = chunk(pk, 2 * kk);
+            *reinterpret_cast<v4i*>(wslot + swz(srow, 2 * kk + 1)) = chunk(pk, 2 * kk + 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma_fp4(av[i], bv[j], acc[i][j]);
         }
-        pk = gload(st + 5);
+        pk = gload(st + 3);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     };
     int st = 0;
     if (act == 0xFFu)
-        for (; st + 4 <= nst; st += 4) {
+        for (; st + 2 <= nst; st += 2) {
             step_full(p1, st);
-            step_full(p2, st + 1);
-            step_full(p3, st + 2);
-            step_full(p0, st + 3);
+            step_full(p0, st + 1);
         }
-    for (; st < nst; st += 4) {
+    for (; st < nst; st += 2) {
         step(p1, st);
-        step(p2, st + 1);
-        step(p3, st + 2);
-        step(p0, st + 3);
+        step(p0, st + 1);
     }
     if (idle) return;
     const double scale = tau / n_ref_d;

@@ -7,7 +7,7 @@
 //             [small SNPs | large SNPs | padding]; per slot: bed row (-1 = pad), block,
 //             z-score, output index (>= 0 small, -1-i large); slot m of a block doubles as
 //             the row that carries z through the bordered Cholesky
-//   Gp        [n_slots + 256][kpad / 16] dwords of 2-bit dosage codes, kpad = roundup(n_ref, 128)
+//   Gp        [n_slots + 256][kpad / 16] dwords of 2-bit dosage codes, kpad = roundup(n_ref, 256)
 //   M         fp64 per block ld x ld row-major, lower triangle; row m = z (written by the solve)
 //   stats     S, mu, 1/sd per slot; y (solve scratch) per slot; flags/status per block
 // The whole problem stays resident; plan_run re-executes unpack -> gram -> chol from the
@@ -71,6 +71,7 @@ constexpr int kWideSuper = 4;           // ... for blocks of m >= kWideMin (half
 constexpr int kWideMin = 4096;          //     flop; config 5 35.4 -> 34.3 ms/step)
 constexpr int kTiledMaxM = 255 * 128;   // tiled path: 128-row tile and region indices < 256
 constexpr int kGramSq = 4;              // 2D tile squares per XCD of the 256-tile Gram
+constexpr int kTrailSq = 8;             // 2D squares (in 128-tiles) per XCD of the trailing update
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 // Graph capture (launch_graph) vs the device-synchronising setup calls of another host thread
@@ -182,7 +183,7 @@ struct dbslmm_plan {
     int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
     int32_t h2f_mode = 0;                    // dbslmm_options.h2f_mode
-    double cheb_tol = 1e-11;                 // dbslmm_options.cheb_tol
+    double cheb_tol = 1e-10;                 // dbslmm_options.cheb_tol
     bool trsv_pending = false;               // a persistent substitution ran since the last error check
     bool trsv_failed = false;                // ... and one of its hand-off waits gave up (sticky until the next run)
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (DBSLMM_DIAG) only
@@ -429,23 +430,42 @@ static void build_tiled(const std::vector<int32_t>& mv, const std::vector<int32_
                     }
                 }
             const int run = run_force ? run_force : (ntiles >= 1024 ? run2 : 1);
+            // 2-D placement: the tiles are cut into squares of kTrailSq x kTrailSq (tile rows I x tile
+            // columns J), a square's tiles go to one XCD, squares LPT over the XCDs.  The ~32 CUs of
+            // an XCD then work on one or two squares at a time, which read kTrailSq row panels and
+            // kTrailSq column panels between them through that XCD's L2 (keyed on the tile row
+            // alone, every XCD read every column panel from HBM)
+            // (smaller squares when a launch has few tiles, so the LPT over the XCDs stays balanced)
+            const int sq_w = ntiles >= 16 * kTrailSq * kTrailSq ? kTrailSq : ntiles >= 512 ? kTrailSq / 2 : 2;
+            struct Sq { int32_t bq, meta; int i0, i1, j0, j1, jhi; int64_t n; };
+            std::vector<Sq> sqs;
             for (const auto& k : bl)
                 if (active(k)) {
                     const int r0 = (g - k.off) * k.R, rl = std::min(r0 + k.R, k.nr) - 1;
                     if (rl + 1 >= k.nr) continue;
                     const int jlo = near ? 1 : k.R + 1, jhi = near ? k.R : 1 << 20;
                     const int meta = (r0 << 8) | (rl - r0 + 1);
-                    for (int I = rl + jlo; I <= k.Tz2; ++I) {
-                        const int jm = std::min(std::min(I, k.T2 - 1), rl + jhi);
-                        if (jm < rl + jlo) continue;
-                        const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-                        for (int J = rl + jlo; J <= jm; J += run) {
-                            q[x].push_back((k.bq << 16) | (I << 8) | J);
-                            q[x].push_back(meta);
+                    const int jcap = std::min(k.T2 - 1, rl + jhi);
+                    for (int i0 = rl + jlo; i0 <= k.Tz2; i0 += sq_w)
+                        for (int j0 = rl + jlo; j0 <= std::min(i0 + sq_w - 1, jcap); j0 += sq_w) {
+                            const int i1 = std::min(i0 + sq_w - 1, k.Tz2), j1 = std::min(j0 + sq_w - 1, jcap);
+                            int64_t n = 0;
+                            for (int I = i0; I <= i1; ++I) n += std::max(0, std::min(I, j1) - j0 + 1);
+                            if (n > 0) sqs.push_back(Sq{k.bq, meta, i0, i1, j0, j1, jcap, n});
                         }
-                        load[x] += jm - (rl + jlo) + 1;
+                }
+            std::stable_sort(sqs.begin(), sqs.end(), [](const Sq& a, const Sq& b) { return a.n > b.n; });
+            for (const Sq& sq : sqs) {
+                const int x = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+                for (int I = sq.i0; I <= sq.i1; ++I) {
+                    const int jm = std::min(I, sq.j1);
+                    for (int J = sq.j0; J <= jm; J += run) {
+                        q[x].push_back((sq.bq << 16) | (I << 8) | J);
+                        q[x].push_back(sq.meta);
                     }
                 }
+                load[x] += sq.n;
+            }
             trailing_launch(q, run, strm);
         };
         // lookahead: the next super step's R tile columns ("near": chain stream, one tile per
@@ -623,6 +643,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     ARG_CHECK(ctx, pr && out, "null problem/out");
     *out = nullptr;
     ARG_CHECK(ctx, pr->bed && pr->n_ref > 1 && pr->n_obs > 0 && pr->num_block >= 0, "bad sizes");
+    // the FP4 Gram accumulates integers up to 4 n_ref in fp32 (exact below 2^24)
+    ARG_CHECK(ctx, pr->n_ref < (1 << 22), "n_ref must be below 4,194,304 (exact FP4 Gram accumulation)");
     ARG_CHECK(ctx, pr->s_ptr && (pr->s_ptr[pr->num_block] == 0 || (pr->s_pos && pr->z_s)), "bad small CSR");
     ARG_CHECK(ctx, pr->sigma_s > 0.0 && std::isfinite(pr->sigma_s), "sigma_s must be > 0");
     const int64_t bps = pr->n_ref / 4 + (pr->n_ref % 4 ? 1 : 0);
@@ -639,7 +661,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->sigma_s = pr->sigma_s;
     p->tau = pr->tau;
     p->bytes_per_snp = bps;
-    p->kpad = round_up(pr->n_ref, gram::kKS);
+    p->kpad = round_up(pr->n_ref, gram::kKpadAlign);   // the FP4 Gram's K stage (gram_big: 128 divides it)
     p->bed_len = pr->bed_len;
     const dbslmm_options op = pr->opts ? *pr->opts : dbslmm_options{};
     ARG_CHECK(ctx, op.tiled_min >= 0 && op.gram_big_min >= 0 && op.gram_huge_min >= 0 &&
@@ -1245,7 +1267,7 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
             hi[j] = std::max(1.0, 1.0 + ext) * (1.0 + 1e-6);
             if (!(lo[j] > 0.0)) return false;
             // Chebyshev: error <= 2 q^K x the initial error x_c - x_b, itself <= |ext| relative
-            // (the same bound); K so that the final error is 1e-11 of the solution
+            // (the same bound); K so that the final error is 1e-10 of the solution
             // (dbslmm_options.cheb_tol; the BASELINE bar on beta is 1e-5 relative, and the
             // reference's own PCG stops at an absolute residual of 1e-7)
             const double kap = hi[j] / lo[j], q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);

@@ -10,8 +10,8 @@
 // (1 - tau) I >= (1 - tau) I, so the Schur complement of M_b on the small SNPs is
 // >= (d_b + 1 - tau) I and the spectrum of M_b^{-1} M_c lies in [1, 1 + delta / (d_b + 1 - tau)]
 // (delta > 0) or [1 + delta / (d_b + 1 - tau), 1] (delta < 0) -- an interval that does not
-// depend on the data, so the iteration count is fixed on the host (9 for h2f = 0.8 / 1 / 1.2
-// at a relative error of 1e-11) and no inner products are needed.  M_b d is carried by the recurrence
+// depend on the data, so the iteration count is fixed on the host (8 for h2f = 0.8 / 1 / 1.2
+// at a relative error of 1e-10) and no inner products are needed.  M_b d is carried by the recurrence
 // s = alpha s + beta r (M_b z = r), so one iteration is one forward and one backward
 // substitution; the Chebyshev update is the backward kernel's epilogue.
 //

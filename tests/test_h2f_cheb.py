@@ -1,7 +1,7 @@
 """h2f tuning by Chebyshev iteration on one factor (trsv.hip): for the tiled blocks only the base
 copy (median sigma) is factored; the other copies iterate M_b x = z - delta P_s x with the
 persistent forward / backward substitution kernels.  Every copy must match a fresh single-sigma
-solve within the iteration's target (cheb_tol 1e-11; checked at normwise 1e-10), the base copy
+solve within the iteration's target (cheb_tol 1e-10; checked at normwise 1e-10), the base copy
 bit for bit; statuses and the NaN of a
 monomorphic block carry over; the merged-factorisation path (h2f_mode = 1) stays
 bit-identical."""
