@@ -124,8 +124,8 @@ def kernel_roofline(name, ms, wl, n_solve=1):
                     note="factor bytes read by the %d forward + backward substitutions of h2f tuning "
                          "(iterations on the base copy's factor; chain- and streaming-bound, ~5.7 us per 64-row step of the largest block)"
                          % wl["cheb_iters"])
-    if name == "dbslmm_tchol" and wl["cheb_iters"] > 0:
-        n_solve = 1     # h2f: only the base copy of the tiled blocks is factored
+    if name in ("dbslmm_tchol", "dbslmm_chol_large") and wl["cheb_iters"] > 0:
+        n_solve = 1     # h2f: only the base copy of the tiled and single-workgroup blocks is factored
     fl = n_solve * {"dbslmm_chol_large": wl["chol_flops_large"], "dbslmm_chol_small": wl["chol_flops_small"],
                     "dbslmm_tchol": wl["chol_flops_tiled"]}[name]
     a = fl / s / 1e12 if s > 0 else 0.0

@@ -540,11 +540,190 @@ __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* 
         }
     }
     STAMP_END(3);
+    // x = M^{-1} z also into the copy's slot vector: the start of the Chebyshev h2f copies
+    // (dbslmm_chol_cheb) when this is the base copy
+    if (v != y + row0)
+        for (int i = tid; i < m; i += NT) y[row0 + i] = fail ? 0.0 : v[i];
     for (int i = tid; i < m; i += NT) scatter_beta(a, row0, i, fail ? 0.0 : v[i], fail);
     report_status(a, b, row0, m, tid, NT, fail);
 }
 
+// ---------------------------------------------------------------- h2f copies by Chebyshev
+// The single-workgroup blocks (ld > 64) take part in the h2f Chebyshev iteration of trsv.hip too:
+// only the base copy is factored (dbslmm_chol_large), every other copy c iterates
+// M_b x = z - delta_c P_s x with the base factor as the preconditioner (the recurrence and the
+// coefficients of trsv.hip / cheb_plan: d = alpha d + beta M_b^{-1} r, s = alpha s + beta r,
+// x += d, r -= s + delta P_s d; start x = x_b, r = -delta P_s x_b).  One workgroup per block: the
+// vectors of up to kChebR copies live in LDS; per iteration a forward substitution (right-looking
+// over the 32-row tiles: y_J = X_JJ v_J with the stored inverse, then the strip below it) and a
+// backward one (as large_block's), each reading the factor's lower triangle once.  The factor of
+// two more copies (2 m^3 / 3 flops, the whole matrix written twice) becomes ~16 triangular
+// passes (~8 m^2 flops) with far less LDS per workgroup, so several blocks share a CU.
+constexpr int kChebR = 2;                           // copies per launch group (trsv::kMaxR)
+constexpr int kChebMaxM = 512;                      // ld > 64 blocks are below the tiled threshold
+constexpr int kChebLdsDoubles = 5 * kChebR * kChebMaxM + kTileD + kChebR * 8 * kT;
+
+__device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, int nr, int iters,
+                           const double* __restrict__ coef, double* lds) {
+    constexpr int NT = kLargeThreads, NG = NT / kT;
+    const int tid = threadIdx.x;
+    double* X = lds;                                 // [kChebR][kChebMaxM] each
+    double* R = X + kChebR * kChebMaxM;
+    double* Dv = R + kChebR * kChebMaxM;
+    double* Sv = Dv + kChebR * kChebMaxM;
+    double* V = Sv + kChebR * kChebMaxM;             // work vector: r -> y -> z
+    double* Dt = V + kChebR * kChebMaxM;             // diagonal tile, stride kTS
+    double* red = Dt + kTileD;                       // [kChebR][NG][32] partial sums
+    const int T = (m + kT - 1) / kT;
+    for (int k = 0; k < iters; ++k) {
+        for (int e = tid; e < nr * kChebMaxM; e += NT) V[e] = R[e];
+        __syncthreads();
+        // forward L y = r: right-looking over the tiles
+        for (int J = 0; J < T; ++J) {
+            const int c1 = kT * J, jmax = min(kT, m - c1);
+            for (int e = tid; e < kT * kT; e += NT) {
+                const int rr = e >> 5, cc = e & 31;   // stored (rr, cc >= rr) = X[cc][rr]
+                Dt[rr * kTS + cc] = (cc >= rr && cc < jmax) ? A[static_cast<int64_t>(c1 + rr) * ld + c1 + cc] : 0.0;
+            }
+            __syncthreads();
+            {   // y_J[kk] = sum_{c <= kk} X[kk][c] v[c1 + c]
+                const int kk = tid & 31, g = tid >> 5;
+                for (int q = 0; q < nr; ++q) {
+                    double sx = 0.0;
+                    for (int c = g; c <= kk && c < jmax; c += NG) sx += Dt[c * kTS + kk] * V[q * kChebMaxM + c1 + c];
+                    red[(q * NG + g) * kT + kk] = sx;
+                }
+            }
+            __syncthreads();
+            if (tid < kT * nr) {
+                const int kk = tid & 31, q = tid >> 5;
+                double sx = 0.0;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) sx += red[(q * NG + g) * kT + kk];
+                if (kk < jmax) V[q * kChebMaxM + c1 + kk] = sx;
+            }
+            __syncthreads();
+            // v_i -= L[i][c1 ..] y_J for the rows below the tile
+            for (int i = c1 + kT + tid; i < m; i += NT) {
+                const double* Li = A + static_cast<int64_t>(i) * ld + c1;
+                double s0 = 0.0, s1 = 0.0;
+                for (int c = 0; c < jmax; ++c) {
+                    const double l = Li[c];
+                    s0 += l * V[c1 + c];
+                    if (nr > 1) s1 += l * V[kChebMaxM + c1 + c];
+                }
+                V[i] -= s0;
+                if (nr > 1) V[kChebMaxM + i] -= s1;
+            }
+            __syncthreads();
+        }
+        // backward L^T z = y, right-looking over J = T-1 .. 0 (as large_block)
+        for (int J = T - 1; J >= 0; --J) {
+            const int c1 = kT * J, jmax = min(kT, m - c1);
+            for (int e = tid; e < kT * kT; e += NT) {
+                const int rr = e >> 5, cc = e & 31;
+                Dt[rr * kTS + cc] = (cc >= rr && cc < jmax) ? A[static_cast<int64_t>(c1 + rr) * ld + c1 + cc] : 0.0;
+            }
+            __syncthreads();
+            {   // x_J[c] = sum_{kk >= c} X[kk][c] v[c1 + kk]
+                const int c = tid & 31, g = tid >> 5;
+                for (int q = 0; q < nr; ++q) {
+                    double sx = 0.0;
+                    for (int kk = c + g; kk < jmax; kk += NG) sx += Dt[c * kTS + kk] * V[q * kChebMaxM + c1 + kk];
+                    red[(q * NG + g) * kT + c] = sx;
+                }
+            }
+            __syncthreads();
+            if (tid < kT * nr) {
+                const int c = tid & 31, q = tid >> 5;
+                double sx = 0.0;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) sx += red[(q * NG + g) * kT + c];
+                if (c < jmax) V[q * kChebMaxM + c1 + c] = sx;
+            }
+            __syncthreads();
+            // v[col] -= sum_r L[c1 + r][col] x[r] for col < c1
+            for (int col = tid; col < c1; col += NT) {
+                double s0 = 0.0, s1 = 0.0;
+                for (int r = 0; r < jmax; ++r) {
+                    const double l = A[static_cast<int64_t>(c1 + r) * ld + col];
+                    s0 += l * V[c1 + r];
+                    if (nr > 1) s1 += l * V[kChebMaxM + c1 + r];
+                }
+                V[col] -= s0;
+                if (nr > 1) V[kChebMaxM + col] -= s1;
+            }
+            __syncthreads();
+        }
+        // Chebyshev update (V = M_b^{-1} r)
+        const double* cf = coef + static_cast<int64_t>(k) * nr * 3;
+        for (int e = tid; e < nr * kChebMaxM; e += NT) {
+            const int q = e / kChebMaxM, i = e - q * kChebMaxM;
+            if (i >= m) continue;
+            const double al = cf[3 * q], be = cf[3 * q + 1], de = cf[3 * q + 2];
+            const double d = al * Dv[e] + be * V[e];
+            X[e] += d;
+            if (k + 1 < iters) {
+                const double s2 = al * Sv[e] + be * R[e];
+                Dv[e] = d;
+                Sv[e] = s2;
+                R[e] = R[e] - s2 - (i < ms ? de * d : 0.0);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace chol
+
+// Chebyshev h2f copies (cheb_block) of the ld > 64 blocks for one launch group of copies c0 (and
+// c1 when nr = 2): workgroup g = block order[g]; M_base = the base copy's factors, x_base its
+// solution (slot vector), coef = the group's [iters][nr][3] {alpha, beta, delta}.
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_cheb(
+    const double* __restrict__ M_base, const int32_t* __restrict__ order, int32_t n_blocks,
+    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
+    const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
+    const int64_t* __restrict__ blk_matoff, const int32_t* __restrict__ blk_id,
+    const int32_t* __restrict__ slot_out, const double* __restrict__ x_base,
+    const double* __restrict__ coef, int32_t nr, int32_t iters, double inv_sqrt_n,
+    double* __restrict__ beta_s, double* __restrict__ beta_l, int64_t bs_stride, int64_t bl_stride,
+    const int32_t* __restrict__ st_base, int32_t* __restrict__ status, int64_t st_stride,
+    int32_t c0, int32_t c1) {
+    using namespace chol;
+    const int g = static_cast<int>(blockIdx.x);
+    if (g >= n_blocks) return;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int b = order[g];
+    const int row0 = blk_row0[b], m = blk_m[b], ms = blk_ms[b], ld = blk_ld[b];
+    const int tid = threadIdx.x;
+    const int32_t st = st_base[blk_id[b]];
+    const bool fail = st >= DBSLMM_BLOCK_NOT_PD;
+    if (tid < nr) status[(tid == 0 ? c0 : c1) * st_stride + blk_id[b]] = st;
+    double* X = lds;
+    double* R = X + kChebR * kChebMaxM;
+    double* Dv = R + kChebR * kChebMaxM;
+    double* Sv = Dv + kChebR * kChebMaxM;
+    if (!fail) {
+        for (int e = tid; e < nr * kChebMaxM; e += kLargeThreads) {
+            const int q = e / kChebMaxM, i = e - q * kChebMaxM;
+            const double xb = i < m ? x_base[row0 + i] : 0.0;
+            X[e] = xb;
+            R[e] = i < ms ? -coef[3 * q + 2] * xb : 0.0;
+            Dv[e] = 0.0;
+            Sv[e] = 0.0;
+        }
+        __syncthreads();
+        cheb_block(M_base + blk_matoff[b], ld, m, ms, nr, iters, coef, lds);
+    }
+    for (int e = tid; e < nr * m; e += kLargeThreads) {
+        const int q = e / m, i = e - q * m;
+        const int cq = q == 0 ? c0 : c1;
+        const double v = fail ? __builtin_nan("") : X[q * kChebMaxM + i] * inv_sqrt_n;
+        const int o = slot_out[row0 + i];
+        if (o >= 0) beta_s[cq * bs_stride + o] = v;
+        else beta_l[cq * bl_stride - 1 - o] = v;
+    }
+}
 
 // Blocks with ld <= 64: one wave each, kSmallWaves per workgroup.
 extern "C" __global__ __launch_bounds__(chol::kSmallWaves * chol::kWave) void dbslmm_chol_small(

@@ -80,6 +80,35 @@ __device__ __forceinline__ v4i expand_dose(uint32_t w) {
     return out;
 }
 
+// The Gram kernels multiply on the FP4 matrix cores: dosages 0 / 1 / 2 (and the 0 / 1 masks of
+// the missing-call form) are exact e2m1 values, every product is exact and every partial sum an
+// integer below 4 n_ref < 2^24, so v_mfma_scale_f32_32x32x64_f8f6f4 with unit E8M0 scales gives
+// the integer Gram bit for bit -- at twice the MACs per clock of v_mfma_i32_32x32x32_i8, with half
+// its operand bytes.  A Gp dword (16 two-bit codes c) becomes two FP4 dwords with one shift and one
+// mask each: (w << 1) & 0x66666666 puts the even-numbered codes in the nibbles as e2m1 (c << 1 =
+// 0.0 / 1.0 / 2.0), (w >> 1) & 0x66666666 the odd ones (a fixed permutation of the individuals, the
+// same on both operands, so every product sums each individual once).
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+constexpr int kE8M0One = 0x7F7F7F7F;       // E8M0 scale 2^0 in every byte
+// 16 B of FP4 operand (32 individuals) from Gp dwords w0, w1
+__device__ __forceinline__ v4i fp4_chunk(uint32_t w0, uint32_t w1) {
+    return v4i{static_cast<int>((w0 << 1) & 0x66666666u), static_cast<int>((w0 >> 1) & 0x66666666u),
+               static_cast<int>((w1 << 1) & 0x66666666u), static_cast<int>((w1 >> 1) & 0x66666666u)};
+}
+// C += A B^T over 64 individuals (32 per lane half), 32 x 32 tile
+__device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
+    const v8i a8{a[0], a[1], a[2], a[3], 0, 0, 0, 0}, b8{b[0], b[1], b[2], b[3], 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
+}
+// missing-call form of a Gp dword (code 3 = missing): g = the dosages with missing calls as 0,
+// o = 1 for observed calls (padding individuals count as observed: pad_k in the epilogue)
+__device__ __forceinline__ void split_missing(uint32_t x, uint32_t& g, uint32_t& o) {
+    const uint32_t m2 = x & (x >> 1) & 0x55555555u;
+    g = x & ~(3u * m2);
+    o = m2 ^ 0x55555555u;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -207,55 +236,48 @@ __device__ __forceinline__ int copy_hi(int m, int32_t tmin, int32_t tcopy, int32
 }
 
 // One 32 x 32 output tile (rows r0.., cols c0.. of block-local slots) on one wave, K over all
-// kpad individuals with operands straight from Gp (L2).  Per 128 individuals (8 Gp dwords) lane
-// (row, h = lane >> 5) loads dwords 4 h .. 4 h + 3 of its row and feeds dword 4 h + s to MFMA s:
-// both operands use the same individual -> k map, so every product sums each individual once.
-// missing: the four products GG, GO, OG, OO of the observed-call expansion.
+// kpad individuals with operands straight from Gp (L2), FP4 MFMAs.  Per 128 individuals (8 Gp
+// dwords) lane (row, h = lane >> 5) loads dwords 4 h .. 4 h + 3 of its row and feeds dwords
+// 4 h + 2 s, 4 h + 2 s + 1 to MFMA s: both operands use the same individual -> k map, so every
+// product sums each individual once.  missing: the four products GG, GO, OG, OO of the
+// observed-call expansion.
 __device__ __forceinline__ void gram_tile32(
     const uint32_t* __restrict__ Gp, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
     int r0, int c0, int lane, const double* __restrict__ S, const double* __restrict__ mu,
     const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M,
     int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
-    const int64_t kw = kpad / 16;                 // Gp dwords per slot (kpad: a multiple of 128)
+    const int64_t kw = kpad / 16;                 // Gp dwords per slot (kpad: a multiple of 256)
     const uint32_t* pa = Gp + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kw + 4 * (lane >> 5);
     const uint32_t* pb = Gp + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kw + 4 * (lane >> 5);
 
-    v16i acc = {0};
-    v16i acc_go = {0}, acc_og = {0}, acc_oo = {0};
+    v16f acc = {0.0f};
+    v16f acc_go = {0.0f}, acc_og = {0.0f}, acc_oo = {0.0f};
     if (!missing) {
         for (int64_t w = 0; w < kw; w += 8) {
             const v4i wa = *reinterpret_cast<const v4i*>(pa + w);
             const v4i wb = *reinterpret_cast<const v4i*>(pb + w);
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(expand_dose(static_cast<uint32_t>(wa[q])),
-                                                            expand_dose(static_cast<uint32_t>(wb[q])), acc, 0, 0, 0);
+            for (int q = 0; q < 2; ++q)
+                acc = mfma_fp4(fp4_chunk(static_cast<uint32_t>(wa[2 * q]), static_cast<uint32_t>(wa[2 * q + 1])),
+                               fp4_chunk(static_cast<uint32_t>(wb[2 * q]), static_cast<uint32_t>(wb[2 * q + 1])), acc);
         }
     } else {
-        // code y = dosage or 3 (missing): m = y & (y >> 1), g = y without the missing, o = 1 - m
         for (int64_t w = 0; w < kw; w += 8) {
           const v4i wa = *reinterpret_cast<const v4i*>(pa + w);
           const v4i wb = *reinterpret_cast<const v4i*>(pb + w);
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const v4i a0 = expand_dose(static_cast<uint32_t>(wa[s4]));
-            const v4i b0 = expand_dose(static_cast<uint32_t>(wb[s4]));
-            v4i ga, oa, gb, ob;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t xa = static_cast<uint32_t>(a0[q]);
-                const uint32_t xb = static_cast<uint32_t>(b0[q]);
-                const uint32_t ma = xa & (xa >> 1) & 0x01010101u;
-                const uint32_t mb = xb & (xb >> 1) & 0x01010101u;
-                ga[q] = static_cast<int>(xa & ~(3u * ma));
-                gb[q] = static_cast<int>(xb & ~(3u * mb));
-                oa[q] = static_cast<int>(ma ^ 0x01010101u);
-                ob[q] = static_cast<int>(mb ^ 0x01010101u);
-            }
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ga, gb, acc, 0, 0, 0);
-            acc_go = __builtin_amdgcn_mfma_i32_32x32x32_i8(ga, ob, acc_go, 0, 0, 0);
-            acc_og = __builtin_amdgcn_mfma_i32_32x32x32_i8(oa, gb, acc_og, 0, 0, 0);
-            acc_oo = __builtin_amdgcn_mfma_i32_32x32x32_i8(oa, ob, acc_oo, 0, 0, 0);
+          for (int q = 0; q < 2; ++q) {
+            uint32_t ga0, oa0, ga1, oa1, gb0, ob0, gb1, ob1;
+            split_missing(static_cast<uint32_t>(wa[2 * q]), ga0, oa0);
+            split_missing(static_cast<uint32_t>(wa[2 * q + 1]), ga1, oa1);
+            split_missing(static_cast<uint32_t>(wb[2 * q]), gb0, ob0);
+            split_missing(static_cast<uint32_t>(wb[2 * q + 1]), gb1, ob1);
+            const v4i ga = fp4_chunk(ga0, ga1), oa = fp4_chunk(oa0, oa1);
+            const v4i gb = fp4_chunk(gb0, gb1), ob = fp4_chunk(ob0, ob1);
+            acc = mfma_fp4(ga, gb, acc);
+            acc_go = mfma_fp4(ga, ob, acc_go);
+            acc_og = mfma_fp4(oa, gb, acc_og);
+            acc_oo = mfma_fp4(oa, ob, acc_oo);
           }
         }
     }
@@ -311,19 +333,19 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
 
 // ------------------------------------------------------------------------------------------
 // Kernel 2b: the same Gram for blocks without missing calls, 128 x 128 output tile per
-// 256-thread workgroup (wave w: 64 x 64 quadrant (w >> 1, w & 1) = 2 x 2 MFMA 32x32x32 i8).
-// K runs in stages of 128 individuals through double-buffered LDS (row stride 144 B: the 16 rows
-// of a ds_read_b128 lane group land on 16 distinct 16-B bank groups); global loads run ahead of
-// the current stage's 16 MFMAs per wave (see below).  Diagonal tiles stage
-// one operand and skip the strictly-upper quadrant.  Global loads run two stages ahead (two
-// register sets, loop unrolled by two).  Tiles come in per-XCD queues (entry e runs
-// on XCD e % 8) so a block's rows stay in one L2; entries with block < 0 are padding.
-// Blocks with a missing call (flag set by the unpack) take the exact 4-product 32 x 32 path.
+// 256-thread workgroup (wave w: 64 x 64 quadrant (w >> 1, w & 1) = 2 x 2 FP4 MFMA 32x32x64).
+// K runs in stages of 256 individuals through double-buffered LDS: 128 B of FP4 codes per row,
+// row stride 144 B (the 16 rows of a ds_read_b128 lane group land on 16 distinct 16-B bank
+// groups); global loads run two stages ahead (two register sets, loop unrolled by two) of the
+// current stage's 16 MFMAs per wave.  Diagonal tiles stage one operand and skip the
+// strictly-upper quadrant.  Tiles come in per-XCD queues (entry e runs on XCD e % 8) so a block's
+// rows stay in one L2; entries with block < 0 are padding.  Blocks with a missing call (flag set
+// by the unpack) take the exact 4-product 32 x 32 path.
 // ------------------------------------------------------------------------------------------
 namespace gram {
 constexpr int kGT = 128;                  // output tile edge
-constexpr int kKS = 128;                  // individuals (bytes) per K stage
-constexpr int kRS = kKS + 16;             // LDS row stride (bytes)
+constexpr int kKS = 256;                  // individuals per K stage
+constexpr int kRS = kKS / 2 + 16;         // LDS row stride (bytes): 128 B of FP4 codes + pad
 constexpr int kOpBytes = kGT * kRS;       // one operand stage
 constexpr int kLdsBytes = 2 * 2 * kOpBytes;   // 2 stages x (A, B) = 73,728 B
 }  // namespace gram
@@ -361,38 +383,40 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     const int64_t kw = kpad / 16;
     const uint32_t* ga = Gp + static_cast<int64_t>(row0 + kGT * tile.ti) * kw;
     const uint32_t* gb = Gp + static_cast<int64_t>(row0 + kGT * tile.tj) * kw;
-    // staging map: 128 rows x 8 Gp dwords (16 individuals each) per operand; thread t moves dwords
-    // t + 256 q and expands them to 16 B of int8 codes on the way into LDS.  Two register sets:
-    // the global loads of stage s + 2 are issued before stage s's MFMAs.
-    uint32_t ra0[4], rb0[4], ra1[4], rb1[4];
-    auto gload = [&](uint32_t (&ra)[4], uint32_t (&rb)[4], int st) {
+    // staging map: 128 rows x 16 Gp dwords (16 individuals each) per operand and stage; thread t
+    // moves dword pairs e = t + 256 q (row e >> 3, pair e & 7) and expands each pair to one 16-B
+    // FP4 chunk on the way into LDS.  Two register sets: the global loads of stage s + 2 are
+    // issued before stage s's MFMAs.
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    u2 ra0[4], rb0[4], ra1[4], rb1[4];
+    auto gload = [&](u2 (&ra)[4], u2 (&rb)[4], int st) {
         const int64_t w0 = static_cast<int64_t>(st) * (kKS / 16);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = q * 256 + tid, r = e >> 3, c = e & 7;
-            ra[q] = ga[static_cast<int64_t>(r) * kw + w0 + c];
-            if (!diag) rb[q] = gb[static_cast<int64_t>(r) * kw + w0 + c];
+            ra[q] = *reinterpret_cast<const u2*>(ga + static_cast<int64_t>(r) * kw + w0 + 2 * c);
+            if (!diag) rb[q] = *reinterpret_cast<const u2*>(gb + static_cast<int64_t>(r) * kw + w0 + 2 * c);
         }
     };
-    auto lstore = [&](const uint32_t (&ra)[4], const uint32_t (&rb)[4], int buf) {
+    auto lstore = [&](const u2 (&ra)[4], const u2 (&rb)[4], int buf) {
         int8_t* A = glds + buf * 2 * kOpBytes;
         int8_t* B = A + kOpBytes;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = q * 256 + tid, r = e >> 3, c = e & 7;
-            *reinterpret_cast<v4i*>(A + r * kRS + 16 * c) = expand_dose(ra[q]);
-            if (!diag) *reinterpret_cast<v4i*>(B + r * kRS + 16 * c) = expand_dose(rb[q]);
+            *reinterpret_cast<v4i*>(A + r * kRS + 16 * c) = fp4_chunk(ra[q][0], ra[q][1]);
+            if (!diag) *reinterpret_cast<v4i*>(B + r * kRS + 16 * c) = fp4_chunk(rb[q][0], rb[q][1]);
         }
     };
     const int wr = wave >> 1, wc = wave & 1;
     const bool idle = diag && wc > wr;            // strictly-upper quadrant of a diagonal tile
-    v16i acc[2][2];
+    v16f acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = v16i{0};
-    // operand read offsets: lane l -> row (l & 31) of a 32-row group, k bytes 16 (l >> 5) of a
-    // 32-byte k-step
+        for (int j = 0; j < 2; ++j) acc[i][j] = v16f{0.0f};
+    // operand read offsets: lane l -> row (l & 31) of a 32-row group, the 16-B half (l >> 5) of a
+    // 32-byte (64-individual) k-step
     const int rsub = lane & 31, ksub = 16 * (lane >> 5);
     auto compute = [&](int buf) {
         if (idle) return;
@@ -401,15 +425,15 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
         const int8_t* pa = A + (64 * wr + rsub) * kRS + ksub;
         const int8_t* pb = B + (64 * wc + rsub) * kRS + ksub;
 #pragma unroll
-        for (int kk = 0; kk < kKS; kk += 32) {
+        for (int kk = 0; kk < kKS / 2; kk += 32) {
             const v4i a0 = *reinterpret_cast<const v4i*>(pa + kk);
             const v4i a1 = *reinterpret_cast<const v4i*>(pa + 32 * kRS + kk);
             const v4i b0 = *reinterpret_cast<const v4i*>(pb + kk);
             const v4i b1 = *reinterpret_cast<const v4i*>(pb + 32 * kRS + kk);
-            acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
+            acc[0][0] = mfma_fp4(a0, b0, acc[0][0]);
+            acc[0][1] = mfma_fp4(a0, b1, acc[0][1]);
+            acc[1][0] = mfma_fp4(a1, b0, acc[1][0]);
+            acc[1][1] = mfma_fp4(a1, b1, acc[1][1]);
         }
     };
     const int nst = static_cast<int>(kpad / kKS);
@@ -472,8 +496,6 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 // Diagonal tiles stage one operand; MFMA tiles strictly above the diagonal or wholly past m (edge
 // tiles) are skipped.  Missing-call blocks: exact 4-product i8 path per 32 x 32 sub-tile.
 // ------------------------------------------------------------------------------------------
-typedef int v8i __attribute__((ext_vector_type(8)));
-typedef float v16f __attribute__((ext_vector_type(16)));
 namespace gram {
 constexpr int kHT = 256;                   // output tile edge
 constexpr int kHK = 256;                   // individuals per K stage
@@ -482,21 +504,11 @@ constexpr int kHOp = kHT * kHRow;          // one operand stage (32 KiB)
 constexpr int kHSlots = 2;                 // LDS double buffer
 constexpr int kHLdsBytes = kHSlots * 2 * kHOp;   // 128 KiB
 constexpr int kKpadAlign = kHK;            // kpad: a multiple of the FP4 stage
-constexpr int kE8M0One = 0x7F7F7F7F;       // E8M0 scale 2^0 in every byte
 // logical 16-B chunk c of row r at position c ^ f(r), f(r) = (r ^ r >> 2 ^ r >> 3) & 7: conflict-free
 // for the expansion writes (ds_write_b128: 8-lane groups of consecutive rows, 32 banks) and the
 // MFMA operand reads (ds_read_b128: 16-lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}
 // of 32 rows, 64 banks) -- MI355X_MICROARCH.md LDS table; (r >> 2) & 3 left the writes 2-way
 __device__ __forceinline__ int swz(int r, int c) { return r * kHRow + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 7)); }
-// 16-B LDS chunk c of a row (32 individuals) from Gp dwords 2c, 2c + 1
-__device__ __forceinline__ v4i fp4_chunk(uint32_t w0, uint32_t w1) {
-    return v4i{static_cast<int>((w0 << 1) & 0x66666666u), static_cast<int>((w0 >> 1) & 0x66666666u),
-               static_cast<int>((w1 << 1) & 0x66666666u), static_cast<int>((w1 >> 1) & 0x66666666u)};
-}
-__device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
-    const v8i a8{a[0], a[1], a[2], a[3], 0, 0, 0, 0}, b8{b[0], b[1], b[2], b[3], 0, 0, 0, 0};
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
-}
 }  // namespace gram
 
 extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(

@@ -42,6 +42,7 @@ namespace {
 // [8] / [7] around the h2f Chebyshev iterations (stream2)
 constexpr int kEvPerRun = 11;   // 9, 10: around the lead group's Gram (between the unpack halves)
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
+constexpr size_t kCholChebLds = sizeof(double) * chol::kChebLdsDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
 constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3Doubles;
@@ -535,6 +536,9 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(kCholLargeLds)) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_cheb),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(kCholChebLds)) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_big),
                             hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge),
@@ -1244,7 +1248,8 @@ struct ChebPlan {
 // M_b^{-1} M_c lies in [1, 1 + delta / (d_b + 1 - tau)] (delta > 0) or its mirror (delta < 0).
 // Not applicable (false): tau outside (0, 1], or more than 60 iterations needed.
 static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPlan& cp) {
-    if (p->h2f_mode != 0 || n < 2 || p->n_tiled == 0 || !(p->tau > 0.0 && p->tau <= 1.0)) return false;
+    if (p->h2f_mode != 0 || n < 2 || (p->n_tiled == 0 && p->n_large == 0) || !(p->tau > 0.0 && p->tau <= 1.0))
+        return false;
     std::vector<int> idx(n);
     std::iota(idx.begin(), idx.end(), 0);
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return sigmas[a] < sigmas[b]; });
@@ -1437,7 +1442,10 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     p->trsv_failed = false;
     ChebPlan cp;
     const bool cheb = front && p->n_nonempty > 0 && cheb_plan(p, sigmas, n, cp);
-    const int32_t tcopy = cheb ? cp.base : -1;   // Gram epilogues: tiled blocks write this copy only
+    const int32_t tcopy = cheb ? cp.base : -1;   // Gram epilogues: iterated blocks write this copy only
+    // ... the blocks with m >= tmin_copy: the tiled ones and the single-workgroup ones (ld > 64),
+    // whose other h2f copies iterate on the base factor too (dbslmm_chol_cheb)
+    const int32_t tmin_copy = chol::kSmallLd;
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
     if (p->timing) {
@@ -1493,7 +1501,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_htiles + t0, nt, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
+                           p->tau, p->d_M, n, p->M_elems, tmin_copy, tcopy);
     };
     if (front && p->n_htiles_lead > 0) {
         gram_huge(0, p->n_htiles_lead);
@@ -1526,7 +1534,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
                            static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M, n, p->M_elems,
-                           p->tiled_min, tcopy);
+                           tmin_copy, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_htiles > p->n_htiles_tiled) {
@@ -1538,7 +1546,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems, p->tiled_min, tcopy);
+                           p->tau, p->d_M, n, p->M_elems, tmin_copy, tcopy);
         HIP_TRY(ctx, hipGetLastError());
     }
     // (the factorisation overwrites its matrix: the Gram epilogues write all n copies)
@@ -1550,7 +1558,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
             HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
         }
-        if (p->n_large > 0) {   // every copy in one launch
+        if (p->n_large > 0 && !cheb) {   // every copy in one launch
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large * n), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M, p->d_order, p->n_large,
                                p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
@@ -1558,6 +1566,27 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                                p->d_status, n, p->M_elems, static_cast<int64_t>(p->n_slots), p->n_s, p->n_l,
                                p->nbk);
             HIP_TRY(ctx, hipGetLastError());
+        } else if (p->n_large > 0) {
+            // h2f by Chebyshev: the base copy is factored, the others iterate on its factor
+            const int64_t bc = cp.base;
+            hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large), dim3(chol::kLargeThreads), kCholLargeLds, s,
+                               p->d_M + bc * p->M_elems, p->d_order, p->n_large, p->d_row0, p->d_m, p->d_ms,
+                               p->d_ld, p->d_matoff, p->d_blk_id, p->d_z, p->d_slot_out, p->d_rsd,
+                               p->d_dshift + bc, isn, p->d_y + bc * p->n_slots, p->d_beta_s + bc * p->n_s,
+                               p->d_beta_l + bc * p->n_l, p->d_status + bc * p->nbk, 1, p->M_elems,
+                               static_cast<int64_t>(p->n_slots), p->n_s, p->n_l, p->nbk);
+            HIP_TRY(ctx, hipGetLastError());
+            for (size_t g = 0; g < cp.iters.size(); ++g) {
+                const size_t g0 = g * chol::kChebR;
+                const int nr = static_cast<int>(std::min<size_t>(chol::kChebR, cp.others.size() - g0));
+                hipLaunchKernelGGL(dbslmm_chol_cheb, dim3(p->n_large), dim3(chol::kLargeThreads), kCholChebLds, s,
+                                   p->d_M + bc * p->M_elems, p->d_order, p->n_large, p->d_row0, p->d_m, p->d_ms,
+                                   p->d_ld, p->d_matoff, p->d_blk_id, p->d_slot_out, p->d_y + bc * p->n_slots,
+                                   p->d_coef + cp.coef_off[g], nr, cp.iters[g], isn, p->d_beta_s, p->d_beta_l,
+                                   p->n_s, p->n_l, p->d_status + bc * p->nbk, p->d_status,
+                                   static_cast<int64_t>(p->nbk), cp.others[g0], nr > 1 ? cp.others[g0 + 1] : 0);
+                HIP_TRY(ctx, hipGetLastError());
+            }
         }
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], s));
         // single-wave blocks: concurrently on stream2 when there is no tiled sequence, else
