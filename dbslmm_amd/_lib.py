@@ -19,10 +19,10 @@ EXPORTS = (
     "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
     "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
     "dbslmm_ctx_create_multi", "dbslmm_ctx_num_devices", "dbslmm_plan_shard_info",
-    "dbslmm_ctx_cache_bed",
+    "dbslmm_ctx_cache_bed", "dbslmm_ctx_cache_bed_fd",
 )
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv")
@@ -99,6 +99,7 @@ def load(path: str | None = None):
     L.dbslmm_valid_blocks.argtypes = [V, V, C.c_int64, C.c_int32, C.c_int32, V, V, V, V, V, V]
     L.dbslmm_plan_variance.argtypes = [V, P(TestPanel), V, V]
     L.dbslmm_ctx_cache_bed.argtypes = [V, V, C.c_int64]
+    L.dbslmm_ctx_cache_bed_fd.argtypes = [V, C.c_int, C.c_int64, V]
     if L.dbslmm_abi_version() != ABI_VERSION:
         raise DbslmmError("ABI version mismatch")
     _lib = L

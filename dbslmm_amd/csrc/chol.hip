@@ -561,11 +561,12 @@ __device__ void large_block(const BlockArgs& a, double* __restrict__ M, double* 
 // passes (~8 m^2 flops) with far less LDS per workgroup, so several blocks share a CU.
 constexpr int kChebR = 2;                           // copies per launch group (trsv::kMaxR)
 constexpr int kChebMaxM = 512;                      // ld > 64 blocks are below the tiled threshold
-constexpr int kChebLdsDoubles = 5 * kChebR * kChebMaxM + kTileD + kChebR * 8 * kT;
+constexpr int kChebThreads = 512;                   // one strip row / column per thread (m <= 512)
+constexpr int kChebLdsDoubles = 5 * kChebR * kChebMaxM + kTileD + kChebR * (kChebThreads / kT) * kT;
 
 __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, int nr, int iters,
                            const double* __restrict__ coef, double* lds) {
-    constexpr int NT = kLargeThreads, NG = NT / kT;
+    constexpr int NT = kChebThreads, NG = NT / kT;
     const int tid = threadIdx.x;
     double* X = lds;                                 // [kChebR][kChebMaxM] each
     double* R = X + kChebR * kChebMaxM;
@@ -578,9 +579,16 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
     for (int k = 0; k < iters; ++k) {
         for (int e = tid; e < nr * kChebMaxM; e += NT) V[e] = R[e];
         __syncthreads();
-        // forward L y = r: right-looking over the tiles
+        // forward L y = r: right-looking over the tiles.  Per tile, the diagonal block and the
+        // strip below it (rows i0 = c1 + 32 + tid and i0 + 256: m <= 512) are loaded together up
+        // front, so a tile step waits for one round of loads
         for (int J = 0; J < T; ++J) {
             const int c1 = kT * J, jmax = min(kT, m - c1);
+            v2d l0[kT / 2];
+            const int i0 = c1 + kT + tid;                 // m <= 512: one row per thread
+#pragma unroll
+            for (int c = 0; c < kT / 2; ++c)
+                l0[c] = i0 < m ? reinterpret_cast<const v2d*>(A + static_cast<int64_t>(i0) * ld + c1)[c] : v2d{0.0, 0.0};
             for (int e = tid; e < kT * kT; e += NT) {
                 const int rr = e >> 5, cc = e & 31;   // stored (rr, cc >= rr) = X[cc][rr]
                 Dt[rr * kTS + cc] = (cc >= rr && cc < jmax) ? A[static_cast<int64_t>(c1 + rr) * ld + c1 + cc] : 0.0;
@@ -604,22 +612,29 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
             }
             __syncthreads();
             // v_i -= L[i][c1 ..] y_J for the rows below the tile
-            for (int i = c1 + kT + tid; i < m; i += NT) {
-                const double* Li = A + static_cast<int64_t>(i) * ld + c1;
+            if (i0 < m) {
                 double s0 = 0.0, s1 = 0.0;
-                for (int c = 0; c < jmax; ++c) {
-                    const double l = Li[c];
-                    s0 += l * V[c1 + c];
-                    if (nr > 1) s1 += l * V[kChebMaxM + c1 + c];
+#pragma unroll
+                for (int c = 0; c < kT; ++c) {
+                    const double y0 = c < jmax ? V[c1 + c] : 0.0;
+                    const double y1 = (nr > 1 && c < jmax) ? V[kChebMaxM + c1 + c] : 0.0;
+                    s0 += l0[c >> 1][c & 1] * y0;
+                    s1 += l0[c >> 1][c & 1] * y1;
                 }
-                V[i] -= s0;
-                if (nr > 1) V[kChebMaxM + i] -= s1;
+                V[i0] -= s0;
+                if (nr > 1) V[kChebMaxM + i0] -= s1;
             }
             __syncthreads();
         }
-        // backward L^T z = y, right-looking over J = T-1 .. 0 (as large_block)
+        // backward L^T z = y, right-looking over J = T-1 .. 0 (as large_block); the strip
+        // L[c1 + r][col], col < c1 (columns tid and tid + 256), loaded with the diagonal block
         for (int J = T - 1; J >= 0; --J) {
             const int c1 = kT * J, jmax = min(kT, m - c1);
+            double l0[kT];
+            const int col0 = tid;                          // c1 < 512: one column per thread
+#pragma unroll
+            for (int r = 0; r < kT; ++r)
+                l0[r] = (col0 < c1 && r < jmax) ? A[static_cast<int64_t>(c1 + r) * ld + col0] : 0.0;
             for (int e = tid; e < kT * kT; e += NT) {
                 const int rr = e >> 5, cc = e & 31;
                 Dt[rr * kTS + cc] = (cc >= rr && cc < jmax) ? A[static_cast<int64_t>(c1 + rr) * ld + c1 + cc] : 0.0;
@@ -643,15 +658,17 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
             }
             __syncthreads();
             // v[col] -= sum_r L[c1 + r][col] x[r] for col < c1
-            for (int col = tid; col < c1; col += NT) {
+            if (col0 < c1) {
                 double s0 = 0.0, s1 = 0.0;
-                for (int r = 0; r < jmax; ++r) {
-                    const double l = A[static_cast<int64_t>(c1 + r) * ld + col];
-                    s0 += l * V[c1 + r];
-                    if (nr > 1) s1 += l * V[kChebMaxM + c1 + r];
+#pragma unroll
+                for (int r = 0; r < kT; ++r) {
+                    const double x0 = r < jmax ? V[c1 + r] : 0.0;
+                    const double x1 = (nr > 1 && r < jmax) ? V[kChebMaxM + c1 + r] : 0.0;
+                    s0 += l0[r] * x0;
+                    s1 += l0[r] * x1;
                 }
-                V[col] -= s0;
-                if (nr > 1) V[kChebMaxM + col] -= s1;
+                V[col0] -= s0;
+                if (nr > 1) V[kChebMaxM + col0] -= s1;
             }
             __syncthreads();
         }
@@ -679,7 +696,7 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
 // Chebyshev h2f copies (cheb_block) of the ld > 64 blocks for one launch group of copies c0 (and
 // c1 when nr = 2): workgroup g = block order[g]; M_base = the base copy's factors, x_base its
 // solution (slot vector), coef = the group's [iters][nr][3] {alpha, beta, delta}.
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_cheb(
+extern "C" __global__ __launch_bounds__(chol::kChebThreads) void dbslmm_chol_cheb(
     const double* __restrict__ M_base, const int32_t* __restrict__ order, int32_t n_blocks,
     const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
     const int32_t* __restrict__ blk_ms, const int32_t* __restrict__ blk_ld,
@@ -704,7 +721,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_ch
     double* Dv = R + kChebR * kChebMaxM;
     double* Sv = Dv + kChebR * kChebMaxM;
     if (!fail) {
-        for (int e = tid; e < nr * kChebMaxM; e += kLargeThreads) {
+        for (int e = tid; e < nr * kChebMaxM; e += kChebThreads) {
             const int q = e / kChebMaxM, i = e - q * kChebMaxM;
             const double xb = i < m ? x_base[row0 + i] : 0.0;
             X[e] = xb;
@@ -715,7 +732,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_chol_ch
         __syncthreads();
         cheb_block(M_base + blk_matoff[b], ld, m, ms, nr, iters, coef, lds);
     }
-    for (int e = tid; e < nr * m; e += kLargeThreads) {
+    for (int e = tid; e < nr * m; e += kChebThreads) {
         const int q = e / m, i = e - q * m;
         const int cq = q == 0 ? c0 : c1;
         const double v = fail ? __builtin_nan("") : X[q * kChebMaxM + i] * inv_sqrt_n;

@@ -557,7 +557,7 @@ int main(int argc, char** argv) {
                 if (dbslmm_ctx_create(p.gpu, &ctx) != DBSLMM_OK) { gpu_err = "no usable HIP device (dbslmm_ctx_create)"; return; }
                 t_ctx = walltime() - t;
                 t = walltime();
-                if (dbslmm_ctx_cache_bed(ctx, bed.p, static_cast<int64_t>(bed.n)) != DBSLMM_OK) {
+                if (dbslmm_ctx_cache_bed_fd(ctx, bed.fd, static_cast<int64_t>(bed.n), bed.p) != DBSLMM_OK) {
                     gpu_err = string("uploading the .bed: ") + dbslmm_last_error(ctx);
                     return;
                 }

@@ -13,6 +13,7 @@
 // The whole problem stays resident; plan_run re-executes unpack -> gram -> chol from the
 // packed genotypes (nothing cached between runs except the uploaded inputs).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -102,6 +103,13 @@ struct dbslmm_ctx {
     uint8_t* d_bed_cache = nullptr;    // bed_cache.get()
     std::vector<dbslmm_ctx*> subs;   // multi-device context (multi.hip): one context per device,
                                      // device = -1 and no streams of its own
+    // dbslmm_ctx_create returns once the main stream exists; the other streams, the events and the
+    // kernel attributes are set up on this thread meanwhile (each stream costs ~15-30 ms of HIP
+    // runtime time), joined by ctx_ready() before anything uses them.  dbslmm_ctx_cache_bed and
+    // dbslmm_bed_maf need only the main stream, so a .bed upload overlaps the rest of the set-up.
+    std::thread setup;
+    std::mutex setup_mu;
+    bool setup_ok = true;
 };
 struct dbslmm_plan;
 // the shards of a multi-device plan (multi.hip)
@@ -181,6 +189,9 @@ struct dbslmm_plan {
     // iteration vectors [Y, Z, X, R, D, S] x kMaxR x n_slots
     int32_t *d_tri_f = nullptr, *d_tri_b = nullptr, *d_foff = nullptr, *d_tflags = nullptr, *d_tb = nullptr;
     int32_t n_titems = 0, n_tflags = 0;
+    int32_t* d_tepi = nullptr;                 // per tile: epoch of its last stored Chebyshev update
+    int32_t* d_cheb_items = nullptr;           // work list of the fused Chebyshev launch (K iterations)
+    int32_t n_cheb_items = 0, cheb_items_K = -1;
     int32_t trsv_epoch = 0;                  // tile-flag value of the latest substitution launch
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
     int32_t h2f_mode = 0;                    // dbslmm_options.h2f_mode
@@ -267,6 +278,53 @@ static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_
         }
         for (auto& t : th) t.join();
         e = hipMemcpyAsync(static_cast<char*>(dst) + off, stage[b], len, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(done[b], st);
+    }
+    const hipError_t e2 = hipStreamSynchronize(st);
+    for (int b = 0; b < 2; ++b) {
+        if (done[b]) (void)hipEventDestroy(done[b]);
+        if (stage[b]) (void)hipHostFree(stage[b]);
+    }
+    return e != hipSuccess ? e : e2;
+}
+
+// upload_staged reading the bytes from a file descriptor (pread straight into the pinned staging
+// buffers, several threads per chunk): the caller's pages of the file are never faulted in, so
+// neither the copy nor the process's exit pays for hundreds of thousands of page-table entries.
+static hipError_t upload_staged_fd(void* dst, int fd, size_t n, hipStream_t st) {
+    constexpr size_t kChunk = size_t(64) << 20;
+    void* stage[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+        e = hipHostMalloc(&stage[b], kChunk, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&done[b], hipEventDisableTiming);
+    }
+    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (size_t off = 0, k = 0; off < n && e == hipSuccess; off += kChunk, ++k) {
+        const int b = static_cast<int>(k & 1);
+        const size_t len = std::min(kChunk, n - off);
+        if (k >= 2 && (e = hipEventSynchronize(done[b])) != hipSuccess) break;   // buffer b free again
+        char* d0 = static_cast<char*>(stage[b]);
+        std::vector<std::thread> th;
+        std::vector<char> ok(hw, 1);
+        const size_t part = (len + hw - 1) / hw;
+        for (unsigned t = 0; t < hw; ++t) {
+            const size_t a = t * part, z = std::min(len, a + part);
+            if (a < z)
+                th.emplace_back([=, &ok] {
+                    size_t got = a;
+                    while (got < z) {
+                        const ssize_t r = pread(fd, d0 + got, z - got, static_cast<off_t>(off + got));
+                        if (r <= 0) { ok[t] = 0; return; }
+                        got += static_cast<size_t>(r);
+                    }
+                });
+        }
+        for (auto& t : th) t.join();
+        for (char o : ok)
+            if (!o) e = hipErrorInvalidValue;
+        if (e == hipSuccess) e = hipMemcpyAsync(static_cast<char*>(dst) + off, stage[b], len, hipMemcpyHostToDevice, st);
         if (e == hipSuccess) e = hipEventRecord(done[b], st);
     }
     const hipError_t e2 = hipStreamSynchronize(st);
@@ -502,8 +560,22 @@ static hipError_t set_trsv_lds() {
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        static_cast<int>(trsv::kLdsBytes));
     if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_cheb<NR>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
+    if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_bwd<NR>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
+}
+
+// the deferred part of dbslmm_ctx_create (streams 2-5, events, kernel attributes) is done
+static int ctx_ready(dbslmm_ctx* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->setup_mu);
+    if (ctx->setup.joinable()) ctx->setup.join();
+    if (!ctx->setup_ok) {
+        ctx->err = "context set-up (streams / events / kernel attributes) failed";
+        return DBSLMM_E_HIP;
+    }
+    return DBSLMM_OK;
 }
 
 extern "C" {
@@ -518,51 +590,56 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
     if (device < 0 || device >= n) return DBSLMM_E_ARG;
     auto* c = new dbslmm_ctx();
     c->device = device;
-    int prio_lo = 0, prio_hi = 0;   // the tiled sequence is the critical path: high priority
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        // the lead (or only) sequence's bulk trailing stream high too: its far updates pace the
-        // lead chain (normal priority left config 5 bimodal, 34 / 39 ms per step)
-        hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->fork2, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->join4, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kCholLargeLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_cheb),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kCholChebLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_big),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_region),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kRegionLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_panel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTiledLds)) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(kTrail3Lds)) != hipSuccess ||
-        set_trsv_lds<1>() != hipSuccess || set_trsv_lds<2>() != hipSuccess ||
         hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
         dbslmm_ctx_destroy(c);
         return DBSLMM_E_HIP;
     }
+    c->setup = std::thread([c, device] {
+        int prio_lo = 0, prio_hi = 0;   // the tiled sequence is the critical path: high priority
+        c->setup_ok =
+            hipSetDevice(device) == hipSuccess &&
+            hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+            // the lead (or only) sequence's bulk trailing stream high too: its far updates pace the
+            // lead chain (normal priority left config 5 bimodal, 34 / 39 ms per step)
+            hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->fork2, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->join4, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->join, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->join3, hipEventDisableTiming) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_large),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(kCholLargeLds)) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_chol_cheb),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(kCholChebLds)) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_big),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_region),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(kRegionLds)) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_panel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(kTiledLds)) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(kTrail3Lds)) == hipSuccess &&
+            set_trsv_lds<1>() == hipSuccess && set_trsv_lds<2>() == hipSuccess;
+    });
     *out = c;
     return DBSLMM_OK;
 }
 
 void dbslmm_ctx_destroy(dbslmm_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->setup.joinable()) ctx->setup.join();
     for (dbslmm_ctx* s : ctx->subs) dbslmm_ctx_destroy(s);
     if (ctx->device < 0) {
         delete ctx;
@@ -610,6 +687,34 @@ int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len) {
     return DBSLMM_OK;
 }
 
+int dbslmm_ctx_cache_bed_fd(dbslmm_ctx* ctx, int fd, int64_t bed_len, const uint8_t* key) {
+    if (!ctx) return DBSLMM_E_ARG;
+    if (!ctx->subs.empty()) return DBSLMM_OK;   // multi-device: each device gets its own rows
+    ARG_CHECK(ctx, fd >= 0 && key && bed_len > 0, "fd / bed_len / key");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ctx->bed_cache.reset();
+    ctx->d_bed_cache = nullptr;
+    ctx->bed_host = nullptr;
+    ctx->bed_host_len = 0;
+    uint8_t* d = nullptr;
+    HIP_TRY(ctx, hipMalloc(&d, bed_len + 16));
+    const int dev = ctx->device;
+    ctx->bed_cache = std::shared_ptr<uint8_t>(d, [dev](uint8_t* q) {
+        (void)hipSetDevice(dev);
+        (void)hipFree(q);
+    });
+    HIP_TRY(ctx, hipMemset(d + bed_len, 0, 16));
+    if (upload_staged_fd(d, fd, static_cast<size_t>(bed_len), ctx->stream) != hipSuccess) {
+        ctx->bed_cache.reset();
+        ctx->err = "reading / uploading the .bed from its file descriptor failed";
+        return DBSLMM_E_HIP;
+    }
+    ctx->d_bed_cache = d;
+    ctx->bed_host = key;
+    ctx->bed_host_len = bed_len;
+    return DBSLMM_OK;
+}
+
 void dbslmm_plan_destroy(dbslmm_plan* p) {
     if (!p) return;
     if (p->mp) {
@@ -626,7 +731,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
-                    p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order};
+                    p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -646,6 +751,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if (!ctx->subs.empty()) return mp_create(ctx, pr, out);
     ARG_CHECK(ctx, pr && out, "null problem/out");
     *out = nullptr;
+    if (const int rc = ctx_ready(ctx)) return rc;
     ARG_CHECK(ctx, pr->bed && pr->n_ref > 1 && pr->n_obs > 0 && pr->num_block >= 0, "bad sizes");
     // the FP4 Gram accumulates integers up to 4 n_ref in fp32 (exact below 2^24)
     ARG_CHECK(ctx, pr->n_ref < (1 << 22), "n_ref must be below 4,194,304 (exact FP4 Gram accumulation)");
@@ -985,6 +1091,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     // [tile flags | ticket counter | error word | spare]
     if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
     if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
+    if ((e = hipMalloc(&p->d_tepi, std::max(1, p->n_tflags) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
+    if ((e = hipMemset(p->d_tepi, 0, std::max(1, p->n_tflags) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
     if ((e = hipMalloc(&p->d_mu, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -1337,20 +1445,76 @@ static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
     return DBSLMM_OK;
 }
 
+// Work list of the fused Chebyshev launch (dbslmm_trsv_cheb) for K iterations: every (tiled
+// block, pass p < 2K, tile) item, the passes alternating forward (tiles 0 .. T-1) and backward
+// (T-1 .. 0).  Keys model when an item can run: a block's chain needs (p T + pos) steps of
+// kChainStep, and the bulk of the substitutions streams at kStreamBw, so a block cannot usefully
+// run ahead of its share of the bytes either: key = max(chain time, bulk time).  Both grow along
+// each block's own order, so every dependency has a smaller ticket (deadlock-free for any
+// residency); across blocks the small ones finish their iterations early at the memory bandwidth
+// while the largest blocks' chains go on beside them and then alone.
+static void build_cheb_items(const dbslmm_plan* p, int K, std::vector<int32_t>& items) {
+    constexpr double kChainStep = 4.0e-6, kStreamBw = 5.5e12;
+    struct It { double key; int T; int32_t w, I; };
+    std::vector<It> v;
+    double tb = 0.0;
+    for (int32_t b : p->h_tb) {
+        const double T = (p->h_m[b] + trsv::kT - 1) / trsv::kT;
+        tb += T * (T + 1) / 2 * trsv::kT * trsv::kT * sizeof(double);
+    }
+    const double t_bw = 2.0 * K * tb / kStreamBw;
+    for (int32_t b : p->h_tb) {
+        const int T = (p->h_m[b] + trsv::kT - 1) / trsv::kT;
+        for (int ps = 0; ps < 2 * K; ++ps)
+            for (int pos = 0; pos < T; ++pos) {
+                const double chain = (static_cast<double>(ps) * T + pos) * kChainStep;
+                const double bulk = (ps + static_cast<double>(pos) / T) / (2.0 * K) * t_bw;
+                v.push_back({std::max(chain, bulk), T, b | (ps << 16), (ps & 1) ? T - 1 - pos : pos});
+            }
+    }
+    std::stable_sort(v.begin(), v.end(), [](const It& x, const It& y) {
+        return x.key != y.key ? x.key < y.key : x.T > y.T;
+    });
+    items.clear();
+    items.reserve(2 * v.size());
+    for (const It& x : v) {
+        items.push_back(x.w);
+        items.push_back(x.I);
+    }
+}
+
+// Passes: one launch per forward / backward pass (default), or, with DBSLMM_CHEB_FUSED=1 in the
+// environment (experimental: measured slower at config 4, 15.9 vs 13.9 ms -- every pass there is
+// bound by the largest block's 150-tile chain and by the streaming bandwidth alike, and the fused
+// items' own-input waits and update hand-offs cost more than the launch boundaries they remove),
+// all 2K passes of a group in one dbslmm_trsv_cheb launch over the whole plan (grp = tgroup_all).
 static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup& grp) {
     dbslmm_ctx* ctx = p->ctx;
     hipStream_t st = grp.st;
     if (grp.n_items == 0) return DBSLMM_OK;
+    const char* fenv = getenv("DBSLMM_CHEB_FUSED");
+    const bool fused = fenv && fenv[0] == '1' && grp.item_off == 0 && grp.n_items == p->n_titems;
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
     const int64_t blk = trsv::kMaxR * vs;
     double *Y = p->d_cheb, *Z = Y + blk, *X = Z + blk, *R = X + blk, *D = R + blk, *S = D + blk;
-    const int grid = grp.grid;
     for (size_t g = 0; g < cp.iters.size(); ++g) {
         const size_t g0 = g * trsv::kMaxR;
         const int nr = static_cast<int>(std::min<size_t>(trsv::kMaxR, cp.others.size() - g0));
+        const int K = cp.iters[g];
         int cix[trsv::kMaxR] = {0, 0};
         for (int j = 0; j < nr; ++j) cix[j] = cp.others[g0 + j];
         const double* coef = p->d_coef + cp.coef_off[g];
+        if (fused && p->cheb_items_K != K) {   // the work list of K iterations (cached: K depends on the sigmas)
+            std::lock_guard<std::mutex> lk(g_capture_mu);   // synchronous upload below
+            std::vector<int32_t> items;
+            build_cheb_items(p, K, items);
+            HIP_TRY(ctx, hipStreamSynchronize(st));
+            if (p->d_cheb_items) (void)hipFree(p->d_cheb_items);
+            p->d_cheb_items = nullptr;
+            HIP_TRY(ctx, dev_upload(&p->d_cheb_items, items));
+            p->n_cheb_items = static_cast<int32_t>(items.size() / 2);
+            p->cheb_items_K = K;
+        }
         hipLaunchKernelGGL(dbslmm_cheb_init, dim3(grp.n_tb), dim3(256), 0, st, p->d_tb + grp.tb_off, p->d_row0, p->d_m,
                            p->d_ms, p->d_blk_id, p->d_y + static_cast<int64_t>(cp.base) * p->n_slots, coef,
                            nr, vs, X, R, D, S, p->d_status + cp.base * p->nbk, p->d_status, p->nbk,
@@ -1365,9 +1529,10 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
         a.row0 = p->d_row0;
         a.blk_id = p->d_blk_id;
         a.slot_out = p->d_slot_out;
-        a.n_items = grp.n_items;
+        a.grid = grp.grid;
         a.foff = p->d_foff;
         a.flags = p->d_tflags;
+        a.epi = p->d_tepi;
         a.ctr = grp.ctr;
         a.err = p->d_tflags + p->n_tflags + 1;
         a.vs = vs;
@@ -1375,6 +1540,10 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
         a.R = R;
         a.D = D;
         a.S = S;
+        a.Y = Y;
+        a.Z = Z;
+        a.coef = coef;
+        a.iters = K;
         a.inv_sqrt_n = isn;
         a.beta_s = p->d_beta_s;
         a.beta_l = p->d_beta_l;
@@ -1391,27 +1560,44 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
             a.stamp_b = bmax;
         }
 #endif
-        const int K = cp.iters[g];
-        a.grid = grid;
-        for (int k = 0; k < K; ++k) {
-            for (int pass = 0; pass < 2; ++pass) {
-                const bool fwd = pass == 0;
-                if (++p->trsv_epoch == INT32_MAX) {   // flags restart from a clean slate
-                    HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
-                    p->trsv_epoch = 1;
+        if (!fused) {   // one launch per pass (the launch boundary orders the passes)
+            a.n_items = grp.n_items;
+            for (int k = 0; k < K; ++k)
+                for (int pass = 0; pass < 2; ++pass) {
+                    const bool fwd = pass == 0;
+                    if (++p->trsv_epoch == INT32_MAX) {   // flags restart from a clean slate
+                        HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
+                        p->trsv_epoch = 1;
+                    }
+                    a.epoch = p->trsv_epoch;
+                    a.items = (fwd ? p->d_tri_f : p->d_tri_b) + 2 * grp.item_off;
+                    a.src = fwd ? R : Y;
+                    a.dst = fwd ? Y : Z;
+                    a.coef = coef + static_cast<int64_t>(k) * nr * 3;
+                    a.last = k == K - 1;
+                    if (nr == 1) launch_trsv<1>(fwd, a.grid, st, a);
+                    else launch_trsv<2>(fwd, a.grid, st, a);
+                    HIP_TRY(ctx, hipGetLastError());
+                    p->trsv_pending = true;
                 }
-                a.epoch = p->trsv_epoch;
-                a.items = (fwd ? p->d_tri_f : p->d_tri_b) + 2 * grp.item_off;
-                a.src = fwd ? R : Y;
-                a.dst = fwd ? Y : Z;
-                a.coef = coef + static_cast<int64_t>(k) * nr * 3;
-                a.last = k == K - 1;
-                if (nr == 1) launch_trsv<1>(fwd, grid, st, a);
-                else launch_trsv<2>(fwd, grid, st, a);
-                HIP_TRY(ctx, hipGetLastError());
-                p->trsv_pending = true;
-            }
+            continue;
         }
+        a.fused = 1;
+        a.items = p->d_cheb_items;
+        a.n_items = p->n_cheb_items;
+        a.grid = std::max(1, std::min(ctx->n_cu, p->n_cheb_items));
+        // passes 0 .. 2K-1 run at epochs epoch .. epoch + 2K - 1 (flags and update flags only grow)
+        if (p->trsv_epoch + 2 * K + 2 >= INT32_MAX) {
+            HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
+            HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), st));
+            p->trsv_epoch = 0;
+        }
+        a.epoch = p->trsv_epoch + 1;
+        p->trsv_epoch += 2 * K;
+        if (nr == 1) hipLaunchKernelGGL(dbslmm_trsv_cheb<1>, dim3(a.grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
+        else hipLaunchKernelGGL(dbslmm_trsv_cheb<2>, dim3(a.grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
+        HIP_TRY(ctx, hipGetLastError());
+        p->trsv_pending = true;
     }
     return DBSLMM_OK;
 }
@@ -1579,7 +1765,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             for (size_t g = 0; g < cp.iters.size(); ++g) {
                 const size_t g0 = g * chol::kChebR;
                 const int nr = static_cast<int>(std::min<size_t>(chol::kChebR, cp.others.size() - g0));
-                hipLaunchKernelGGL(dbslmm_chol_cheb, dim3(p->n_large), dim3(chol::kLargeThreads), kCholChebLds, s,
+                hipLaunchKernelGGL(dbslmm_chol_cheb, dim3(p->n_large), dim3(chol::kChebThreads), kCholChebLds, s,
                                    p->d_M + bc * p->M_elems, p->d_order, p->n_large, p->d_row0, p->d_m, p->d_ms,
                                    p->d_ld, p->d_matoff, p->d_blk_id, p->d_slot_out, p->d_y + bc * p->n_slots,
                                    p->d_coef + cp.coef_off[g], nr, cp.iters[g], isn, p->d_beta_s, p->d_beta_l,
@@ -1995,6 +2181,7 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
                         const int32_t* pos, int32_t n_rows, double* out, double* maf) {
     if (!ctx) return DBSLMM_E_ARG;
     ON_FIRST_DEVICE(ctx, dbslmm_read_snp_std(ctx0_, bed, bed_len, n_ref, pos, n_rows, out, maf));
+    if (const int rc = ctx_ready(ctx)) return rc;
     ARG_CHECK(ctx, bed && pos && out && n_ref > 1 && n_rows >= 0, "bad arguments");
     const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
     for (int32_t j = 0; j < n_rows; ++j)
@@ -2052,6 +2239,7 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
                         const double* z1, const double* z2, double* nume, double* deno) {
     if (!ctx) return DBSLMM_E_ARG;
     ON_FIRST_DEVICE(ctx, dbslmm_valid_blocks(ctx0_, bed, bed_len, n_ref, num_block, ptr, pos, z1, z2, nume, deno));
+    if (const int rc = ctx_ready(ctx)) return rc;
     ARG_CHECK(ctx, bed && ptr && nume && deno && n_ref > 1 && num_block >= 0, "bad arguments");
     const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
     const int64_t n_rows = ptr[num_block];

@@ -90,7 +90,26 @@ struct Args {
                                  // system (y = the matrix's z row, x -> X, beta of copy cix[0])
     unsigned long long* stamps;  // diagnostic build (DBSLMM_DIAG, env DBSLMM_TRSV_STAMPS): per tile of block stamp_b,
     int32_t stamp_b;             // 100 MHz times [claim, last hand-off staged, stream done, publish]
+    // all passes of a Chebyshev group in one launch (dbslmm_trsv_cheb): pass p = 2 k (+1 for the
+    // backward substitution) of iteration k runs at epoch + p; the vectors live in Y (forward
+    // result), Z (backward result) and X / R / D / S; `epi` flags a tile's Chebyshev update
+    int32_t fused;               // 1: the item waits for its own inputs (no launch boundary) and
+                                 // reads the per-pass vectors with sc1 loads
+    int32_t iters;               // K
+    int32_t* epi;                // per tile: epoch of the backward pass whose update is stored
+    double* Y;
+    double* Z;
 };
+// the per-pass inputs of an item (the separate forward / backward launches take them from Args)
+struct Pass {
+    int32_t epoch;
+    const double* src;
+    double* dst;
+    const double* coef;
+    int32_t last;
+};
+__device__ __forceinline__ Pass pass_of(const Args& a) { return Pass{a.epoch, a.src, a.dst, a.coef, a.last}; }
+
 __device__ __forceinline__ void stamp(const Args& a, int b, int I, int k) {
 #ifdef DBSLMM_DIAG
     if (a.stamps && b == a.stamp_b) a.stamps[8 * I + k] = __builtin_amdgcn_s_memrealtime();
@@ -110,8 +129,23 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// flags only grow (epochs), and a tile's hand-off data of pass p is overwritten only at pass p + 2,
+// after every consumer of pass p: ">=" serves consumers that run late
 __device__ __forceinline__ bool flag_set(const int32_t* f, int32_t epoch) {
-    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+}
+// the calling wave waits for flag f >= epoch (bounded; every lane polls the same word: one
+// request per poll), then an acquire fence for the wave's later loads
+__device__ __forceinline__ void wave_wait_flag(const Args& a, const int32_t* f, int32_t epoch) {
+    for (long spins = 0; !flag_set(f, epoch); ++spins) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spins > (1L << 25) ||
+            ((spins & 1023) == 1023 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            atomicOr(a.err, 1);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 __device__ __forceinline__ void publish(int32_t* f, int32_t epoch, int tid) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
@@ -132,6 +166,9 @@ __device__ __forceinline__ double red8(double v) {   // sum over an aligned grou
 // every workgroup draws tickets until one is past the list; the last of those resets the counter.
 // Also resets the ring words for the next item.
 __device__ __forceinline__ int take_ticket(const Args& a, Ring* rg, int tid) {
+    // tid made opaque per call: a loop-invariant "tid == 0" at the loop head was jump-threaded
+    // into a lane-divergent inner loop around the barriers below (a deadlock)
+    asm volatile("" : "+v"(tid));
     if (tid == 0) {
         const int t = atomicAdd(a.ctr, 1);
         if (t == a.n_items + a.grid - 1) __hip_atomic_store(a.ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -141,7 +178,10 @@ __device__ __forceinline__ int take_ticket(const Args& a, Ring* rg, int tid) {
         for (int w = 0; w < kSW; ++w) rg->done[w] = 0;
     }
     __syncthreads();
-    const int t = rg->ticket;
+    // uniform by construction; readfirstlane makes it so for the compiler too (scalar loop exit
+    // and item branches -- a "divergent" exit around the barriers of the fused kernel's two item
+    // kinds was structurised into a loop that deadlocked)
+    const int t = __builtin_amdgcn_readfirstlane(rg->ticket);
     __syncthreads();
     return t;
 }
@@ -151,8 +191,8 @@ __device__ __forceinline__ int take_ticket(const Args& a, Ring* rg, int tid) {
 // per lane (= row) and right-hand side per tile, and publishes the new ready count.  A slot is
 // reused only when every streaming wave has consumed the tile that held it.
 template <int NR>
-__device__ __forceinline__ void control(const Args& a, Ring* rg, double* ring, const int32_t* flag, int g0,
-                                        int m, int j0, int dj, int n, int lane) {
+__device__ __forceinline__ void control(const Args& a, int32_t epoch, const double* dst, Ring* rg, double* ring,
+                                        const int32_t* flag, int g0, int m, int j0, int dj, int n, int lane) {
     for (int p = 0; p < n;) {
         for (;;) {   // slot reuse: position p + kGrp - 1 must not overrun the slowest streaming wave
             int mn = n;
@@ -164,11 +204,14 @@ __device__ __forceinline__ void control(const Args& a, Ring* rg, double* ring, c
         int cnt = 0;
         for (long spins = 0;; ++spins) {
             bool ok = false;
-            if (lane < kGrp && p + lane < n) ok = flag_set(flag + j0 + (p + lane) * dj, a.epoch);
+            if (lane < kGrp && p + lane < n) ok = flag_set(flag + j0 + (p + lane) * dj, epoch);
             cnt = __builtin_ctzll(~__ballot(ok));   // length of the done prefix
             if (cnt > 0) break;
             __builtin_amdgcn_s_sleep(1);
-            if (spins > (1L << 25)) {   // bounded (about a second): report and proceed
+            // bounded (about a second): report and proceed; once any wait has given up, every
+            // later wait of the launch gives up at once (the launch ends promptly, results invalid)
+            if (spins > (1L << 25) ||
+                ((spins & 1023) == 1023 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 if (lane == 0) atomicOr(a.err, 1);
                 cnt = 1;
                 break;
@@ -181,7 +224,7 @@ __device__ __forceinline__ void control(const Args& a, Ring* rg, double* ring, c
             if (u < cnt) {
                 const int gr = kT * (j0 + (p + u) * dj) + lane;
 #pragma unroll
-                for (int c = 0; c < NR; ++c) v[u][c] = gr < m ? ld_sc1(a.dst + c * a.vs + g0 + gr) : 0.0;
+                for (int c = 0; c < NR; ++c) v[u][c] = gr < m ? ld_sc1(dst + c * a.vs + g0 + gr) : 0.0;
             }
 #pragma unroll
         for (int u = 0; u < kGrp; ++u)
@@ -200,269 +243,237 @@ __device__ __forceinline__ void wait_ready(Ring* rg, int p) {
 
 }  // namespace trsv
 
-// Forward substitution L y = r (NR right-hand sides), one 64-row tile per work item.  Streaming
-// wave w owns rows 8 w .. 8 w + 7, lane = column of L_IJ (512-B coalesced rows, kPF tiles in
-// flight); y_J comes from the control wave's LDS ring.  Diagonal: y_I = X_I v with X_I^T stored
-// on and above the diagonal tile's diagonal.
+// One 64-row tile of a substitution (NR right-hand sides).  Forward (L y = r): the later rows
+// of tile I against the earlier tiles J < I of L.  Backward (L^T z = y): rows of tile I of L^T,
+// read from the upper triangle (the panel / region kernels store each off-diagonal 64 x 64 tile
+// of L transposed there too), against the later tiles J = T - 1 down to I + 1 -- so both stream
+// rows the same way: wave w owns rows 8 w .. 8 w + 7 of tile I, lane = column of tile J
+// (512-B coalesced rows, kPF tiles in flight), acc += tile_IJ v_J with v_J from the control
+// wave's LDS ring, row sums through a wave-private LDS transpose, then the diagonal: v_I = X_I w
+// (forward; X_I^T stored on and above the diagonal tile's diagonal) or X_I^T w (backward).
+// One body for both directions: the fused Chebyshev kernel runs both kinds of item in one ticket
+// loop, and two inlined bodies there were structurised into a lane-divergent loop around their
+// barriers (deadlock); the direction is a uniform runtime branch here.
+//   wait_f / wait_e: (fused passes) the item's own input is ready when *wait_f >= wait_e
+//   (forward: the previous backward pass's Chebyshev update of r_I, in a.epi; backward: y_I)
+//   epi: (backward) the Chebyshev update of the tile's rows after the hand-off
 template <int NR>
-__global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args a) {
+__device__ __forceinline__ void tile_item(const trsv::Args& a, const trsv::Pass& ps, trsv::Ring* rg, double* lds,
+                                          int b, int I, bool bwd, const int32_t* wait_f, int32_t wait_e, int tid) {
     using namespace trsv;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
     double* ring = lds;                       // [kNS][64][NR]
-    double* vs = ring + kNS * kT * NR;        // [64][NR]: r_I - sum_J L_IJ y_J
-    double* rt = vs + kT * NR;                // [8 waves][8 NR][65]: lane partial sums (transpose)
-    Ring* rg = reinterpret_cast<Ring*>(rt + kSW * 8 * NR * (kT + 1));
-    const int tid = threadIdx.x, row = tid >> 3, part = tid & 7, lane = tid & 63, wave = tid >> 6;
-    constexpr int kV = 8 * NR, kG = kT / kV;  // row sums per wave; lanes per row sum
-    for (;;) {
-        const int it = take_ticket(a, rg, tid);
-        if (it >= a.n_items) break;
-        const int b = a.items[2 * it], I = a.items[2 * it + 1];
-        const int m = a.m[b], ld = a.ld[b], g0 = a.row0[b];
-        const double* A = a.M + a.matoff[b];
-        const int r0 = kT * I, jmax = min(kT, m - r0);
-        const int32_t* flag = a.flags + a.foff[b];
-        double xd[8];
-        if (tid == 0) stamp(a, b, I, 0);
-        if (wave == kSW) {
-            control<NR>(a, rg, ring, flag, g0, m, 0, 1, I, lane);
-            if (lane == 0) stamp(a, b, I, 1);
-        } else {
-            // xd[k] = X[row][8 part + k] = A(r0 + 8 part + k, r0 + row) (8 part + k <= row)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int rr = 8 * part + k;
-                const double x = A[static_cast<int64_t>(r0 + rr) * ld + r0 + row];   // inside ld x ld
-                xd[k] = (rr <= row && row < jmax) ? x : 0.0;
-            }
-            // this lane's share of r_I, read now (off the dependency chain): value v = lane / kG
-            const int vv = lane / kG, vk = vv / NR, vc = vv - vk * NR, vr = 8 * wave + vk;
-            const double rsrc = vr < jmax ? a.src[vc * a.vs + g0 + r0 + vr] : 0.0;
-            const double* Lw = A + static_cast<int64_t>(r0 + 8 * wave) * ld + lane;
-            double acc[8][NR];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int c = 0; c < NR; ++c) acc[k][c] = 0.0;
-            double lr[kPF][8];
-#pragma unroll
-            for (int u = 0; u < kPF; ++u)
-                if (u < I) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) lr[u][k] = Lw[static_cast<int64_t>(k) * ld + kT * u];
-                }
-            for (int J = 0; J < I; J += kPF) {
-#pragma unroll
-                for (int u = 0; u < kPF; ++u) {
-                    const int j = J + u;
-                    if (j < I) {
-                        wait_ready(rg, j);
-                        const double* y = ring + ((j % kNS) * kT + lane) * NR;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-#pragma unroll
-                            for (int c = 0; c < NR; ++c) acc[k][c] += lr[u][k] * y[c];
-                        if (lane == 0) lds_put(&rg->done[wave], j + 1);
-                        if (j + kPF < I) {
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) lr[u][k] = Lw[static_cast<int64_t>(k) * ld + kT * (j + kPF)];
-                        }
-                    }
-                }
-            }
-            if (tid == 0) stamp(a, b, I, 2);
-            // row sums over the 64 lanes: transpose through LDS (wave-private region), then lane
-            // group g of kG lanes sums value v = lane / kG over 64 / kG lanes each
-            double* rw = rt + wave * kV * (kT + 1);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int c = 0; c < NR; ++c) rw[(k * NR + c) * (kT + 1) + lane] = acc[k][c];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            double sum = 0.0;
-            const int q0 = (lane % kG) * (kT / kG);
-#pragma unroll
-            for (int q = 0; q < kT / kG; ++q) sum += rw[vv * (kT + 1) + q0 + q];
-#pragma unroll
-            for (int sft = 1; sft < kG; sft <<= 1) sum += __shfl_xor(sum, sft);
-            if (tid == 0) stamp(a, b, I, 4);
-            if (lane % kG == 0) vs[vr * NR + vc] = vr < jmax ? rsrc - sum : 0.0;
-        }
-        __syncthreads();
-        if (tid == 0) stamp(a, b, I, 5);
-        if (wave < kSW) {
-            double y[NR];
-#pragma unroll
-            for (int c = 0; c < NR; ++c) y[c] = 0.0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int c = 0; c < NR; ++c) y[c] += xd[k] * vs[(8 * part + k) * NR + c];
-#pragma unroll
-            for (int c = 0; c < NR; ++c) y[c] = red8(y[c]);
-            if (part == 0 && row < jmax) {
-#pragma unroll
-                for (int c = 0; c < NR; ++c) st_sc1(a.dst + c * a.vs + g0 + r0 + row, y[c]);
-            }
-        }
-        if (tid == 0) stamp(a, b, I, 6);
-        publish(a.flags + a.foff[b] + I, a.epoch, tid);   // (its barrier also frees vs)
-        if (tid == 0) stamp(a, b, I, 3);
-    }
-}
-
-// Backward substitution L^T z = y, then the Chebyshev update of the tile's rows.  It reads L^T
-// from the upper triangle (the panel / region kernels store each off-diagonal 64 x 64 tile of L
-// transposed there too), so it streams rows exactly like the forward kernel: wave w owns rows
-// 8 w .. 8 w + 7 of tile I, lane = column of the later tile J (J = T - 1 down to I + 1),
-// acc += (L^T)_IJ z_J with z_J from the control wave's LDS ring, then row sums through the
-// wave-private LDS transpose.
-template <int NR>
-__global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args a) {
-    using namespace trsv;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* ring = lds;                       // [kNS][64][NR]
-    double* ws = ring + kNS * kT * NR;        // [64][NR]: y_I - sum_J (L^T)_IJ z_J
-    double* zt = ws + kT * NR;                // [64][NR] this tile's z
+    double* ws = ring + kNS * kT * NR;        // [64][NR]: v_I's source minus sum_J tile_IJ v_J
+    double* zt = ws + kT * NR;                // [64][NR]: this tile's result (backward epilogue)
     double* rt = zt + kT * NR;                // [8 waves][8 NR][65]: lane partial sums (transpose)
-    Ring* rg = reinterpret_cast<Ring*>(rt + kSW * 8 * NR * (kT + 1));
-    const int tid = threadIdx.x, row = tid >> 3, part = tid & 7, wave = tid >> 6, lane = tid & 63;
+    const int row = tid >> 3, part = tid & 7, wave = tid >> 6, lane = tid & 63;
     constexpr int kV = 8 * NR, kG = kT / kV;  // row sums per wave; lanes per row sum
-    for (;;) {
-        const int it = take_ticket(a, rg, tid);
-        if (it >= a.n_items) break;
-        const int b = a.items[2 * it], I = a.items[2 * it + 1];
-        const int m = a.m[b], ld = a.ld[b], g0 = a.row0[b];
-        const int T = (m + kT - 1) / kT;
-        const double* A = a.M + a.matoff[b];
-        const int r0 = kT * I, jmax = min(kT, m - r0);
-        const int32_t* flag = a.flags + a.foff[b];
-        const int cnt = T - 1 - I;                // later tiles, taken from the last one down
-        double xd[8];
-        if (wave == kSW) {
-            control<NR>(a, rg, ring, flag, g0, m, T - 1, -1, cnt, lane);
-        } else {
-            // xd[k] = X^T[row][8 part + k] = A(r0 + row, r0 + 8 part + k), on and above the diagonal
+    const int m = a.m[b], ld = a.ld[b], g0 = a.row0[b];
+    const int T = (m + kT - 1) / kT;
+    const double* A = a.M + a.matoff[b];
+    const int r0 = kT * I, jmax = min(kT, m - r0);
+    const int32_t* flag = a.flags + a.foff[b];
+    const int cnt = bwd ? T - 1 - I : I;      // tiles streamed (backward: from the last one down)
+    if (tid == 0) stamp(a, b, I, 0);
+    double xd[8];
+    if (wave == kSW) {
+        control<NR>(a, ps.epoch, ps.dst, rg, ring, flag, g0, m, bwd ? T - 1 : 0, bwd ? -1 : 1, cnt, lane);
+        if (lane == 0) stamp(a, b, I, 1);
+    } else {
+        // forward: xd[k] = X[row][8 part + k] = A(r0 + 8 part + k, r0 + row) (8 part + k <= row);
+        // backward: xd[k] = X^T[row][8 part + k] = A(r0 + row, r0 + 8 part + k) (on and above)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int q = 8 * part + k;
+            const int64_t o = bwd ? static_cast<int64_t>(r0 + row) * ld + r0 + q
+                                  : static_cast<int64_t>(r0 + q) * ld + r0 + row;   // inside ld x ld
+            const double x = A[o];
+            xd[k] = (bwd ? (q >= row && q < jmax) : (q <= row && row < jmax)) ? x : 0.0;
+        }
+        // this lane's share of the source (value v = lane / kG), read now (off the dependency
+        // chain: the control wave meanwhile polls the hand-offs; fused passes wait for it here)
+        if (wait_e > 0) wave_wait_flag(a, wait_f, wait_e);
+        const int vv = lane / kG, vk = vv / NR, vc = vv - vk * NR, vr = 8 * wave + vk;
+        const double* sp = ps.src + vc * a.vs + g0 + r0 + vr;
+        const double src = vr >= jmax ? 0.0
+                           : (bwd && a.mode) ? A[static_cast<int64_t>(m) * ld + r0 + vr]   // bordered row m: y = L^-1 z
+                                             : a.fused ? ld_sc1(sp) : *sp;
+        const double* Lw = A + static_cast<int64_t>(r0 + 8 * wave) * ld + lane;   // rows of tile I
+        double acc[8][NR];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int c = 0; c < NR; ++c) acc[k][c] = 0.0;
+        double lr[kPF][8];
+        auto issue = [&](int u, int t) {
+            const int cj = kT * (bwd ? T - 1 - t : t);   // columns of tile J: cj + lane < 64 T <= ld
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const int q = 8 * part + k;
-                const double x = A[static_cast<int64_t>(r0 + row) * ld + r0 + q];
-                xd[k] = (q >= row && q < jmax) ? x : 0.0;
+                const double x = Lw[static_cast<int64_t>(k) * ld + cj];
+                lr[u][k] = cj + lane < m ? x : 0.0;      // past m: bordered row / padding
             }
-            // this lane's share of y_I (value v = lane / kG), read now (off the dependency chain)
-            const int vv = lane / kG, vk = vv / NR, vc = vv - vk * NR, vr = 8 * wave + vk;
-            const double ysrc = vr >= jmax ? 0.0
-                                : a.mode ? A[static_cast<int64_t>(m) * ld + r0 + vr]   // bordered row m: y = L^-1 z
-                                         : a.src[vc * a.vs + g0 + r0 + vr];
-            const double* Uw = A + static_cast<int64_t>(r0 + 8 * wave) * ld + lane;   // rows of tile I
-            double acc[8][NR];
+        };
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
+        for (int u = 0; u < kPF; ++u)
+            if (u < cnt) issue(u, u);
+        for (int t0 = 0; t0 < cnt; t0 += kPF) {
 #pragma unroll
-                for (int c = 0; c < NR; ++c) acc[k][c] = 0.0;
-            double lr[kPF][8];
-            auto issue = [&](int u, int t) {
-                const int cj = kT * (T - 1 - t);          // columns of tile J: cj + lane < 64 T <= ld
+            for (int u = 0; u < kPF; ++u) {
+                const int t = t0 + u;
+                if (t < cnt) {
+                    wait_ready(rg, t);
+                    const double* v = ring + ((t % kNS) * kT + lane) * NR;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const double x = Uw[static_cast<int64_t>(k) * ld + cj];
-                    lr[u][k] = cj + lane < m ? x : 0.0;   // past m: bordered row / padding
-                }
-            };
+                    for (int k = 0; k < 8; ++k)
 #pragma unroll
-            for (int u = 0; u < kPF; ++u)
-                if (u < cnt) issue(u, u);
-            for (int t0 = 0; t0 < cnt; t0 += kPF) {
-#pragma unroll
-                for (int u = 0; u < kPF; ++u) {
-                    const int t = t0 + u;
-                    if (t < cnt) {
-                        wait_ready(rg, t);
-                        const double* z = ring + ((t % kNS) * kT + lane) * NR;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-#pragma unroll
-                            for (int c = 0; c < NR; ++c) acc[k][c] += lr[u][k] * z[c];
-                        if (lane == 0) lds_put(&rg->done[wave], t + 1);
-                        if (t + kPF < cnt) issue(u, t + kPF);
-                    }
-                }
-            }
-            double* rw = rt + wave * kV * (kT + 1);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int c = 0; c < NR; ++c) rw[(k * NR + c) * (kT + 1) + lane] = acc[k][c];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            double sum = 0.0;
-            const int q0 = (lane % kG) * (kT / kG);
-#pragma unroll
-            for (int q = 0; q < kT / kG; ++q) sum += rw[vv * (kT + 1) + q0 + q];
-#pragma unroll
-            for (int sft = 1; sft < kG; sft <<= 1) sum += __shfl_xor(sum, sft);
-            if (lane % kG == 0) ws[vr * NR + vc] = vr < jmax ? ysrc - sum : 0.0;
-        }
-        __syncthreads();
-        if (wave < kSW) {
-            double z[NR];
-#pragma unroll
-            for (int c = 0; c < NR; ++c) z[c] = 0.0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int c = 0; c < NR; ++c) z[c] += xd[k] * ws[(8 * part + k) * NR + c];
-#pragma unroll
-            for (int c = 0; c < NR; ++c) z[c] = red8(z[c]);
-            if (part == 0 && row < jmax) {
-#pragma unroll
-                for (int c = 0; c < NR; ++c) {
-                    st_sc1(a.dst + c * a.vs + g0 + r0 + row, z[c]);
-                    zt[row * NR + c] = z[c];
+                        for (int c = 0; c < NR; ++c) acc[k][c] += lr[u][k] * v[c];
+                    if (lane == 0) lds_put(&rg->done[wave], t + 1);
+                    if (t + kPF < cnt) issue(u, t + kPF);
                 }
             }
         }
-        publish(a.flags + a.foff[b] + I, a.epoch, tid);
-        // Chebyshev epilogue: d = alpha d + beta z; s = alpha s + beta r; x += d;
-        // r -= s + delta P_s d  (this tile's rows; read and written only here in this launch)
-        if (tid < kT * NR) {
-            const int rr = tid / NR, c = tid - rr * NR;
-            if (rr < jmax) {
-                const int i = r0 + rr;
-                const int64_t gi = g0 + i;
-                const bool small = i < a.ms[b];
-                const bool fail = a.status[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
-                if (a.mode) {   // plain solve: x and beta (NR = 1)
-                    const double x = zt[tid];
-                    a.X[gi] = x;
-                    const double v = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
-                    const int so = a.slot_out[gi];
-                    if (so >= 0) a.beta_s[a.cix[0] * a.ns_stride + so] = v;
-                    else a.beta_l[a.cix[0] * a.nl_stride - 1 - so] = v;
-                    continue;
-                }
-                const double al = a.coef[3 * c], be = a.coef[3 * c + 1], de = a.coef[3 * c + 2];
+        if (tid == 0) stamp(a, b, I, 2);
+        // row sums over the 64 lanes: transpose through LDS (wave-private region), then lane
+        // group g of kG lanes sums value v = lane / kG over 64 / kG lanes each
+        double* rw = rt + wave * kV * (kT + 1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int c = 0; c < NR; ++c) rw[(k * NR + c) * (kT + 1) + lane] = acc[k][c];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double sum = 0.0;
+        const int q0 = (lane % kG) * (kT / kG);
+#pragma unroll
+        for (int q = 0; q < kT / kG; ++q) sum += rw[vv * (kT + 1) + q0 + q];
+#pragma unroll
+        for (int sft = 1; sft < kG; sft <<= 1) sum += __shfl_xor(sum, sft);
+        if (tid == 0) stamp(a, b, I, 4);
+        if (lane % kG == 0) ws[vr * NR + vc] = vr < jmax ? src - sum : 0.0;
+    }
+    __syncthreads();
+    if (tid == 0) stamp(a, b, I, 5);
+    if (wave < kSW) {
+        double v[NR];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) v[c] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int c = 0; c < NR; ++c) v[c] += xd[k] * ws[(8 * part + k) * NR + c];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) v[c] = red8(v[c]);
+        if (part == 0 && row < jmax) {
+#pragma unroll
+            for (int c = 0; c < NR; ++c) {
+                st_sc1(ps.dst + c * a.vs + g0 + r0 + row, v[c]);
+                zt[row * NR + c] = v[c];
+            }
+        }
+    }
+    if (tid == 0) stamp(a, b, I, 6);
+    publish(a.flags + a.foff[b] + I, ps.epoch, tid);   // (its barrier also frees ws and orders zt)
+    if (tid == 0) stamp(a, b, I, 3);
+    if (!bwd) return;
+    // Chebyshev epilogue: d = alpha d + beta z; s = alpha s + beta r; x += d;
+    // r -= s + delta P_s d  (this tile's rows; read and written only here in this pass)
+    if (tid < kT * NR) {
+        const int rr = tid / NR, c = tid - rr * NR;
+        if (rr < jmax) {
+            const int i = r0 + rr;
+            const int64_t gi = g0 + i;
+            const bool small = i < a.ms[b];
+            const bool fail = a.status[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
+            if (a.mode) {   // plain solve: x and beta (NR = 1)
+                const double x = zt[tid];
+                a.X[gi] = x;
+                const double v = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
+                const int so = a.slot_out[gi];
+                if (so >= 0) a.beta_s[a.cix[0] * a.ns_stride + so] = v;
+                else a.beta_l[a.cix[0] * a.nl_stride - 1 - so] = v;
+            } else {
+                const double al = ps.coef[3 * c], be = ps.coef[3 * c + 1], de = ps.coef[3 * c + 2];
                 const int64_t o = c * a.vs + gi;
-                const double d = al * a.D[o] + be * zt[tid];
-                const double x = a.X[o] + d;
-                if (a.last) {
+                // fused passes: the state of this tile was written by another workgroup's update
+                // in the previous pass (sc1 both ways); separate launches: plain accesses
+                auto ld_v = [&](const double* q) { return a.fused ? ld_sc1(q) : *q; };
+                auto st_v = [&](double* q, double v) { if (a.fused) st_sc1(q, v); else *q = v; };
+                const double d = al * ld_v(a.D + o) + be * zt[tid];
+                const double x = ld_v(a.X + o) + d;
+                if (ps.last) {
                     const double v = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
                     const int so = a.slot_out[gi];
                     if (so >= 0) a.beta_s[a.cix[c] * a.ns_stride + so] = v;
                     else a.beta_l[a.cix[c] * a.nl_stride - 1 - so] = v;
                 } else {
-                    const double r = a.R[o];
-                    const double s2 = al * a.S[o] + be * r;
-                    a.D[o] = d;
-                    a.S[o] = s2;
-                    a.X[o] = x;
-                    a.R[o] = r - s2 - (small ? de * d : 0.0);
+                    const double r = ld_v(a.R + o);
+                    const double s2 = al * ld_v(a.S + o) + be * r;
+                    st_v(a.D + o, d);
+                    st_v(a.S + o, s2);
+                    st_v(a.X + o, x);
+                    st_v(a.R + o, r - s2 - (small ? de * d : 0.0));
                 }
             }
         }
+    }
+    if (a.fused && !ps.last) publish(a.epi + a.foff[b] + I, ps.epoch, tid);   // the update is stored
+}
+
+template <int NR>
+__global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args a) {
+    using namespace trsv;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Ring* rg = reinterpret_cast<Ring*>(lds + kNS * kT * NR + 2 * kT * NR + kSW * 8 * NR * (kT + 1));
+    const int tid = threadIdx.x;
+    for (;;) {
+        const int it = take_ticket(a, rg, tid);
+        if (it >= a.n_items) break;
+        const int b = __builtin_amdgcn_readfirstlane(a.items[2 * it]);
+        const int I = __builtin_amdgcn_readfirstlane(a.items[2 * it + 1]);
+        tile_item<NR>(a, pass_of(a), rg, lds, b, I, false, nullptr, 0, tid);
+    }
+}
+
+template <int NR>
+__global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args a) {
+    using namespace trsv;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Ring* rg = reinterpret_cast<Ring*>(lds + kNS * kT * NR + 2 * kT * NR + kSW * 8 * NR * (kT + 1));
+    const int tid = threadIdx.x;
+    for (;;) {
+        const int it = take_ticket(a, rg, tid);
+        if (it >= a.n_items) break;
+        const int b = __builtin_amdgcn_readfirstlane(a.items[2 * it]);
+        const int I = __builtin_amdgcn_readfirstlane(a.items[2 * it + 1]);
+        tile_item<NR>(a, pass_of(a), rg, lds, b, I, true, nullptr, 0, tid);
+    }
+}
+
+// Every pass of a Chebyshev group in one persistent launch: items (block | pass << 16, tile) in
+// an order where each block's items follow its own dependency order (passes in sequence, tiles
+// in their substitution order) -- so every wait is on a smaller ticket (deadlock-free) -- while
+// the blocks are interleaved by a timing model: the small blocks' many iterations stream at the
+// memory bandwidth while the largest blocks' long chains advance beside them, instead of every
+// block waiting for the largest one at the end of each pass (plan.hip, build_cheb_items).
+template <int NR>
+__global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_cheb(trsv::Args a) {
+    using namespace trsv;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    Ring* rg = reinterpret_cast<Ring*>(lds + kNS * kT * NR + 2 * kT * NR + kSW * 8 * NR * (kT + 1));
+    const int tid = threadIdx.x;
+    for (;;) {
+        const int it = take_ticket(a, rg, tid);
+        if (it >= a.n_items) break;
+        const int32_t w = __builtin_amdgcn_readfirstlane(a.items[2 * it]);
+        const int32_t I = __builtin_amdgcn_readfirstlane(a.items[2 * it + 1]);
+        const int b = w & 0xFFFF, p = w >> 16, k = p >> 1;
+        const bool bwd = p & 1;
+        // backward: y_I of this iteration's forward pass; forward k > 0: the previous backward
+        // pass's update of r_I
+        const Pass ps{a.epoch + p, bwd ? a.Y : a.R, bwd ? a.Z : a.Y,
+                      a.coef + static_cast<int64_t>(k) * NR * 3, bwd && k == a.iters - 1};
+        const int32_t* wf = (bwd ? a.flags : a.epi) + a.foff[b] + I;
+        tile_item<NR>(a, ps, rg, lds, b, I, bwd, wf, (bwd || k > 0) ? a.epoch + p - 1 : 0, tid);
     }
 }
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 7
+#define DBSLMM_ABI_VERSION 8
 
 enum {
     DBSLMM_OK = 0,
@@ -166,6 +166,13 @@ const char* dbslmm_last_error(const dbslmm_ctx* ctx);
  * if the context releases or replaces it.  bed == NULL releases the context's reference.  A
  * multi-device context ignores the call (each device holds only its shard's rows). */
 int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len);
+/* dbslmm_ctx_cache_bed with the image read from an open file descriptor (pread straight into the
+ * pinned staging buffers: the caller's pages of the file are never touched, so a caller that maps
+ * the file pays no page faults and no page-table teardown for it).  `key` -- typically the
+ * caller's mmap of the same file, never dereferenced here -- identifies the image: dbslmm_bed_maf
+ * and dbslmm_plan_create calls that pass (key, bed_len) as their .bed read the cached copy.  The
+ * file must not change while cached.  (ABI 8; the dbslmm CLI uses it.) */
+int dbslmm_ctx_cache_bed_fd(dbslmm_ctx* ctx, int fd, int64_t bed_len, const uint8_t* key);
 
 /* DBSLMMFIT::est replacement: upload, solve, download, free.  beta_s has s_ptr[num_block]
  * entries, beta_l l_ptr[num_block] (ignored when l_ptr == NULL); block_status (optional) has

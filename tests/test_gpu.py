@@ -251,3 +251,47 @@ def test_cached_and_staged_bed_upload_identical(fit):
     b = fit.est(prob)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+
+
+def test_cache_bed_from_file_descriptor(fit, tmp_path):
+    """dbslmm_ctx_cache_bed_fd (ABI 8, the CLI's path): the image read with pread from the file
+    into the staged upload, keyed by a pointer that is never dereferenced; bed_maf and a plan
+    created with that key equal the uncached path bit for bit.  Also: a plan created from the
+    cached image keeps it alive after the context releases it (read in place)."""
+    import ctypes as C
+    from dbslmm_amd import BlockProblem, Context, Plan, bed_maf
+    rng = np.random.default_rng(5)
+    n_ref, n_snp = 1001, 300_001
+    bps = (n_ref + 3) // 4
+    bed = rng.integers(0, 256, size=3 + n_snp * bps, dtype=np.uint8)
+    bed[:3] = (0x6C, 0x1B, 0x01)
+    path = str(tmp_path / "x.bed")
+    bed.tofile(path)
+    plain = bed_maf(fit.ctx, bed, n_ref, n_snp)
+    ctx = Context(0)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        ctx.check(ctx.lib.dbslmm_ctx_cache_bed_fd(ctx.h, fd, bed.size, bed.ctypes.data_as(C.c_void_p)),
+                  "ctx_cache_bed_fd")
+    finally:
+        os.close(fd)
+    np.testing.assert_array_equal(bed_maf(ctx, bed, n_ref, n_snp), plain)
+    d = td_problem(nsnp=996, tau=0.8)
+    path2 = str(tmp_path / "td.bed")
+    d["bed"].tofile(path2)
+    fd = os.open(path2, os.O_RDONLY)
+    try:
+        ctx.check(ctx.lib.dbslmm_ctx_cache_bed_fd(ctx.h, fd, d["bed"].size,
+                                                  d["bed"].ctypes.data_as(C.c_void_p)), "ctx_cache_bed_fd")
+    finally:
+        os.close(fd)
+    prob = BlockProblem(bed=d["bed"], n_ref=d["n_ref"], n_obs=d["n_obs"], sigma_s=d["sigma_s"],
+                        s_ptr=d["s_ptr"], s_pos=d["s_pos"], z_s=d["z_s"], l_ptr=d["l_ptr"],
+                        l_pos=d["l_pos"], z_l=d["z_l"], tau=0.8)
+    plan = Plan(ctx, prob)
+    ctx.cache_bed(None)                  # the plan holds its own reference to the cached image
+    plan.run()
+    a = plan.download()
+    b = fit.est(prob)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)

@@ -131,3 +131,22 @@ def test_cheb_error_within_target(cheb_tol):
         p2 = Plan(Context(0), prob)
         p2.run_multi(sig)
         assert p2.workload()["cheb_iters"] < iters
+
+
+@pytest.mark.parametrize("factors", [(0.8, 1.0, 1.2), (0.5, 0.7, 1.0, 1.3, 1.6, 2.0)])
+def test_fused_cheb_launch_bit_identical(monkeypatch, factors):
+    """DBSLMM_CHEB_FUSED=1 runs all 2K passes of a copy group in one dbslmm_trsv_cheb launch
+    (items of every pass interleaved across blocks, own-input waits on flags); the arithmetic is
+    the per-pass kernels' own, so the betas are bit-identical (groups of 2 and of 1 copy)."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=5, mono_block=3)
+    prob.opts["tiled_min"] = 64
+    sig = [prob.sigma_s * f for f in factors]
+    ref = Plan(Context(0), prob).run_multi(sig)
+    monkeypatch.setenv("DBSLMM_CHEB_FUSED", "1")
+    plan = Plan(Context(0), prob)
+    for _ in range(2):   # the cached work list is reused
+        got = plan.run_multi(sig)
+        for x, y in zip(got, ref):
+            np.testing.assert_array_equal(_cat(x), _cat(y))
+            np.testing.assert_array_equal(x[2], y[2])
