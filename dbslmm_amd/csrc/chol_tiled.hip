@@ -600,7 +600,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tcho
 namespace chol {
 constexpr int kT2 = 128;                 // tile edge
 constexpr int kK2 = 32;                  // K per stage
-constexpr int kRun2 = 2;                 // tiles per run (when a step has plenty of tiles)
+constexpr int kRun2 = 1;                 // tiles per run (2 measured slower with two workgroups per CU:
+                                         // trail_bench m 9596 K 512, 63.5 vs 73.5 % of the f64 peak)
 }  // namespace chol
 
 // The same update fed by LDS-DMA (global_load_lds_dwordx4): no staging registers, no LDS store
@@ -614,63 +615,86 @@ constexpr int kRun2 = 2;                 // tiles per run (when a step has plent
 #define DBSLMM_T3_DIAG 0
 #endif
 namespace chol {
-constexpr int kOp3 = kT2 * kK2;                // one operand stage, unpadded (32 KiB)
-constexpr int kTrail3Doubles = 4 * kOp3;       // A, B x 2 slots (128 KiB)
+// KS = K per stage: 32 (two 64 KiB slots, one workgroup per CU) or 16 (two 32 KiB slots, two
+// workgroups per CU, so one's barrier / DMA wait hides under the other's MFMAs)
+template <int KS> struct T3 {
+    static constexpr int kOp = kT2 * KS;              // one operand stage, unpadded
+    static constexpr int kDoubles = 4 * kOp;          // A, B x 2 slots
+    static constexpr int kChunks = KS / 2;            // 16-B chunks per operand row
+    static constexpr int kRowsPerInst = 64 / kChunks; // rows one DMA instruction covers
+    // LDS position of K chunk c in row r: conflict-free ds_read_b128 for 16 consecutive rows
+    __device__ static __forceinline__ int swz(int c, int r) { return KS == 32 ? c ^ (r & 15) : c ^ ((r >> 1) & 7); }
+};
+constexpr int kOp3 = T3<kK2>::kOp;                   // (K = 32: 32 KiB per operand stage)
+constexpr int kTrail3Doubles = T3<kK2>::kDoubles;    // 128 KiB
+constexpr int kTrail3k16Doubles = T3<16>::kDoubles;  // 64 KiB
 typedef __attribute__((address_space(1))) const void* gptr_f;
 typedef __attribute__((address_space(3))) void* lptr_f;
 
+// (32-bit element offsets from the block's base -- tiled blocks have m < 32640, so ld <= 32768 and
+// ld * ld <= 2^30 (plan_create) --
+// so the loads take a scalar base + one VGPR offset each instead of 64-bit addresses)
 __device__ __forceinline__ void t3_load_c(v4d (&c)[4][2], const double* A, int ld, int r0, int c0, int lane) {
+    const int o = (r0 + (lane >> 4)) * ld + c0 + (lane & 15);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                c[i][j][q] = -A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)];
+            for (int q = 0; q < 4; ++q) c[i][j][q] = -A[o + (16 * i + 4 * q) * ld + 16 * j];
 }
 __device__ __forceinline__ void t3_store_c(const v4d (&c)[4][2], double* A, int ld, int r0, int c0, int lane) {
+    const int o = (r0 + (lane >> 4)) * ld + c0 + (lane & 15);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                A[static_cast<int64_t>(r0 + 16 * i + (lane >> 4) + 4 * q) * ld + c0 + 16 * j + (lane & 15)] = -c[i][j][q];
+            for (int q = 0; q < 4; ++q) A[o + (16 * i + 4 * q) * ld + 16 * j] = -c[i][j][q];
 }
-// DMA of one stage (rows 16 w .. 16 w + 15 of each operand; 4 rows per instruction)
+// DMA of one stage (rows 16 w .. 16 w + 15 of each operand)
+template <int KS>
 __device__ __forceinline__ void t3_issue(double* slot, const double* A, int ld, int I, int J, int col,
                                          bool diag, int wave, int lane) {
-    const int rr = lane >> 4, p = lane & 15;
+    using P = T3<KS>;
+    const int rr = lane / P::kChunks, p = lane % P::kChunks;
 #pragma unroll
     for (int op = 0; op < 2; ++op) {
         if (op == 1 && diag) break;
         const int rb = kT2 * (op ? J : I);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = 16 * wave + 4 * q + rr;
-            const int c = p ^ (r & 15);
-            __builtin_amdgcn_global_load_lds((gptr_f)(A + static_cast<int64_t>(rb + r) * ld + col + 2 * c),
-                                             (lptr_f)(slot + op * kOp3 + (16 * wave + 4 * q) * kK2), 16, 0, 0);
+        for (int q = 0; q < 16 / P::kRowsPerInst; ++q) {
+            const int r = 16 * wave + P::kRowsPerInst * q + rr;
+            const int c = P::swz(p, r);   // (the swizzle is an involution: position p holds chunk c)
+            __builtin_amdgcn_global_load_lds((gptr_f)(A + ((rb + r) * ld + col + 2 * c)),
+                                             (lptr_f)(slot + op * P::kOp + (16 * wave + P::kRowsPerInst * q) * KS), 16, 0, 0);
         }
     }
 }
+template <int KS>
 __device__ __forceinline__ void t3_mfma_stage(v4d (&acc)[4][2], const double* SA, const double* SB,
                                               int wr, int wc, int lane) {
+    using P = T3<KS>;
     const int ri = lane & 15, kq = lane >> 4;
     // operand reads one 8-deep group ahead of the MFMAs that consume them
     v2d a[2][4], b[2][2];
     auto load = [&](int j8, int u) {
-        const int pc = 2 * ((4 * j8 + kq) ^ ri);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[u][i] = *reinterpret_cast<const v2d*>(SA + (64 * wr + 16 * i + ri) * kK2 + pc);
+        for (int i = 0; i < 4; ++i) {
+            const int r = 64 * wr + 16 * i + ri;
+            a[u][i] = *reinterpret_cast<const v2d*>(SA + r * KS + 2 * P::swz(4 * j8 + kq, r));
+        }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[u][j] = *reinterpret_cast<const v2d*>(SB + (32 * wc + 16 * j + ri) * kK2 + pc);
+        for (int j = 0; j < 2; ++j) {
+            const int r = 32 * wc + 16 * j + ri;
+            b[u][j] = *reinterpret_cast<const v2d*>(SB + r * KS + 2 * P::swz(4 * j8 + kq, r));
+        }
     };
     load(0, 0);
 #pragma unroll
-    for (int j8 = 0; j8 < kK2 / 8; ++j8) {
+    for (int j8 = 0; j8 < KS / 8; ++j8) {
         const int u = j8 & 1;
-        if (j8 + 1 < kK2 / 8) load(j8 + 1, u ^ 1);
+        if (j8 + 1 < KS / 8) load(j8 + 1, u ^ 1);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -680,12 +704,15 @@ __device__ __forceinline__ void t3_mfma_stage(v4d (&acc)[4][2], const double* SA
                     acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][i][h], b[u][j][h], acc[i][j], 0, 0, 0);
     }
 }
-}  // namespace chol
 
-extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
-    chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
-    using namespace chol;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
+template <int KS>
+__device__ __forceinline__ void trailing3_body(const TiledArgs& a0, int32_t run, const int32_t* __restrict__ items,
+                                               int32_t n_items, double* lds) {
+    using P = T3<KS>;
+    // K = 32: the next tile's C is prefetched during the current tile's last stage; K = 16 (two
+    // workgroups per CU, 128 VGPRs) loads it at the tile's first stage -- the other workgroup's
+    // MFMAs cover that wait
+    constexpr bool kPrefetchC = KS == 32;
     if (static_cast<int>(blockIdx.x) >= n_items) return;
     const int32_t it = items[2 * blockIdx.x];
     if (it < 0) return;
@@ -700,37 +727,41 @@ extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
     double* A = a.M + a.blk_matoff[b];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
     const int c0 = 2 * kBT * s;
-    const int nst = 4 * nk;
+    const int nst = (kT2 / KS) * nk;
     const int total = nst * (J1 - J0 + 1);
     v4d acc[4][2], nxt[4][2];
-    t3_issue(lds, A, ld, I, J0, c0, I == J0, wave, lane);
+    t3_issue<KS>(lds, A, ld, I, J0, c0, I == J0, wave, lane);
     t3_load_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J0 + 32 * wc, lane);
     // tile j's C store is issued at the start of tile j+1's first stage (after that stage's DMA),
     // so it drains under that stage's MFMAs instead of in front of the next vmcnt wait
     for (int g = 0; g < total; ++g) {
         const int J = J0 + g / nst, t = g % nst;
         const bool diag = I == J;
-        double* S = lds + (g & 1) * 2 * kOp3;
+        double* S = lds + (g & 1) * 2 * P::kOp;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA (and C traffic)
         __builtin_amdgcn_s_barrier();                        // stage g is in LDS; slot g+1 free
         if (g + 1 < total) {
             const int Jn = J0 + (g + 1) / nst, tn = (g + 1) % nst;
 #if DBSLMM_T3_DIAG != 2
-            t3_issue(lds + ((g + 1) & 1) * 2 * kOp3, A, ld, I, Jn, c0 + kK2 * tn, I == Jn, wave, lane);
+            t3_issue<KS>(lds + ((g + 1) & 1) * 2 * P::kOp, A, ld, I, Jn, c0 + KS * tn, I == Jn, wave, lane);
 #endif
-            if (tn == 0) t3_load_c(nxt, A, ld, kT2 * I + 64 * wr, kT2 * Jn + 32 * wc, lane);
+            if (kPrefetchC && tn == 0) t3_load_c(nxt, A, ld, kT2 * I + 64 * wr, kT2 * Jn + 32 * wc, lane);
         }
         if (t == 0 && g > 0) {
             const int Jp = J - 1;
             if (!(Jp == I && 32 * wc > 64 * wr + 63)) t3_store_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * Jp + 32 * wc, lane);
+            if (kPrefetchC) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = nxt[i][j];
+                    for (int j = 0; j < 2; ++j) acc[i][j] = nxt[i][j];
+            } else {
+                t3_load_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J + 32 * wc, lane);
+            }
         }
         const bool skip = diag && 32 * wc > 64 * wr + 63;
 #if DBSLMM_T3_DIAG != 1   // diagnostic builds only (1: no MFMAs, 2: no operand DMA)
-        if (!skip) t3_mfma_stage(acc, S, diag ? S : S + kOp3, wr, wc, lane);
+        if (!skip) t3_mfma_stage<KS>(acc, S, diag ? S : S + P::kOp, wr, wc, lane);
 #endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -738,5 +769,17 @@ extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
         const int J = J1;
         if (!(J == I && 32 * wc > 64 * wr + 63)) t3_store_c(acc, A, ld, kT2 * I + 64 * wr, kT2 * J + 32 * wc, lane);
     }
+}
+}  // namespace chol
+
+extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
+    chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    chol::trailing3_body<chol::kK2>(a0, run, items, n_items, lds);
+}
+extern "C" __global__ __launch_bounds__(512, 4) void dbslmm_tchol_trailing3k16(   // 4 waves per SIMD: two workgroups per CU
+    chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    chol::trailing3_body<16>(a0, run, items, n_items, lds);
 }
 

@@ -46,7 +46,7 @@ constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kCholChebLds = sizeof(double) * chol::kChebLdsDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
-constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3Doubles;
+constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3k16Doubles;   // the K = 16 variant (2 per CU)
 constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
 constexpr int kTiledMinSmall = 256;     // the same when no block reaches kTiledMinDefault
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
@@ -628,7 +628,7 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
             hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_panel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 static_cast<int>(kTiledLds)) == hipSuccess &&
-            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3k16),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 static_cast<int>(kTrail3Lds)) == hipSuccess &&
             set_trsv_lds<1>() == hipSuccess && set_trsv_lds<2>() == hipSuccess;
@@ -1191,7 +1191,7 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
         switch (L.kind) {
         case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, act, L.items); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, act, L.items); break;
-        default: hipLaunchKernelGGL(dbslmm_tchol_trailing3, g, dim3(512), kTrail3Lds, st, ta, L.n, act, L.items); break;
+        default: hipLaunchKernelGGL(dbslmm_tchol_trailing3k16, g, dim3(512), kTrail3Lds, st, ta, L.n, act, L.items); break;
         }
     }
     HIP_TRY(ctx, hipGetLastError());
@@ -1252,7 +1252,6 @@ static TGroup tgroup_all(const dbslmm_plan* p) {
     return TGroup{0, p->n_titems, 0, p->n_tiled, p->ctx->stream2, p->d_tflags + p->n_tflags,
                   std::max(1, std::min(p->ctx->n_cu, p->n_titems))};
 }
-
 static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     dbslmm_ctx* ctx = p->ctx;
     hipStream_t st = grp.st;
@@ -1335,12 +1334,7 @@ static int run_tiled_copy(dbslmm_plan* p, double isn, int copy) {
 }
 static int run_rest_copy(dbslmm_plan* p, double isn, int copy) {
     if (static_cast<int>(p->graph_rest.size()) <= copy) p->graph_rest.resize(copy + 1, nullptr);
-    dbslmm_ctx* ctx = p->ctx;
-    const int rc = launch_graph(p, isn, p->tl_rest, p->d_tlist, copy, p->graph_rest[copy], seq_rest(p));
-    if (rc != DBSLMM_OK) return rc;
-    HIP_TRY(ctx, hipEventRecord(ctx->join4, ctx->stream4));
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->join4, 0));
-    return DBSLMM_OK;
+    return launch_graph(p, isn, p->tl_rest, p->d_tlist, copy, p->graph_rest[copy], seq_rest(p));
 }
 
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
@@ -1631,7 +1625,9 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     const int32_t tcopy = cheb ? cp.base : -1;   // Gram epilogues: iterated blocks write this copy only
     // ... the blocks with m >= tmin_copy: the tiled ones and the single-workgroup ones (ld > 64),
     // whose other h2f copies iterate on the base factor too (dbslmm_chol_cheb)
-    const int32_t tmin_copy = chol::kSmallLd;
+    const char* lenv = getenv("DBSLMM_LARGE_CHEB");   // A/B switch: 0 = factor every copy
+    const bool large_cheb = cheb && !(lenv && lenv[0] == '0');
+    const int32_t tmin_copy = large_cheb ? chol::kSmallLd : p->tiled_min;
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
     if (p->timing) {
@@ -1744,7 +1740,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             HIP_TRY(ctx, hipEventRecord(ctx->fork2, s));
             HIP_TRY(ctx, hipStreamWaitEvent(lead ? ctx->stream4 : ctx->stream2, ctx->fork2, 0));
         }
-        if (p->n_large > 0 && !cheb) {   // every copy in one launch
+        if (p->n_large > 0 && !large_cheb) {   // every copy in one launch
             hipLaunchKernelGGL(dbslmm_chol_large, dim3(p->n_large * n), dim3(chol::kLargeThreads),
                                kCholLargeLds, s, p->d_M, p->d_order, p->n_large,
                                p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_blk_id, p->d_z,
@@ -1805,6 +1801,12 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             if (n == 1 || cheb) {
                 // h2f: factor only the base copy, iterate the others on its factor
                 int rc = lead ? DBSLMM_OK : run_tiled_copy(p, isn, fcopy);
+                if (lead) {   // the rest sequence is done before the substitutions (one launch
+                              // sequence over all tiled blocks: per-group substitutions measured
+                              // slower)
+                    HIP_TRY(ctx, hipEventRecord(ctx->join4, ctx->stream4));
+                    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->join4, 0));
+                }
                 if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, tgroup_all(p));
                 if (rc != DBSLMM_OK) return rc;
                 if (cheb) {

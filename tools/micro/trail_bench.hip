@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <cmath>
+#include <algorithm>
 #include "../../include/dbslmm_hip.h"
 #include "../../dbslmm_amd/csrc/chol.hip"
 #include "../../dbslmm_amd/csrc/chol_tiled.hip"
@@ -48,23 +50,44 @@ int main(int argc, char** argv) {
                        d_dbl, d_dbl, 1.0, d_dbl, d_dbl, d_dbl, d_i32 + 5, 1, 0, 0, 0, 0, 0};
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3),
                            hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(double) * chol::kTrail3Doubles));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_trailing3k16),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(double) * chol::kTrail3k16Doubles));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int k = 1; k < 2; ++k) {   // (k = 0 held a measured-and-dropped variant)
-        for (int w = 0; w < 2; ++w)
-            if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, (int)items.size() / 2);
+    const int n_it = static_cast<int>(items.size() / 2);
+    for (int k = 0; k < 2; ++k) {   // 0: K = 32 per stage, one workgroup per CU; 1: K = 16, two
+        auto launch = [&] {
+            if (k == 0) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(n_it), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, n_it);
+            else hipLaunchKernelGGL(dbslmm_tchol_trailing3k16, dim3(n_it), dim3(512), sizeof(double) * chol::kTrail3k16Doubles, 0, ta, run, d_items, n_it);
+        };
+        for (int w = 0; w < 2; ++w) launch();
+        CK(hipGetLastError());
         CK(hipEventRecord(e0));
         const int reps = 5;
-        for (int r = 0; r < reps; ++r)
-            if (k) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(items.size() / 2), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, (int)items.size() / 2);
+        for (int r = 0; r < reps; ++r) launch();
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
-        printf("%s m=%d nk=%d run=%d items=%zu  %.3f ms  %.1f TF/s (%.1f%% of 78.6)\n", "trailing3",
-               m, nk, run, items.size() / 2, ms, flops / ms * 1e-9, flops / ms * 1e-9 / 78.6 * 100);
+        printf("%s m=%d nk=%d run=%d items=%d  %.3f ms  %.1f TF/s (%.1f%% of 78.6)\n", k ? "trailing3k16" : "trailing3",
+               m, nk, run, n_it, ms, flops / ms * 1e-9, flops / ms * 1e-9 / 78.6 * 100);
     }
+    // the two variants must agree bit for bit (same K order per element): rerun each once from the
+    // same input and compare
+    std::vector<double> r0(h.size()), r1(h.size());
+    for (int k = 0; k < 2; ++k) {
+        CK(hipMemcpy(M, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+        if (k == 0) hipLaunchKernelGGL(dbslmm_tchol_trailing3, dim3(n_it), dim3(512), sizeof(double) * chol::kTrail3Doubles, 0, ta, run, d_items, n_it);
+        else hipLaunchKernelGGL(dbslmm_tchol_trailing3k16, dim3(n_it), dim3(512), sizeof(double) * chol::kTrail3k16Doubles, 0, ta, run, d_items, n_it);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(k ? r1.data() : r0.data(), M, h.size() * 8, hipMemcpyDeviceToHost));
+    }
+    size_t ndiff = 0;
+    double maxd = 0;
+    for (size_t i = 0; i < h.size(); ++i)
+        if (r0[i] != r1[i]) { ++ndiff; maxd = std::max(maxd, std::fabs(r0[i] - r1[i])); }
+    printf("k16 vs k32: %zu elements differ, max |diff| %.3e\n", ndiff, maxd);
     return 0;
 }
