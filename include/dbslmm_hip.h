@@ -64,9 +64,10 @@ typedef struct dbslmm_plan dbslmm_plan;
  * h2f_mode       plan_run_multi: 0 = tiled blocks factored once, the other sigmas solved by
  *                Chebyshev iteration on that factor when the bound allows (tau in (0, 1],
  *                <= 60 iterations); 1 = one factorisation per sigma (the merged sequence)
- * cheb_tol       relative error target of the Chebyshev iteration (default 1e-10: five orders below
- *                the 1e-5 parity bar on beta, two below the reference PCG's own deviation; the
- *                measured error is ~0.2 x the target: 8 iterations at h2f 0.8 / 1 / 1.2)
+ * cheb_tol       relative error target of the Chebyshev iteration (default 1e-9: four orders below
+ *                the 1e-5 parity bar on beta, one below the reference PCG's own deviation from the
+ *                exact solution (~1e-8); the measured error is ~0.2 x the target: 7 iterations at
+ *                h2f 0.8 / 1 / 1.2)
  * lead_min       tiled blocks with m >= lead_min form the lead group: their Gram tiles run first
  *                and their factorisation (the longest dependency chains) starts right after
  *                them, beside the rest of the Gram and the other blocks' factorisation (default

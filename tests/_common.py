@@ -19,6 +19,11 @@ def load_bed(path) -> np.ndarray:
     return np.fromfile(path, dtype=np.uint8)
 
 
+# dbslmm_options.cheb_tol default: the normwise bound of the h2f copies the Chebyshev iteration
+# solves on the base copy's factor (include/dbslmm_hip.h); direct solves are held to 1e-10
+CHEB_TOL = 1e-9
+
+
 def normwise(a, ref) -> float:
     a = np.asarray(a, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import ref_numpy as R
-from _common import BLOCKS_EUR1, GOLD, ROOT, TD, l_snps, rows_close
+from _common import BLOCKS_EUR1, CHEB_TOL, GOLD, ROOT, TD, l_snps, rows_close
 
 CLI = os.path.join(ROOT, "dbslmm_amd", "bin", "dbslmm")
 SUMM = os.path.join(TD, "summary_gemma_chr1.assoc.txt")
@@ -127,7 +127,7 @@ def test_cli_h2f_tuning_matches_separate_runs(tmp_path, monkeypatch, cheb):
     (<prefix>_h2f<hh>.dbslmm.txt, software/DBSLMM.R:204-219) with the same rows as three runs
     with -h 0.5*hh: identical with the merged factorisations (--h2f-merged); with the
     Chebyshev path (one factor, the other factors iterated) the same rows and values within
-    1e-10 of the largest |beta| (the base factor's file stays identical)."""
+    cheb_tol (CHEB_TOL) of the largest |beta| (the base factor's file stays identical)."""
     s, l = split_summary(tmp_path)
     base = ["-s", s, "-l", l, "-r", REF, "-b", BLOCKS_EUR1, "-n", "2400", "-nsnp", "996",
             "-mafMax", "0.2", "--precise-out"]
@@ -147,7 +147,7 @@ def test_cli_h2f_tuning_matches_separate_runs(tmp_path, monkeypatch, cheb):
             kt, vt = _eff_rows(tuned)
             kr, vr = _eff_rows(ref)
             assert kt == kr
-            assert np.max(np.abs(vt - vr)) <= 1e-10 * np.max(np.abs(vr))
+            assert np.max(np.abs(vt - vr)) <= CHEB_TOL * np.max(np.abs(vr))
 
 
 @pytest.mark.gpu

@@ -7,7 +7,8 @@ block by block with the oracle's direct fp64 solve of the reference equations
 * every block with m >= 2000 SNPs -- this includes the largest EUR block (~9.6k SNPs at 1M) and
   the largest AFR block (~11.7k), i.e. the tiled sequence's long-chain regime (>= 37 super steps,
   ~150-tile substitution chains) at n_ref = 10k, and for config 4 the Chebyshev h2f copies on
-  those blocks: normwise max|dbeta| / max|beta| <= 1e-10 per block, every h2f factor;
+  those blocks: normwise max|dbeta| / max|beta| <= 1e-10 per block (the Chebyshev-iterated h2f
+  copies: <= cheb_tol, CHEB_TOL), every h2f factor;
 * the same blocks against the reference-faithful Jacobi-PCG (abs. tol 1e-7, :629-678): <= 1e-5;
 * a random sample of the smaller blocks through the C oracle (direct): <= 1e-10;
 * every block: status OK and beta finite.
@@ -18,7 +19,7 @@ import pytest
 
 import oracle as O
 import ref_numpy as R
-from _common import normwise
+from _common import CHEB_TOL, normwise
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
@@ -105,6 +106,9 @@ def test_fullscale_blocks_match_oracle(cfg, devices):
         assert np.all(np.isfinite(bs)) and np.all(np.isfinite(bl))
     if len(factors) > 1:
         assert wl["cheb_iters"] > 0          # the Chebyshev h2f path is the one under test
+    # the base copy (median sigma) is solved directly, the others by Chebyshev on its factor
+    base = int(np.argsort(sig, kind="stable")[len(sig) // 2])
+    tol_c = [1e-10 if (len(sig) == 1 or c == base) else CHEB_TOL for c in range(len(sig))]
     thr = _threads()
     O.use_blas(True)
     O.blas_threads(thr)
@@ -119,7 +123,7 @@ def test_fullscale_blocks_match_oracle(cfg, devices):
                 d = normwise(got, ref["chol"][c])
                 p = normwise(got, ref["pcg"][c])
                 worst_d, worst_p = max(worst_d, d), max(worst_p, p)
-                assert d <= 1e-10, (cfg, int(b), int(m_b[b]), c, d)
+                assert d <= tol_c[c], (cfg, int(b), int(m_b[b]), c, d)
                 assert p <= 1e-5, (cfg, int(b), int(m_b[b]), c, p)
         print(f"config {cfg}: {len(big)} blocks >= {BIG} SNPs (max {int(m_b.max())}), "
               f"worst normwise vs direct {worst_d:.2e}, vs PCG {worst_p:.2e}")
@@ -138,4 +142,4 @@ def test_fullscale_blocks_match_oracle(cfg, devices):
         assert rc == 0
         got = np.concatenate([out[c][0][s_idx], out[c][1][l_idx]])
         ref = np.concatenate([rs, rl])
-        assert normwise(got, ref) <= 1e-10, (cfg, c)
+        assert normwise(got, ref) <= tol_c[c], (cfg, c)
