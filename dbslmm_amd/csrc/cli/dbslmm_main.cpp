@@ -55,6 +55,7 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     string gpu_ids;                 // --gpus N -> "0,1,..,N-1"; --gpu-ids a,b,..
     double tau = 0.8;
     bool precise = false, dry_run = false, h2f_merged = false, timing = false;
+    int repeat = 0;                 // --repeat N: N more solves of the resident problem (timing)
     string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
 };
 
@@ -101,6 +102,8 @@ void print_help() {
               << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
               << " --precise-out          17 significant digits in <eff>.txt (extension)\n"
               << " --timing               phase wall times as one JSON line on stderr (extension)\n"
+              << " --repeat  [num]        with --timing: num more solves of the resident problem, their\n"
+              << "                        wall times in the JSON line as solve_repeat (extension)\n"
               << " -h2f      [list]       h2 factors, e.g. 0.8,1,1.2: one Gram, one solve per factor,\n"
               << "                        <eff>_h2f<f>.txt each (software/DBSLMM.R tuning, extension)\n"
               << " --h2f-merged           -h2f: one factorisation per factor instead of one factor +\n"
@@ -143,6 +146,7 @@ void assign(int argc, char** argv, Param& p) {
         else if (!strcmp(a, "--h2f-merged")) p.h2f_merged = true;
         else if (!strcmp(a, "--dry-run")) p.dry_run = true;
         else if (!strcmp(a, "--timing")) p.timing = true;
+        else if (!strcmp(a, "--repeat")) { if ((v = take(i))) p.repeat = std::max(0, atoi(v)); }
     }
 }
 
@@ -387,6 +391,9 @@ struct Phases {
         char buf[96];
         snprintf(buf, sizeof(buf), "%s\"%s\": %.6f", json.empty() ? "" : ", ", name, sec);
         json += buf;
+    }
+    void put_raw(const char* name, const string& v) {
+        json += (json.empty() ? "\"" : ", \"") + string(name) + "\": " + v;
     }
     void mark(const char* name) {
         const double t = walltime();
@@ -717,6 +724,18 @@ int main(int argc, char** argv) {
     ph.mark("plan");
     if (rc == DBSLMM_OK) rc = dbslmm_plan_run_multi(plan, sigmas.data(), nf, beta_s.data(), beta_l.data(), status.data());
     ph.mark("solve");
+    if (p.timing && p.repeat > 0 && rc == DBSLMM_OK) {   // the same solve again, inputs resident
+        string rep;
+        for (int k = 0; k < p.repeat && rc == DBSLMM_OK; ++k) {
+            const double r0 = walltime();
+            rc = dbslmm_plan_run_multi(plan, sigmas.data(), nf, beta_s.data(), beta_l.data(), status.data());
+            char buf[32];
+            snprintf(buf, sizeof(buf), "%s%.6f", k ? ", " : "", walltime() - r0);
+            rep += buf;
+        }
+        ph.put_raw("solve_repeat", "[" + rep + "]");
+        ph.last = walltime();
+    }
     if (rc != DBSLMM_OK) {
         dbslmm_plan_destroy(plan);
         return fail(string("dbslmm_plan_run_multi: ") + dbslmm_last_error(ctx));
