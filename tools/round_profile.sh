@@ -13,6 +13,8 @@ tail -1 $O/bench_c4.log > $O/bench_c4.json
 run 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-isolated > $O/c4_prof.log 2>&1
 run 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc4 -o fetch -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-isolated > $O/pmc4_fetch.log 2>&1
 run 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc4 -o write -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-isolated > $O/pmc4_write.log 2>&1
+run 300 python bench.py --config 1 > $O/bench_c1.log 2>&1
+tail -1 $O/bench_c1.log > $O/bench_c1.json
 for N in 2 3 5; do
   CPU=""; [ $N -le 3 ] || CPU="--no-cpu-baseline"
   STEPS="--steps 5 --warmup 2"; [ $N -eq 2 ] && STEPS="--steps 20 --warmup 3"
