@@ -706,17 +706,16 @@ __device__ __forceinline__ void t3_mfma_stage(v4d (&acc)[4][2], const double* SA
 }
 
 template <int KS>
-__device__ __forceinline__ void trailing3_body(const TiledArgs& a0, int32_t run, const int32_t* __restrict__ items,
-                                               int32_t n_items, double* lds) {
+__device__ __forceinline__ void trailing3_item(const TiledArgs& a0, int32_t run, const int32_t* __restrict__ items,
+                                               int e, double* lds) {
     using P = T3<KS>;
     // K = 32: the next tile's C is prefetched during the current tile's last stage; K = 16 (two
     // workgroups per CU, 128 VGPRs) loads it at the tile's first stage -- the other workgroup's
     // MFMAs cover that wait
     constexpr bool kPrefetchC = KS == 32;
-    if (static_cast<int>(blockIdx.x) >= n_items) return;
-    const int32_t it = items[2 * blockIdx.x];
+    const int32_t it = items[2 * e];
     if (it < 0) return;
-    const int32_t meta = items[2 * blockIdx.x + 1];
+    const int32_t meta = items[2 * e + 1];
     const int s = meta >> 8, nk = meta & 255;
     const int I = (it >> 8) & 255, J0 = it & 255;
     int b;
@@ -772,14 +771,23 @@ __device__ __forceinline__ void trailing3_body(const TiledArgs& a0, int32_t run,
 }
 }  // namespace chol
 
+// Work item e of the launch's list, for e = blockIdx.x, + gridDim.x, ... (a grid capped to a
+// multiple of 8 keeps item e on XCD e % 8; the plan launches one workgroup per item -- capped
+// grids that left 16 / 32 CUs to the chain kernels measured no faster)
 extern "C" __global__ __launch_bounds__(512, 1) void dbslmm_tchol_trailing3(
     chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    chol::trailing3_body<chol::kK2>(a0, run, items, n_items, lds);
+    for (int e = blockIdx.x; e < n_items; e += gridDim.x) {
+        chol::trailing3_item<chol::kK2>(a0, run, items, e, lds);
+        __syncthreads();   // every wave is done with the LDS slots before the next item's DMA
+    }
 }
 extern "C" __global__ __launch_bounds__(512, 4) void dbslmm_tchol_trailing3k16(   // 4 waves per SIMD: two workgroups per CU
     chol::TiledArgs a0, int32_t run, const int32_t* __restrict__ items, int32_t n_items) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    chol::trailing3_body<16>(a0, run, items, n_items, lds);
+    for (int e = blockIdx.x; e < n_items; e += gridDim.x) {
+        chol::trailing3_item<16>(a0, run, items, e, lds);
+        __syncthreads();
+    }
 }
 
