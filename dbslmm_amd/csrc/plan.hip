@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -249,90 +250,99 @@ static int mp_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int32_t n_ref, int64_
         }                                                                \
     } while (0)
 
-// Host -> device copy of a large, possibly pageable (mmap'd, page-cache backed) buffer through two
-// pinned staging buffers: while chunk k is DMA'd, host threads copy chunk k + 1 into the other
-// buffer (the page-cache reads of an mmap'd .bed are the slow side, so they run on several
-// threads).  Small buffers take a plain hipMemcpy.  Ends synchronised.
-static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_t st) {
-    constexpr size_t kChunk = size_t(64) << 20;
-    if (n <= 2 * kChunk) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice);
-    void* stage[2] = {nullptr, nullptr};
-    hipEvent_t done[2] = {nullptr, nullptr};
+// Host -> device copy of a large buffer through pinned staging buffers: a pool of host threads
+// fills chunk k + 1 (memcpy from the caller's memory, or pread from a file) while chunk k's DMA
+// runs; kStageBufs buffers, each reused once its copy's event has completed.  The threads live
+// for the whole copy (no per-chunk thread start).  Small buffers take a plain hipMemcpy.  Ends
+// synchronised.  fill(dst, offset, len) -> false on error.
+template <class Fill>
+static hipError_t upload_pipelined(void* dst, size_t n, hipStream_t st, Fill fill) {
+    // 4 x 16 MiB: pinning costs ~0.25 ms per MiB on the box (3 x 64 MiB took 47 ms), while 16 MiB
+    // DMAs still run at ~45 GB/s (tools/micro/upload_probe)
+    constexpr size_t kChunk = size_t(16) << 20;
+    constexpr int kStageBufs = 4;
+    void* stage[kStageBufs] = {};
+    hipEvent_t done[kStageBufs] = {};
     hipError_t e = hipSuccess;
-    for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+    for (int b = 0; b < kStageBufs && e == hipSuccess; ++b) {
         e = hipHostMalloc(&stage[b], kChunk, hipHostMallocDefault);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&done[b], hipEventDisableTiming);
     }
-    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    for (size_t off = 0, k = 0; off < n && e == hipSuccess; off += kChunk, ++k) {
-        const int b = static_cast<int>(k & 1);
-        const size_t len = std::min(kChunk, n - off);
-        if (k >= 2 && (e = hipEventSynchronize(done[b])) != hipSuccess) break;   // buffer b free again
-        const char* s0 = static_cast<const char*>(src) + off;
-        char* d0 = static_cast<char*>(stage[b]);
-        std::vector<std::thread> th;
-        const size_t part = (len + hw - 1) / hw;
-        for (unsigned t = 0; t < hw; ++t) {
-            const size_t a = t * part, z = std::min(len, a + part);
-            if (a < z) th.emplace_back([=] { memcpy(d0 + a, s0 + a, z - a); });
+    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t nchunk = (n + kChunk - 1) / kChunk;
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t go = -1;                      // chunks the workers may fill (buffer free)
+    std::vector<unsigned> parts(nchunk, 0);
+    bool bad = false, stop = false;
+    std::vector<std::thread> th;
+    if (e == hipSuccess)
+        for (unsigned t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                for (size_t k = 0; k < nchunk; ++k) {
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return go >= static_cast<int64_t>(k) || stop; });
+                        if (stop) return;
+                    }
+                    const size_t off = k * kChunk, len = std::min(kChunk, n - off);
+                    const size_t part = (len + T - 1) / T, a0 = std::min(len, t * part), z = std::min(len, a0 + part);
+                    const bool ok = a0 >= z || fill(static_cast<char*>(stage[k % kStageBufs]) + a0, off + a0, z - a0);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (!ok) bad = true;
+                    ++parts[k];
+                    cv.notify_all();
+                }
+            });
+    for (size_t k = 0; k < nchunk && e == hipSuccess; ++k) {
+        const int b = static_cast<int>(k % kStageBufs);
+        if (k >= kStageBufs && (e = hipEventSynchronize(done[b])) != hipSuccess) break;   // buffer b free
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            go = static_cast<int64_t>(k);
+            cv.notify_all();
+            cv.wait(lk, [&] { return parts[k] == T; });
+            if (bad) { e = hipErrorInvalidValue; break; }
         }
-        for (auto& t : th) t.join();
+        const size_t off = k * kChunk, len = std::min(kChunk, n - off);
         e = hipMemcpyAsync(static_cast<char*>(dst) + off, stage[b], len, hipMemcpyHostToDevice, st);
         if (e == hipSuccess) e = hipEventRecord(done[b], st);
     }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+        cv.notify_all();
+    }
+    for (auto& t : th) t.join();
     const hipError_t e2 = hipStreamSynchronize(st);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kStageBufs; ++b) {
         if (done[b]) (void)hipEventDestroy(done[b]);
         if (stage[b]) (void)hipHostFree(stage[b]);
     }
     return e != hipSuccess ? e : e2;
 }
 
-// upload_staged reading the bytes from a file descriptor (pread straight into the pinned staging
-// buffers, several threads per chunk): the caller's pages of the file are never faulted in, so
-// neither the copy nor the process's exit pays for hundreds of thousands of page-table entries.
+static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_t st) {
+    if (n <= (size_t(128) << 20)) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice);
+    return upload_pipelined(dst, n, st, [src](char* d, size_t off, size_t len) {
+        memcpy(d, static_cast<const char*>(src) + off, len);
+        return true;
+    });
+}
+
+// The same reading the bytes from a file descriptor (pread straight into the pinned staging
+// buffers): the caller's pages of the file are never faulted in, so neither the copy nor the
+// process's exit pays for hundreds of thousands of page-table entries.
 static hipError_t upload_staged_fd(void* dst, int fd, size_t n, hipStream_t st) {
-    constexpr size_t kChunk = size_t(64) << 20;
-    void* stage[2] = {nullptr, nullptr};
-    hipEvent_t done[2] = {nullptr, nullptr};
-    hipError_t e = hipSuccess;
-    for (int b = 0; b < 2 && e == hipSuccess; ++b) {
-        e = hipHostMalloc(&stage[b], kChunk, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&done[b], hipEventDisableTiming);
-    }
-    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    for (size_t off = 0, k = 0; off < n && e == hipSuccess; off += kChunk, ++k) {
-        const int b = static_cast<int>(k & 1);
-        const size_t len = std::min(kChunk, n - off);
-        if (k >= 2 && (e = hipEventSynchronize(done[b])) != hipSuccess) break;   // buffer b free again
-        char* d0 = static_cast<char*>(stage[b]);
-        std::vector<std::thread> th;
-        std::vector<char> ok(hw, 1);
-        const size_t part = (len + hw - 1) / hw;
-        for (unsigned t = 0; t < hw; ++t) {
-            const size_t a = t * part, z = std::min(len, a + part);
-            if (a < z)
-                th.emplace_back([=, &ok] {
-                    size_t got = a;
-                    while (got < z) {
-                        const ssize_t r = pread(fd, d0 + got, z - got, static_cast<off_t>(off + got));
-                        if (r <= 0) { ok[t] = 0; return; }
-                        got += static_cast<size_t>(r);
-                    }
-                });
+    return upload_pipelined(dst, n, st, [fd](char* d, size_t off, size_t len) {
+        size_t got = 0;
+        while (got < len) {
+            const ssize_t r = pread(fd, d + got, len - got, static_cast<off_t>(off + got));
+            if (r <= 0) return false;
+            got += static_cast<size_t>(r);
         }
-        for (auto& t : th) t.join();
-        for (char o : ok)
-            if (!o) e = hipErrorInvalidValue;
-        if (e == hipSuccess) e = hipMemcpyAsync(static_cast<char*>(dst) + off, stage[b], len, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipEventRecord(done[b], st);
-    }
-    const hipError_t e2 = hipStreamSynchronize(st);
-    for (int b = 0; b < 2; ++b) {
-        if (done[b]) (void)hipEventDestroy(done[b]);
-        if (stage[b]) (void)hipHostFree(stage[b]);
-    }
-    return e != hipSuccess ? e : e2;
+        return true;
+    });
 }
 
 // memcpy on up to 8 host threads (a result download lands in pinned memory; the caller's arrays
@@ -890,14 +900,25 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                             ld_[x] += 1;
                         }
                 }
-            ops_exec += 2.0 * p->kpad * gram::kHT * gram::kHT * (T * (T + 1) / 2);
+            // MFMA work actually issued (dbslmm_gram_huge): 32 x 32 sub-tiles with rows and
+            // columns < m, and on a diagonal tile not strictly above its diagonal
+            int64_t sub = 0;
+            for (int ti = 0; ti < T; ++ti)
+                for (int tj = 0; tj <= ti; ++tj) {
+                    const int64_t rv = std::min<int64_t>(gram::kHT, m - int64_t(gram::kHT) * ti);
+                    const int64_t cv = std::min<int64_t>(gram::kHT, m - int64_t(gram::kHT) * tj);
+                    const int64_t ni = (rv + 31) / 32, nj = (cv + 31) / 32;
+                    sub += ti != tj ? ni * nj : ni * (ni + 1) / 2;   // (diagonal: rv == cv)
+                }
+            ops_exec += 2.0 * p->kpad * 32 * 32 * sub;
         } else if (m >= gram_big_min) {   // 128 x 128 tiles, the block's queue on the least-loaded XCD
             const int T = static_cast<int>((m + gram::kGT - 1) / gram::kGT);
             const int x = static_cast<int>(std::min_element(xload.begin(), xload.end()) - xload.begin());
             for (int ti = 0; ti < T; ++ti)
                 for (int tj = 0; tj <= ti; ++tj) xq[x].push_back({nb, ti, tj, 0});
             xload[x] += T * (T + 1) / 2;
-            ops_exec += 2.0 * p->kpad * gram::kGT * gram::kGT * (T * (T + 1) / 2);
+            // (dbslmm_gram_big: whole 128 x 128 tiles; a diagonal tile skips its upper quadrant)
+            ops_exec += 2.0 * p->kpad * gram::kGT * gram::kGT * (T * (T - 1) / 2 + 0.75 * T);
         } else {
             const int T = static_cast<int>((m + kTile - 1) / kTile);   // tiles holding SNP rows
             for (int ti = 0; ti < T; ++ti)
