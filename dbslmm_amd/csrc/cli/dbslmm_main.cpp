@@ -761,7 +761,8 @@ int main(int argc, char** argv) {
             return fail("variance.txt cannot be written");
         }
     }
-    dbslmm_plan_destroy(plan);
+    // (no dbslmm_plan_destroy / dbslmm_ctx_destroy on the way out: the process ends with _Exit
+    // below and the driver releases its device memory; freeing ~10 GB first only delays the exit)
     std::cout << "Fitting time: " << walltime() - t0 << " seconds.\n";
     ph.mark("variance");
 
@@ -791,7 +792,6 @@ int main(int argc, char** argv) {
     }
     if (!write_eff_files(names, lists, p.precise ? 17 : 6)) return fail(names[0] + ".txt cannot be written");
     ph.mark("write");
-    dbslmm_ctx_destroy(ctx);
     if (p.timing) ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));
     // the parsed inputs (views of the mappings, hash index, host arrays) need no teardown
     std::cout.flush();
