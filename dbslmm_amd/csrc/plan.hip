@@ -183,6 +183,7 @@ struct dbslmm_plan {
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev;  // kEvPerRun per run
+    std::vector<hipEvent_t> dl_ev;   // result download: one per factorisation copy
     std::vector<hipEvent_t> tev; // dependencies between the tiled sequence's two streams
     std::vector<hipEvent_t> tev_rest;   // ... of the rest sequence
     // h2f tuning by Chebyshev on one factor (trsv.hip): tile work lists of the tiled blocks in
@@ -745,6 +746,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : p->dl_ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : p->tev) (void)hipEventDestroy(e);
     for (hipEvent_t e : p->tev_rest) (void)hipEventDestroy(e);
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
@@ -1916,15 +1918,28 @@ static int download_copies(dbslmm_plan* p, int c0, int n, double* beta_s, double
     double* ps = static_cast<double*>(p->h_pin);
     double* pl = ps + nbs;
     int32_t* pt = reinterpret_cast<int32_t*>(pl + nbl);
-    if (nbs) HIP_TRY(ctx, hipMemcpyAsync(ps, p->d_beta_s + static_cast<int64_t>(c0) * p->n_s, nbs * sizeof(double),
-                                         hipMemcpyDeviceToHost, ctx->stream));
-    if (nbl) HIP_TRY(ctx, hipMemcpyAsync(pl, p->d_beta_l + static_cast<int64_t>(c0) * p->n_l, nbl * sizeof(double),
-                                         hipMemcpyDeviceToHost, ctx->stream));
+    // per copy: its DMA into the pinned buffer, an event, then (below) its host copy-out while the
+    // next copy's DMA runs
+    while (static_cast<int>(p->dl_ev.size()) < n) {
+        hipEvent_t e;
+        HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        p->dl_ev.push_back(e);
+    }
     if (nst) HIP_TRY(ctx, hipMemcpyAsync(pt, p->d_status + c0 * p->nbk, nst * sizeof(int32_t),
                                          hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (nbs) par_memcpy(beta_s, ps, nbs * sizeof(double));
-    if (nbl) par_memcpy(beta_l, pl, nbl * sizeof(double));
+    const size_t cs = nbs / n, cl = nbl / n;   // per copy
+    for (int c = 0; c < n; ++c) {
+        if (cs) HIP_TRY(ctx, hipMemcpyAsync(ps + c * cs, p->d_beta_s + static_cast<int64_t>(c0 + c) * p->n_s,
+                                            cs * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        if (cl) HIP_TRY(ctx, hipMemcpyAsync(pl + c * cl, p->d_beta_l + static_cast<int64_t>(c0 + c) * p->n_l,
+                                            cl * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(p->dl_ev[c], ctx->stream));
+    }
+    for (int c = 0; c < n; ++c) {
+        HIP_TRY(ctx, hipEventSynchronize(p->dl_ev[c]));
+        if (cs) par_memcpy(beta_s + c * cs, ps + c * cs, cs * sizeof(double));
+        if (cl) par_memcpy(beta_l + c * cl, pl + c * cl, cl * sizeof(double));
+    }
     for (int c = 0; c < n && nst; ++c) {
         int32_t* out = block_status + static_cast<int64_t>(c) * p->num_block;
         memcpy(out, pt + c * p->nbk, p->num_block * sizeof(int32_t));
