@@ -101,6 +101,12 @@ __device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
     const v8i a8{a[0], a[1], a[2], a[3], 0, 0, 0, 0}, b8{b[0], b[1], b[2], b[3], 0, 0, 0, 0};
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
 }
+// centred Gram entry C_ij = G_ij - S_i S_j / n, as G - (S_i S_j) (1 / n) in one fma: S_i S_j is
+// an exact integer (below 2^53), the product with the rounded reciprocal replaces an fp64 divide
+// per element (relative deviation from the divided form ~1e-16 of S_i S_j / n)
+__device__ __forceinline__ double centre(float g, double sisj, double rn) {
+    return __builtin_fma(-sisj, rn, static_cast<double>(g));
+}
 // missing-call form of a Gp dword (code 3 = missing): g = the dosages with missing calls as 0,
 // o = 1 for observed calls (padding individuals count as observed: pad_k in the epilogue)
 __device__ __forceinline__ void split_missing(uint32_t x, uint32_t& g, uint32_t& o) {
@@ -289,7 +295,7 @@ __device__ __forceinline__ void gram_tile32(
     const double Sj = lj < m ? S[sj] : 0.0;
     const double muj = lj < m ? mu[sj] : 0.0;
     const double rj = lj < m ? rsd[sj] : 0.0;
-    const double scale = tau / n_ref_d;
+    const double scale = tau / n_ref_d, rn = 1.0 / n_ref_d;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int i = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -298,7 +304,7 @@ __device__ __forceinline__ void gram_tile32(
         const int si = row0 + li;
         double c;
         if (!missing) {
-            c = static_cast<double>(acc[r]) - S[si] * Sj / n_ref_d;
+            c = centre(acc[r], S[si] * Sj, rn);
         } else {
             const double mui = mu[si];
             c = static_cast<double>(acc[r]) - muj * static_cast<double>(acc_go[r]) -
@@ -457,7 +463,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     if (idle) return;
     // fp64 epilogue (as dbslmm_gram_i8, no-missing form): C/D col = lane & 31,
     // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-    const double scale = tau / n_ref_d;
+    const double scale = tau / n_ref_d, rn = 1.0 / n_ref_d;
 #pragma unroll
     for (int sj = 0; sj < 2; ++sj) {
         const int lj = kGT * tile.tj + 64 * wc + 32 * sj + (lane & 31);
@@ -469,7 +475,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
             for (int r = 0; r < 16; ++r) {
                 const int li = kGT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 if (li >= m) continue;
-                const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
+                const double c = centre(acc[si][sj][r], S[row0 + li] * Sj, rn);
                 double v = scale * (c * rsd[row0 + li] * rj);
                 if (li == lj) v += 1.0 - tau;
                 for (int cp = copy_lo(m, tmin, tcopy); cp < copy_hi(m, tmin, tcopy, ncopy); ++cp)
@@ -511,22 +517,126 @@ constexpr int kKpadAlign = kHK;            // kpad: a multiple of the FP4 stage
 __device__ __forceinline__ int swz(int r, int c) { return r * kHRow + 16 * (c ^ ((r ^ (r >> 2) ^ (r >> 3)) & 7)); }
 }  // namespace gram
 
-extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
-    const uint32_t* __restrict__ Gp, int64_t kpad,
-    const GramTile* __restrict__ tiles, int32_t n_tiles,
-    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,
-    const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,
-    const int32_t* __restrict__ block_flags,
-    const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
-    double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
+// K loop of dbslmm_gram_huge fed by LDS-DMA.  A stage (256 individuals) of a tile row is its 64 B
+// of raw 2-bit Gp codes; global_load_lds_dwordx4 moves them straight into LDS (no staging
+// registers, no LDS store instructions), four slots (32 KiB each: A | B), three stages in flight.
+// LDS image: row r of an operand at r * 64 B, its 16-B chunk q at position q ^ ((r >> 2) & 3) --
+// the DMA writes lane-linear, so the swizzle goes through the source address -- which puts the
+// 16 rows of every ds_read_b128 lane group on 16 distinct bank groups.  Consumer: lane (row,
+// h = lane >> 5) reads chunk q = 2 j + h of its row (16 B = 64 codes) for k-steps 2 j and 2 j + 1
+// and expands each half (Gp dwords 0-1, 2-3) to one 16-B FP4 operand (fp4_chunk); A and B use the
+// same individual -> k map, so every product sums each individual once.  NOP = operands staged
+// (1: a diagonal tile, B = A); kFull: every MFMA tile of the wave's piece is active.
+template <int NOP, bool kFull>
+__device__ __forceinline__ void gram_huge_dma_loop(const uint32_t* __restrict__ Gp, int64_t kw,
+                                                   const int64_t (&rbase)[2], const int (&svl)[2], int nst,
+                                                   int8_t* lds, int wave, int lane, int wr, int wc,
+                                                   uint32_t act, v16f (&acc)[2][4]) {
+    typedef __attribute__((address_space(1))) const void* gptr_g;
+    typedef __attribute__((address_space(3))) void* lptr_g;
+    constexpr int kRowB = 64;                        // raw bytes per row and stage
+    constexpr int kOpB = gram::kHT * kRowB;          // 16 KiB per operand stage
+    constexpr int kSlotB = 2 * kOpB;                 // A | B
+    // DMA map: wave w moves rows 32 w .. 32 w + 31 of each staged operand, 16 rows per
+    // instruction; lane L -> row + (L >> 2), LDS position L & 3 holding chunk (L & 3) ^ ((row >> 2) & 3)
+    const int dr = lane >> 2, dp = lane & 3;
+    const uint32_t* gsrc[NOP][2];
+#pragma unroll
+    for (int op = 0; op < NOP; ++op)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = 32 * wave + 16 * h + dr;
+            const int q = dp ^ ((r >> 2) & 3);
+            gsrc[op][h] = Gp + (rbase[op] + min(r, svl[op] - 1)) * kw + 4 * q;
+        }
+    auto issue = [&](int st) {
+        int8_t* slot = lds + (st & 3) * kSlotB;
+#pragma unroll
+        for (int op = 0; op < NOP; ++op)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                __builtin_amdgcn_global_load_lds((gptr_g)(gsrc[op][h] + 16 * st),
+                                                 (lptr_g)(slot + op * kOpB + (32 * wave + 16 * h) * kRowB), 16, 0, 0);
+    };
+    const int rsub = lane & 31, hh = lane >> 5;
+    // operand read offsets within a slot (chunk 2 j + hh of the row; j adds 32 B before the swizzle)
+    auto roff = [&](int r, int j) { return r * kRowB + 16 * ((2 * j + hh) ^ ((r >> 2) & 3)); };
+    auto compute = [&](int st) {
+        const int8_t* A = lds + (st & 3) * kSlotB;
+        const int8_t* B = NOP == 1 ? A : A + kOpB;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            v4i ar[2], br[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) ar[i] = *reinterpret_cast<const v4i*>(A + roff(64 * wr + 32 * i + rsub, j));
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) br[jj] = *reinterpret_cast<const v4i*>(B + roff(128 * wc + 32 * jj + rsub, j));
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                v4i av[2], bv[4];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    av[i] = fp4_chunk(static_cast<uint32_t>(ar[i][2 * e]), static_cast<uint32_t>(ar[i][2 * e + 1]));
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    bv[jj] = fp4_chunk(static_cast<uint32_t>(br[jj][2 * e]), static_cast<uint32_t>(br[jj][2 * e + 1]));
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        if (kFull || (act & (1u << (4 * i + jj)))) acc[i][jj] = mfma_fp4(av[i], bv[jj], acc[i][jj]);
+            }
+        }
+    };
+    // vmcnt counts this wave's DMA instructions in issue order (2 NOP per stage)
+    auto wait_stage = [&](int ahead) {   // ahead = stages issued after the one awaited
+        if (ahead >= 2) {
+            if constexpr (NOP == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else if (ahead == 1) {
+            if constexpr (NOP == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    };
+    for (int st = 0; st < min(3, nst); ++st) issue(st);
+    for (int st = 0; st < nst; ++st) {
+        wait_stage(min(2, nst - 1 - st));
+        __builtin_amdgcn_s_barrier();            // stage st is in LDS; slot (st + 3) & 3 is free
+        if (st + 3 < nst) issue(st + 3);
+        compute(st);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                // every wave is done with the slots
+}
+
+#define GRAM_HUGE_PARAMS                                                                            \
+    const uint32_t* __restrict__ Gp, int64_t kpad,                                                 \
+    const GramTile* __restrict__ tiles, int32_t n_tiles,                                           \
+    const int32_t* __restrict__ blk_row0, const int32_t* __restrict__ blk_m,                       \
+    const int32_t* __restrict__ blk_ld, const int64_t* __restrict__ blk_matoff,                    \
+    const int32_t* __restrict__ block_flags,                                                       \
+    const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,   \
+    double n_ref_d, double pad_k, double tau, double* __restrict__ M,                              \
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy
+#define GRAM_HUGE_ARGS Gp, kpad, tiles, n_tiles, blk_row0, blk_m, blk_ld, blk_matoff, block_flags, S, \
+    mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride, tmin, tcopy
+// kMode 2: LDS-DMA of the raw 2-bit stages (see gram_huge_dma_loop); kMode 1 (kQuarter): a stage's
+// Gp rows are loaded by 4 lanes each (16 B per lane, 16 rows per wave instruction) and expanded
+// into LDS; kMode 0: one lane loads a whole row's 64 B (64 rows per wave instruction)
+template <int kMode>
+__device__ __forceinline__ void gram_huge_body(GRAM_HUGE_PARAMS) {
+    constexpr bool kQuarter = kMode == 1;
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t hlds[];
     if (static_cast<int>(blockIdx.x) >= n_tiles) return;
     const GramTile tile = tiles[blockIdx.x];
     const int b = tile.block;
     if (b < 0) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // (wave and the per-wave MFMA mask are wave-uniform: readfirstlane keeps their branches scalar)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int row0 = blk_row0[b], m = blk_m[b], ld = blk_ld[b];
     const int64_t moff = blk_matoff[b];
     const bool diag = tile.ti == tile.tj;
@@ -546,14 +656,25 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
     // stages ahead in two register sets.
     const int64_t kw = kpad / 16;
     const int sop = tid >> 8, srow = tid & 255;
+    // kQuarter: thread -> rows sr + 64 i (i = 0..3), 16-B quarter sq of each row's 64 B
+    const int sq = srow & 3, sr = srow >> 2;
     // ragged edge tiles: rows / columns of the tile inside the block (the last tile row / column
     // of a block is partly padding).  Rows past them are not expanded into LDS and their loads
     // re-read the last valid row (an L2 hit); the MFMAs that would only produce rows or columns
     // past m are skipped, so an edge tile costs about its valid area.
     const int rv = min(kHT, m - kHT * tile.ti), cv = min(kHT, m - kHT * tile.tj);
     const int svalid = sop ? cv : rv;
-    const bool stager = !(diag && sop == 1) && srow < svalid;
-    const uint32_t* gs = Gp + static_cast<int64_t>(row0 + kHT * (sop ? tile.tj : tile.ti) + min(srow, svalid - 1)) * kw;
+    const bool sact = !(diag && sop == 1);
+    const bool stager = sact && srow < svalid;
+    const int64_t obase = row0 + kHT * (sop ? tile.tj : tile.ti);
+    // kQuarter: row sr + 64 i of the tile (clamped to the last valid one) at gs + d_i * kw, the row
+    // deltas d_i <= 255 packed in the bytes of dpk
+    const int sr0 = min(sr, svalid - 1);
+    const uint32_t* gs = Gp + (obase + (kQuarter ? sr0 : min(srow, svalid - 1))) * kw + (kQuarter ? 4 * sq : 0);
+    uint32_t dpk = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) dpk |= static_cast<uint32_t>(min(sr + 64 * i, svalid - 1) - sr0) << (8 * i);
+    const uint32_t kw32 = static_cast<uint32_t>(kw);
     const int nst = static_cast<int>(kpad / kHK);   // kpad is a multiple of kHK
     // unconditional loads (clamped stage, valid rows for every thread) keep the vmcnt bookkeeping
     // exact: the newer loads in flight at every use are known
@@ -562,18 +683,30 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         const uint32_t* g = gs + (kHK / 16) * min(st, nst - 1);
         Pk pk;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pk.q[i] = *reinterpret_cast<const v4i*>(g + 4 * i);
+        for (int i = 0; i < 4; ++i)
+            pk.q[i] = *reinterpret_cast<const v4i*>(
+                g + (kQuarter ? ((dpk >> (8 * i)) & 255u) * kw32 : 4u * i));
         return pk;
     };
-    auto chunk = [](const Pk& pk, int c) {           // Gp dwords 2c, 2c + 1
-        return fp4_chunk(static_cast<uint32_t>(pk.q[c >> 1][2 * (c & 1)]),
-                         static_cast<uint32_t>(pk.q[c >> 1][2 * (c & 1) + 1]));
+    // piece e of the 8 16-B FP4 pieces a thread writes per stage: (LDS row, chunk, Gp dwords)
+    auto prow = [&](int e) { return kQuarter ? sr + 64 * (e >> 1) : srow; };
+    // LDS offset of piece e; kQuarter: swz(sr + 64 i, c) = swz(sr, c) + 64 i kHRow (the swizzle
+    // reads row bits 0..5 only)
+    const int wq0 = swz(kQuarter ? sr : srow, kQuarter ? 2 * sq : 0), wq1 = swz(sr, 2 * sq + 1);
+    auto poff = [&](int e) {
+        return kQuarter ? ((e & 1) ? wq1 : wq0) + 64 * kHRow * (e >> 1) : swz(srow, e);
+    };
+    auto chunk = [](const Pk& pk, int e) {           // Gp dwords 2 (e & 1), + 1 of quad e >> 1
+        return fp4_chunk(static_cast<uint32_t>(pk.q[e >> 1][2 * (e & 1)]),
+                         static_cast<uint32_t>(pk.q[e >> 1][2 * (e & 1) + 1]));
     };
     auto lstore = [&](const Pk& pk, int st) {
-        if (!stager) return;
+        if (!(kQuarter ? sact : stager)) return;
         int8_t* slot = hlds + (st & 1) * 2 * kHOp + sop * kHOp;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) *reinterpret_cast<v4i*>(slot + swz(srow, c)) = chunk(pk, c);
+        for (int e = 0; e < 8; ++e)
+            if (!kQuarter || prow(e) < svalid)
+                *reinterpret_cast<v4i*>(slot + poff(e)) = chunk(pk, e);
     };
     // wave -> piece: the two waves of a SIMD (w, w + 4) hold one row group in each half of the
     // tile and opposite column halves, so the skipped MFMAs of an edge tile leave every SIMD with
@@ -589,6 +722,7 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             const int ri = 64 * wr + 32 * i, cj = 128 * wc + 32 * j;
             if (ri < rv && cj < cv && !(diag && cj >= ri + 32)) act |= 1u << (4 * i + j);
         }
+    act = __builtin_amdgcn_readfirstlane(act);
     const bool idle = act == 0;
     v16f acc[2][4];
 #pragma unroll
@@ -617,6 +751,18 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
                     if (act & (1u << (4 * i + j))) acc[i][j] = mfma_fp4(av[i], bv[j], acc[i][j]);
         }
     };
+    if constexpr (kMode == 2) {
+        const int nst2 = static_cast<int>(kpad / kHK);
+        const int64_t rbase[2] = {row0 + kHT * tile.ti, row0 + kHT * tile.tj};
+        const int svl[2] = {rv, cv};
+        if (diag) {
+            if (act == 0xFFu) gram_huge_dma_loop<1, true>(Gp, kw, rbase, svl, nst2, hlds, wave, lane, wr, wc, act, acc);
+            else gram_huge_dma_loop<1, false>(Gp, kw, rbase, svl, nst2, hlds, wave, lane, wr, wc, act, acc);
+        } else {
+            if (act == 0xFFu) gram_huge_dma_loop<2, true>(Gp, kw, rbase, svl, nst2, hlds, wave, lane, wr, wc, act, acc);
+            else gram_huge_dma_loop<2, false>(Gp, kw, rbase, svl, nst2, hlds, wave, lane, wr, wc, act, acc);
+        }
+    } else {
     // two register sets: the loads of stage st + 3 are issued while stage st is multiplied
     Pk p0 = gload(0), p1 = gload(1);
     lstore(p0, 0);
@@ -648,8 +794,8 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
             for (int i = 0; i < 2; ++i) av[i] = *reinterpret_cast<const v4i*>(A + swz(64 * wr + 32 * i + rsub, c));
 #pragma unroll
             for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const v4i*>(B + swz(128 * wc + 32 * j + rsub, c));
-            *reinterpret_cast<v4i*>(wslot + swz(srow, 2 * kk)) = chunk(pk, 2 * kk);
-            *reinterpret_cast<v4i*>(wslot + swz(srow, 2 * kk + 1)) = chunk(pk, 2 * kk + 1);
+            *reinterpret_cast<v4i*>(wslot + poff(2 * kk)) = chunk(pk, 2 * kk);
+            *reinterpret_cast<v4i*>(wslot + poff(2 * kk + 1)) = chunk(pk, 2 * kk + 1);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -669,28 +815,58 @@ extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(
         step(p1, st);
         step(p0, st + 1);
     }
+    }   // kMode != 2
+    // fp64 epilogue.  The per-row (S, rsd) and per-column values of the tile go through LDS (the
+    // K loop's last barrier has passed: no wave reads the stages any more), so the element loop
+    // issues no global loads; rows outer, the four column tiles inner.
+    double* eRow = reinterpret_cast<double*>(hlds);   // [S | rsd] of the tile's 256 rows
+    double* eCol = eRow + 2 * kHT;                     // [S | rsd] of its 256 columns
+    {
+        const int k = tid & 255, idx = kHT * (sop ? tile.tj : tile.ti) + k;
+        double* e = sop ? eCol : eRow;
+        e[k] = idx < m ? S[row0 + idx] : 0.0;
+        e[kHT + k] = idx < m ? rsd[row0 + idx] : 0.0;
+    }
+    __syncthreads();
     if (idle) return;
-    const double scale = tau / n_ref_d;
+    const double scale = tau / n_ref_d, rn = 1.0 / n_ref_d;
+    double Sj[4], rj[4];
 #pragma unroll
     for (int sj = 0; sj < 4; ++sj) {
-        const int lj = kHT * tile.tj + 128 * wc + 32 * sj + (lane & 31);
-        if (lj >= m) continue;
-        const double Sj = S[row0 + lj], rj = rsd[row0 + lj];
+        const int cl = 128 * wc + 32 * sj + (lane & 31);
+        Sj[sj] = eCol[cl];
+        rj[sj] = eCol[kHT + cl];
+    }
 #pragma unroll
-        for (int si = 0; si < 2; ++si) {
-            if (!(act & (1u << (4 * si + sj)))) continue;
+    for (int si = 0; si < 2; ++si) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int li = kHT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (li >= m) continue;
-                const double c = static_cast<double>(acc[si][sj][r]) - S[row0 + li] * Sj / n_ref_d;
-                double v = scale * (c * rsd[row0 + li] * rj);
+        for (int r = 0; r < 16; ++r) {
+            const int rl = 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const int li = kHT * tile.ti + rl;
+            if (li >= m) continue;
+            const double Si = eRow[rl], ri = eRow[kHT + rl];
+#pragma unroll
+            for (int sj = 0; sj < 4; ++sj) {
+                const int lj = kHT * tile.tj + 128 * wc + 32 * sj + (lane & 31);
+                if (!(act & (1u << (4 * si + sj))) || lj >= m) continue;
+                const double c = centre(acc[si][sj][r], Si * Sj[sj], rn);
+                double v = scale * (c * ri * rj[sj]);
                 if (li == lj) v += 1.0 - tau;
                 for (int cp = copy_lo(m, tmin, tcopy); cp < copy_hi(m, tmin, tcopy, ncopy); ++cp)
                     M[moff + cp * cstride + static_cast<int64_t>(li) * ld + lj] = v;
             }
         }
     }
+}
+
+extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge(GRAM_HUGE_PARAMS) {
+    gram_huge_body<2>(GRAM_HUGE_ARGS);
+}
+extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge_quarter(GRAM_HUGE_PARAMS) {
+    gram_huge_body<1>(GRAM_HUGE_ARGS);
+}
+extern "C" __global__ __launch_bounds__(512) void dbslmm_gram_huge_rows(GRAM_HUGE_PARAMS) {
+    gram_huge_body<0>(GRAM_HUGE_ARGS);
 }
 
 // ------------------------------------------------------------------------------------------
