@@ -82,24 +82,28 @@ __device__ __forceinline__ v4i expand_dose(uint32_t w) {
 
 // The Gram kernels multiply on the FP4 matrix cores: dosages 0 / 1 / 2 (and the 0 / 1 masks of
 // the missing-call form) are exact e2m1 values, every product is exact and every partial sum an
-// integer below 4 n_ref < 2^24, so v_mfma_scale_f32_32x32x64_f8f6f4 with unit E8M0 scales gives
-// the integer Gram bit for bit -- at twice the MACs per clock of v_mfma_i32_32x32x32_i8, with half
-// its operand bytes.  A Gp dword (16 two-bit codes c) becomes two FP4 dwords with one shift and one
-// mask each: (w << 1) & 0x66666666 puts the even-numbered codes in the nibbles as e2m1 (c << 1 =
-// 0.0 / 1.0 / 2.0), (w >> 1) & 0x66666666 the odd ones (a fixed permutation of the individuals, the
-// same on both operands, so every product sums each individual once).
+// integer below 4 n_ref < 2^24, so v_mfma_scale_f32_32x32x64_f8f6f4 gives the integer Gram bit for
+// bit -- at twice the MACs per clock of v_mfma_i32_32x32x32_i8, with half its operand bytes.  A Gp
+// dword (16 two-bit codes c) becomes two FP4 dwords with one mask each and one shift per PAIR of
+// dwords: w & 0x33333333 leaves the even-numbered codes in bits 0-1 of the nibbles, which as e2m1
+// read 0.5 c (0.0 / 0.5 / 1.0); (w >> 2) & 0x33333333 the odd ones (one 64-bit shift serves both
+// dwords of a pair -- the bits shifted in from the high dword are masked off).  The E8M0 block
+// scales 2^1 on both operands restore c_a c_b exactly.  (A fixed permutation of the individuals,
+// the same on both operands, so every product sums each individual once.)
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
-constexpr int kE8M0One = 0x7F7F7F7F;       // E8M0 scale 2^0 in every byte
+constexpr int kE8M0Two = static_cast<int>(0x80808080u);   // E8M0 scale 2^1 in every byte
+constexpr uint32_t kFp4Mask = 0x33333333u;
 // 16 B of FP4 operand (32 individuals) from Gp dwords w0, w1
 __device__ __forceinline__ v4i fp4_chunk(uint32_t w0, uint32_t w1) {
-    return v4i{static_cast<int>((w0 << 1) & 0x66666666u), static_cast<int>((w0 >> 1) & 0x66666666u),
-               static_cast<int>((w1 << 1) & 0x66666666u), static_cast<int>((w1 >> 1) & 0x66666666u)};
+    const uint64_t t = ((static_cast<uint64_t>(w1) << 32) | w0) >> 2;
+    return v4i{static_cast<int>(w0 & kFp4Mask), static_cast<int>(static_cast<uint32_t>(t) & kFp4Mask),
+               static_cast<int>(w1 & kFp4Mask), static_cast<int>(static_cast<uint32_t>(t >> 32) & kFp4Mask)};
 }
 // C += A B^T over 64 individuals (32 per lane half), 32 x 32 tile
 __device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
     const v8i a8{a[0], a[1], a[2], a[3], 0, 0, 0, 0}, b8{b[0], b[1], b[2], b[3], 0, 0, 0, 0};
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, kE8M0Two, 0, kE8M0Two);
 }
 // centred Gram entry C_ij = G_ij - S_i S_j / n, as G - (S_i S_j) (1 / n) in one fma: S_i S_j is
 // an exact integer (below 2^53), the product with the rounded reciprocal replaces an fp64 divide
@@ -487,17 +491,14 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
 
 // ------------------------------------------------------------------------------------------
 // Kernel 2c: the Gram of the big blocks (m >= 384), 256 x 256 output tile per 512-thread
-// workgroup, on the FP4 matrix cores.  Dosages 0 / 1 / 2 are exact e2m1 values (0.0, 1.0, 2.0),
-// every product is exact and every partial sum an integer below 4 n_ref < 2^24, so
-// v_mfma_scale_f32_32x32x64_f8f6f4 (unit E8M0 scales) gives the integer Gram bit for bit -- at
-// twice the MACs per clock of v_mfma_i32_32x32x32_i8 and with half its operand bytes in LDS.
-// A Gp dword (16 two-bit codes) becomes two FP4 dwords with one shift and one mask each:
-// (w << 1) & 0x66666666 holds the even-numbered codes, (w >> 1) & 0x66666666 the odd ones (a
-// fixed permutation of the individuals, the same on both operands).  Every wave computes a
-// 64 x 128 piece (2 x 4 MFMA tiles, 128 accumulator registers); the two waves of a SIMD hold
-// pieces in opposite halves of the tile.  K runs in stages of 256 individuals: every thread loads
-// one row's 16 Gp dwords (64 B, two stages ahead in registers) and expands them to 128 B of FP4
-// codes in a double-buffered LDS stage, raw s_barrier per stage, 32 MFMAs per wave.  LDS rows are
+// workgroup, on the FP4 matrix cores (fp4_chunk / mfma_fp4 above: exact integer Gram).  Every
+// wave computes a 64 x 128 piece (2 x 4 MFMA tiles, 128 accumulator registers); the two waves of
+// a SIMD hold pieces in opposite halves of the tile.  K runs in stages of 256 individuals.  The
+// product kernel (kMode 2, gram_huge_dma_loop) moves each stage's raw 2-bit codes into LDS by
+// LDS-DMA and expands them after the operand reads.  The A/B variants (DBSLMM_GRAM_VARIANT): every
+// thread loads 64 B of Gp per stage (one row, or a quarter of four rows), two stages ahead in
+// registers, and expands them to 128 B of FP4 codes in a double-buffered LDS stage, raw s_barrier
+// per stage, 32 MFMAs per wave; LDS rows are
 // swizzled (swz) so that both the expansion writes and the operand reads are bank-conflict free.
 // Diagonal tiles stage one operand; MFMA tiles strictly above the diagonal or wholly past m (edge
 // tiles) are skipped.  Missing-call blocks: exact 4-product i8 path per 32 x 32 sub-tile.
@@ -527,6 +528,9 @@ __device__ __forceinline__ int swz(int r, int c) { return r * kHRow + 16 * (c ^ 
 // and expands each half (Gp dwords 0-1, 2-3) to one 16-B FP4 operand (fp4_chunk); A and B use the
 // same individual -> k map, so every product sums each individual once.  NOP = operands staged
 // (1: a diagonal tile, B = A); kFull: every MFMA tile of the wave's piece is active.
+#ifndef DBSLMM_GRAM_DIAG
+#define DBSLMM_GRAM_DIAG 0
+#endif
 template <int NOP, bool kFull>
 __device__ __forceinline__ void gram_huge_dma_loop(const uint32_t* __restrict__ Gp, int64_t kw,
                                                    const int64_t (&rbase)[2], const int (&svl)[2], int nst,
@@ -564,29 +568,52 @@ __device__ __forceinline__ void gram_huge_dma_loop(const uint32_t* __restrict__ 
     auto compute = [&](int st) {
         const int8_t* A = lds + (st & 3) * kSlotB;
         const int8_t* B = NOP == 1 ? A : A + kOpB;
+        v4i ar[2][2], br[2][4];
+        auto read = [&](int j) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            v4i ar[2], br[4];
+            for (int i = 0; i < 2; ++i) ar[j][i] = *reinterpret_cast<const v4i*>(A + roff(64 * wr + 32 * i + rsub, j));
 #pragma unroll
-            for (int i = 0; i < 2; ++i) ar[i] = *reinterpret_cast<const v4i*>(A + roff(64 * wr + 32 * i + rsub, j));
+            for (int jj = 0; jj < 4; ++jj) br[j][jj] = *reinterpret_cast<const v4i*>(B + roff(128 * wc + 32 * jj + rsub, j));
+        };
+        v4i av[2], bv[4];
+        auto expand = [&](int j, int e) {
+#if DBSLMM_GRAM_DIAG == 1   // diagnostic build only: raw codes as operands (wrong sums, no VALU)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) br[jj] = *reinterpret_cast<const v4i*>(B + roff(128 * wc + 32 * jj + rsub, j));
+            for (int i = 0; i < 2; ++i) av[i] = ar[j][i];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                v4i av[2], bv[4];
+            for (int jj = 0; jj < 4; ++jj) bv[jj] = br[j][jj];
+            return;
+#endif
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    av[i] = fp4_chunk(static_cast<uint32_t>(ar[i][2 * e]), static_cast<uint32_t>(ar[i][2 * e + 1]));
+            for (int i = 0; i < 2; ++i)
+                av[i] = fp4_chunk(static_cast<uint32_t>(ar[j][i][2 * e]), static_cast<uint32_t>(ar[j][i][2 * e + 1]));
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                bv[jj] = fp4_chunk(static_cast<uint32_t>(br[j][jj][2 * e]), static_cast<uint32_t>(br[j][jj][2 * e + 1]));
+        };
+        auto mult = [&]() {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
-                    bv[jj] = fp4_chunk(static_cast<uint32_t>(br[jj][2 * e]), static_cast<uint32_t>(br[jj][2 * e + 1]));
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj)
-                        if (kFull || (act & (1u << (4 * i + jj)))) acc[i][jj] = mfma_fp4(av[i], bv[jj], acc[i][jj]);
-            }
-        }
+                    if (kFull || (act & (1u << (4 * i + jj)))) acc[i][jj] = mfma_fp4(av[i], bv[jj], acc[i][jj]);
+        };
+        // k-steps 2 j + e: the reads of j = 1 are issued once k-step 0's operands are expanded, so
+        // they land under k-steps 0 and 1's MFMAs (sched_barrier pins that order)
+        read(0);
+        __builtin_amdgcn_sched_barrier(0);
+        expand(0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read(1);
+        __builtin_amdgcn_sched_barrier(0);
+        mult();
+        expand(0, 1);
+        mult();
+        __builtin_amdgcn_sched_barrier(0);
+        expand(1, 0);
+        mult();
+        expand(1, 1);
+        mult();
     };
     // vmcnt counts this wave's DMA instructions in issue order (2 NOP per stage)
     auto wait_stage = [&](int ahead) {   // ahead = stages issued after the one awaited
@@ -604,7 +631,9 @@ __device__ __forceinline__ void gram_huge_dma_loop(const uint32_t* __restrict__ 
     for (int st = 0; st < nst; ++st) {
         wait_stage(min(2, nst - 1 - st));
         __builtin_amdgcn_s_barrier();            // stage st is in LDS; slot (st + 3) & 3 is free
+#if DBSLMM_GRAM_DIAG != 2   // diagnostic build only: 2 = no operand DMA after the prologue
         if (st + 3 < nst) issue(st + 3);
+#endif
         compute(st);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
