@@ -633,10 +633,6 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) == hipSuccess &&
-            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge_rows),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) == hipSuccess &&
-            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge_quarter),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_region),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 static_cast<int>(kRegionLds)) == hipSuccess &&
@@ -1707,11 +1703,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             if (rc != DBSLMM_OK) return rc;
         }
     }
-    // A/B switch (diagnostic): DBSLMM_GRAM_VARIANT=0 rows, 1 quarter-row loads, default LDS-DMA
-    static const int gram_var = getenv("DBSLMM_GRAM_VARIANT") ? atoi(getenv("DBSLMM_GRAM_VARIANT")) : 2;
     auto gram_huge = [&](int32_t t0, int32_t nt) {
-        hipLaunchKernelGGL(gram_var == 0 ? dbslmm_gram_huge_rows : gram_var == 1 ? dbslmm_gram_huge_quarter
-                                                                                  : dbslmm_gram_huge, dim3(nt), dim3(512), gram::kHLdsBytes, s, p->d_G,
+        hipLaunchKernelGGL(dbslmm_gram_huge, dim3(nt), dim3(512), gram::kHLdsBytes, s, p->d_G,
                            p->kpad, p->d_htiles + t0, nt, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
