@@ -200,6 +200,18 @@ class Plan:
         self.ctx.check(self.ctx.lib.dbslmm_plan_shard_info(self.h, _ptr(out)), "plan_shard_info")
         return out
 
+    def block_matrix(self, block: int, copy: int = 0) -> np.ndarray:
+        """Diagnostics (dbslmm_plan_block_matrix): block `block`'s ld x ld working matrix of
+        factorisation copy `copy` after the last run -- Sigma after a debug_stop = 1 run, the
+        factor (strict lower L, row m = L^-1 z) after a full run of a tiled block."""
+        ld = C.c_int32()
+        self.ctx.check(self.ctx.lib.dbslmm_plan_block_matrix(self.h, int(block), int(copy), None,
+                                                             C.byref(ld)), "plan_block_matrix")
+        out = np.empty((ld.value, ld.value))
+        self.ctx.check(self.ctx.lib.dbslmm_plan_block_matrix(self.h, int(block), int(copy), _ptr(out),
+                                                             None), "plan_block_matrix")
+        return out
+
     def download(self):
         p = self.prob
         bs = np.zeros(p.n_s)

@@ -19,10 +19,10 @@ EXPORTS = (
     "dbslmm_plan_enable_timing", "dbslmm_plan_kernel_ms", "dbslmm_plan_workload",
     "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
     "dbslmm_ctx_create_multi", "dbslmm_ctx_num_devices", "dbslmm_plan_shard_info",
-    "dbslmm_ctx_cache_bed", "dbslmm_ctx_cache_bed_fd",
+    "dbslmm_ctx_cache_bed", "dbslmm_ctx_cache_bed_fd", "dbslmm_plan_block_matrix",
 )
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv")
@@ -35,6 +35,8 @@ class Options(C.Structure):
     _fields_ = [
         ("tiled_min", C.c_int32), ("gram_big_min", C.c_int32), ("gram_huge_min", C.c_int32),
         ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double), ("lead_min", C.c_int32),
+        ("large_cheb", C.c_int32), ("cheb_fused", C.c_int32), ("debug_delay_us", C.c_int32),
+        ("debug_stop", C.c_int32),
     ]
 
 
@@ -100,6 +102,8 @@ def load(path: str | None = None):
     L.dbslmm_plan_variance.argtypes = [V, P(TestPanel), V, V]
     L.dbslmm_ctx_cache_bed.argtypes = [V, V, C.c_int64]
     L.dbslmm_ctx_cache_bed_fd.argtypes = [V, C.c_int, C.c_int64, V]
+    if hasattr(L, "dbslmm_plan_block_matrix"):   # (tools/race_probe.py loads older builds for A/B)
+        L.dbslmm_plan_block_matrix.argtypes = [V, C.c_int32, C.c_int32, V, V]
     if L.dbslmm_abi_version() != ABI_VERSION:
         raise DbslmmError("ABI version mismatch")
     _lib = L

@@ -815,6 +815,14 @@ extern "C" __global__ void dbslmm_valid_reduce(const double* __restrict__ partia
 // one device scalar, in stream order (the solve kernels read sigma's shift from it)
 extern "C" __global__ void dbslmm_set_scalar(double* __restrict__ dst, double v) { *dst = v; }
 
+// testing only (dbslmm_options.debug_delay_us): one wave that holds its stream for `ticks` of the
+// 100 MHz real-time counter, so work queued behind it on that stream starts late and any
+// dependency another stream is missing on it shows up deterministically
+extern "C" __global__ void dbslmm_debug_spin(int64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (static_cast<int64_t>(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
 // ------------------------------------------------------------------------------------------
 // readSNPIm + nomalizeVec for a list of rows in ORIGINAL individual order (diagnostics and
 // parity): out[j * n_ref + i] = (g_ij - mu_j) * rsd_j with missing calls at the mean (0).

@@ -175,6 +175,8 @@ struct dbslmm_plan {
     std::vector<int32_t> h_m;   // per non-empty block
     std::vector<int32_t> h_tb;  // blocks on the tiled path
     std::vector<int32_t> h_empty;  // original ids of empty blocks
+    std::vector<int32_t> h_blk_id; // per non-empty block: its original id
+    std::vector<int64_t> h_matoff; // per non-empty block: offset of its matrix in a copy
     void* h_pin = nullptr;         // pinned landing buffer of the result downloads
     size_t h_pin_bytes = 0;
     std::vector<int32_t> h_slot_out;  // slot -> small index s, large -1-l, padding INT32_MIN
@@ -199,6 +201,11 @@ struct dbslmm_plan {
     int32_t tiled_min = 0;                   // blocks with m >= this are on the tiled path
     int32_t h2f_mode = 0;                    // dbslmm_options.h2f_mode
     double cheb_tol = 1e-9;                  // dbslmm_options.cheb_tol
+    bool large_cheb_ok = true;               // dbslmm_options.large_cheb and every chol_large block
+                                             // fits dbslmm_chol_cheb (ld <= chol::kChebMaxM)
+    bool cheb_fused = false;                 // dbslmm_options.cheb_fused
+    int32_t debug_delay_us = 0;              // dbslmm_options.debug_delay_us (tests)
+    int32_t debug_stop = 0;                  // dbslmm_options.debug_stop (tests)
     bool trsv_pending = false;               // a persistent substitution ran since the last error check
     bool trsv_failed = false;                // ... and one of its hand-off waits gave up (sticky until the next run)
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (DBSLMM_DIAG) only
@@ -329,7 +336,11 @@ static hipError_t upload_pipelined(void* dst, size_t n, hipStream_t st, Fill fil
 }
 
 static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_t st) {
-    if (n <= (size_t(128) << 20)) return hipMemcpy(dst, src, n, hipMemcpyHostToDevice);
+    if (n <= (size_t(128) << 20)) {   // (stream-ordered: a pageable hipMemcpy may return before its
+                                      // DMA lands, ordered only on the null stream)
+        const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+        return e != hipSuccess ? e : hipStreamSynchronize(st);
+    }
     return upload_pipelined(dst, n, st, [src](char* d, size_t off, size_t len) {
         memcpy(d, static_cast<const char*>(src) + off, len);
         return true;
@@ -381,13 +392,17 @@ static hipError_t bed_to_device(dbslmm_ctx* ctx, uint8_t* dst, const uint8_t* be
     return e != hipSuccess ? e : upload_staged(dst, bed, bed_len, ctx->stream);
 }
 
+// Allocate and fill a device array on stream st; complete on return.  Every host -> device copy
+// of the library is ordered on the stream its consumers run on (or one they are forked from):
+// null-stream transfers are not ordered against the contexts' non-blocking streams, and a pageable
+// hipMemcpy may return before its DMA has landed.
 template <typename T>
-static hipError_t dev_upload(T** dst, const std::vector<T>& src) {
+static hipError_t dev_upload(T** dst, const std::vector<T>& src, hipStream_t st) {
     size_t bytes = std::max<size_t>(sizeof(T), src.size() * sizeof(T));
     hipError_t e = hipMalloc(reinterpret_cast<void**>(dst), bytes);
-    if (e != hipSuccess) return e;
-    if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
-    return e;
+    if (e != hipSuccess || src.empty()) return e;
+    e = hipMemcpyAsync(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice, st);
+    return e != hipSuccess ? e : hipStreamSynchronize(st);
 }
 
 // Launch list of the tiled sequence for the blocks `tb0` (plan block indices), each replicated over
@@ -695,7 +710,7 @@ int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len) {
         (void)hipSetDevice(dev);
         (void)hipFree(q);
     });
-    HIP_TRY(ctx, hipMemset(d + bed_len, 0, 16));
+    HIP_TRY(ctx, hipMemsetAsync(d + bed_len, 0, 16, ctx->stream));
     HIP_TRY(ctx, upload_staged(d, bed, bed_len, ctx->stream));
     ctx->d_bed_cache = d;
     ctx->bed_host = bed;
@@ -719,7 +734,7 @@ int dbslmm_ctx_cache_bed_fd(dbslmm_ctx* ctx, int fd, int64_t bed_len, const uint
         (void)hipSetDevice(dev);
         (void)hipFree(q);
     });
-    HIP_TRY(ctx, hipMemset(d + bed_len, 0, 16));
+    HIP_TRY(ctx, hipMemsetAsync(d + bed_len, 0, 16, ctx->stream));
     if (upload_staged_fd(d, fd, static_cast<size_t>(bed_len), ctx->stream) != hipSuccess) {
         ctx->bed_cache.reset();
         ctx->err = "reading / uploading the .bed from its file descriptor failed";
@@ -792,8 +807,14 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->bed_len = pr->bed_len;
     const dbslmm_options op = pr->opts ? *pr->opts : dbslmm_options{};
     ARG_CHECK(ctx, op.tiled_min >= 0 && op.gram_big_min >= 0 && op.gram_huge_min >= 0 &&
-                   (op.h2f_mode == 0 || op.h2f_mode == 1) && op.cheb_tol >= 0.0, "bad dbslmm_options");
+                   (op.h2f_mode == 0 || op.h2f_mode == 1) && op.cheb_tol >= 0.0 &&
+                   (op.large_cheb == 0 || op.large_cheb == -1) && (op.cheb_fused == 0 || op.cheb_fused == 1) &&
+                   op.debug_delay_us >= -100000 && op.debug_delay_us <= 100000 &&
+                   (op.debug_stop == 0 || op.debug_stop == 1), "bad dbslmm_options");
     p->h2f_mode = op.h2f_mode;
+    p->cheb_fused = op.cheb_fused == 1;
+    p->debug_delay_us = op.debug_delay_us;
+    p->debug_stop = op.debug_stop;
     if (op.cheb_tol > 0.0) p->cheb_tol = std::max(1e-16, op.cheb_tol);
     p->n_s = pr->s_ptr[pr->num_block];
     p->n_l = has_l ? pr->l_ptr[pr->num_block] : 0;
@@ -974,6 +995,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     p->n_htiles = static_cast<int32_t>(htiles.size());
     p->M_elems = moff;
     p->h_ld = ldv;
+    p->h_blk_id = blk_id;
+    p->h_matoff = matoff;
     // Cholesky work lists: large blocks (ld > 64, one workgroup each) then small blocks (one
     // wave each), each largest first (longest-processing-time order)
     std::vector<int32_t> order(p->n_nonempty);
@@ -981,7 +1004,15 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return mv[a] > mv[c]; });
     order.erase(std::remove_if(order.begin(), order.end(), [&](int b) { return is_tiled[b] != 0; }),
                 order.end());
-    for (int32_t b : order) (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
+    int32_t large_ld_max = 0;
+    for (int32_t b : order) {
+        (ldv[b] > chol::kSmallLd ? p->n_large : p->n_small)++;
+        if (ldv[b] > chol::kSmallLd) large_ld_max = std::max(large_ld_max, ldv[b]);
+    }
+    // dbslmm_chol_cheb holds a block's vectors in LDS for ld <= kChebMaxM (the default tiled_min
+    // guarantees it; a larger tiled_min leaves bigger blocks on chol_large, whose h2f copies are
+    // then all factored)
+    p->large_cheb_ok = op.large_cheb == 0 && large_ld_max <= chol::kChebMaxM;
     std::vector<int32_t> tlist;
     {
         std::vector<int32_t> tb, tb_lead, tb_rest;
@@ -1095,32 +1126,35 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     // + kHT spare rows: a 256-row Gram tile may read past the last slot (results discarded)
     const int64_t g_bytes = static_cast<int64_t>(p->n_slots + gram::kHT) * (p->kpad / 4);
     if ((e = hipMalloc(&p->d_G, g_bytes)) != hipSuccess) return fail("hipMalloc G");
-    if ((e = hipMemset(p->d_G, 0, g_bytes)) != hipSuccess) return fail("hipMemset G");
-    if ((e = dev_upload(&p->d_slot_pos, slot_pos)) != hipSuccess) return fail("upload slots");
-    if ((e = dev_upload(&p->d_slot_block, slot_block)) != hipSuccess) return fail("upload slots");
-    if ((e = dev_upload(&p->d_slot_out, slot_out)) != hipSuccess) return fail("upload slots");
-    if ((e = dev_upload(&p->d_z, z)) != hipSuccess) return fail("upload z");
-    if ((e = dev_upload(&p->d_row0, row0)) != hipSuccess) return fail("upload blocks");
-    if ((e = dev_upload(&p->d_m, mv)) != hipSuccess) return fail("upload blocks");
-    if ((e = dev_upload(&p->d_ms, msv)) != hipSuccess) return fail("upload blocks");
-    if ((e = dev_upload(&p->d_ld, ldv)) != hipSuccess) return fail("upload blocks");
-    if ((e = dev_upload(&p->d_matoff, matoff)) != hipSuccess) return fail("upload blocks");
-    if ((e = dev_upload(&p->d_blk_id, blk_id)) != hipSuccess) return fail("upload blocks");
-    if ((e = dev_upload(&p->d_order, order)) != hipSuccess) return fail("upload order");
-    if ((e = dev_upload(&p->d_tiles, tiles)) != hipSuccess) return fail("upload tiles");
-    if ((e = dev_upload(&p->d_btiles, btiles)) != hipSuccess) return fail("upload tiles");
-    if ((e = dev_upload(&p->d_htiles, htiles)) != hipSuccess) return fail("upload tiles");
-    if ((e = dev_upload(&p->d_tlist, tlist)) != hipSuccess) return fail("upload tiled lists");
-    if ((e = dev_upload(&p->d_tri_f, tri_f)) != hipSuccess) return fail("upload trsv lists");
-    if ((e = dev_upload(&p->d_tri_b, tri_b)) != hipSuccess) return fail("upload trsv lists");
-    if ((e = dev_upload(&p->d_foff, foff)) != hipSuccess) return fail("upload trsv lists");
-    if ((e = dev_upload(&p->d_tb, p->h_tb)) != hipSuccess) return fail("upload trsv lists");
-    if (!slot_order.empty() && (e = dev_upload(&p->d_slot_order, slot_order)) != hipSuccess) return fail("upload slot order");
+    // (every memset of the plan's buffers is ordered on the main stream, which every run starts
+    // on: a null-stream hipMemset is not ordered against the context's non-blocking streams, and
+    // one still running under the first run's Gram would zero matrix entries behind it)
+    if ((e = hipMemsetAsync(p->d_G, 0, g_bytes, ctx->stream)) != hipSuccess) return fail("hipMemset G");
+    if ((e = dev_upload(&p->d_slot_pos, slot_pos, ctx->stream)) != hipSuccess) return fail("upload slots");
+    if ((e = dev_upload(&p->d_slot_block, slot_block, ctx->stream)) != hipSuccess) return fail("upload slots");
+    if ((e = dev_upload(&p->d_slot_out, slot_out, ctx->stream)) != hipSuccess) return fail("upload slots");
+    if ((e = dev_upload(&p->d_z, z, ctx->stream)) != hipSuccess) return fail("upload z");
+    if ((e = dev_upload(&p->d_row0, row0, ctx->stream)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_m, mv, ctx->stream)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_ms, msv, ctx->stream)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_ld, ldv, ctx->stream)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_matoff, matoff, ctx->stream)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_blk_id, blk_id, ctx->stream)) != hipSuccess) return fail("upload blocks");
+    if ((e = dev_upload(&p->d_order, order, ctx->stream)) != hipSuccess) return fail("upload order");
+    if ((e = dev_upload(&p->d_tiles, tiles, ctx->stream)) != hipSuccess) return fail("upload tiles");
+    if ((e = dev_upload(&p->d_btiles, btiles, ctx->stream)) != hipSuccess) return fail("upload tiles");
+    if ((e = dev_upload(&p->d_htiles, htiles, ctx->stream)) != hipSuccess) return fail("upload tiles");
+    if ((e = dev_upload(&p->d_tlist, tlist, ctx->stream)) != hipSuccess) return fail("upload tiled lists");
+    if ((e = dev_upload(&p->d_tri_f, tri_f, ctx->stream)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = dev_upload(&p->d_tri_b, tri_b, ctx->stream)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = dev_upload(&p->d_foff, foff, ctx->stream)) != hipSuccess) return fail("upload trsv lists");
+    if ((e = dev_upload(&p->d_tb, p->h_tb, ctx->stream)) != hipSuccess) return fail("upload trsv lists");
+    if (!slot_order.empty() && (e = dev_upload(&p->d_slot_order, slot_order, ctx->stream)) != hipSuccess) return fail("upload slot order");
     // [tile flags | ticket counter | error word | spare]
     if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
-    if ((e = hipMemset(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
+    if ((e = hipMemsetAsync(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t), ctx->stream)) != hipSuccess) return fail("hipMemset trsv flags");
     if ((e = hipMalloc(&p->d_tepi, std::max(1, p->n_tflags) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
-    if ((e = hipMemset(p->d_tepi, 0, std::max(1, p->n_tflags) * sizeof(int32_t))) != hipSuccess) return fail("hipMemset trsv flags");
+    if ((e = hipMemsetAsync(p->d_tepi, 0, std::max(1, p->n_tflags) * sizeof(int32_t), ctx->stream)) != hipSuccess) return fail("hipMemset trsv flags");
     const size_t ns = std::max<size_t>(1, p->n_slots);
     if ((e = hipMalloc(&p->d_S, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
     if ((e = hipMalloc(&p->d_mu, ns * sizeof(double))) != hipSuccess) return fail("hipMalloc stats");
@@ -1131,10 +1165,11 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = hipMalloc(&p->d_flags, nbk * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc flags");
     if ((e = hipMalloc(&p->d_status, nbk * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc status");
     if ((e = hipMalloc(&p->d_M, std::max<int64_t>(1, p->M_elems) * sizeof(double))) != hipSuccess) return fail("hipMalloc M");
-    if ((e = hipMemset(p->d_M, 0, std::max<int64_t>(1, p->M_elems) * sizeof(double))) != hipSuccess) return fail("hipMemset M");
+    if ((e = hipMemsetAsync(p->d_M, 0, std::max<int64_t>(1, p->M_elems) * sizeof(double), ctx->stream)) != hipSuccess) return fail("hipMemset M");
     if ((e = hipMalloc(&p->d_beta_s, std::max<int64_t>(1, p->n_s) * sizeof(double))) != hipSuccess) return fail("hipMalloc beta");
     if ((e = hipMalloc(&p->d_beta_l, std::max<int64_t>(1, p->n_l) * sizeof(double))) != hipSuccess) return fail("hipMalloc beta");
     if ((e = hipMalloc(&p->d_dshift, sizeof(double))) != hipSuccess) return fail("hipMalloc dshift");
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail("plan set-up");
     *out = p;
     return DBSLMM_OK;
 }
@@ -1188,6 +1223,16 @@ struct TSeq {
 static TSeq seq_main(dbslmm_plan* p) { return TSeq{p->ctx->stream2, p->ctx->stream3, &p->tev}; }
 static TSeq seq_rest(dbslmm_plan* p) { return TSeq{p->ctx->stream4, p->ctx->stream5, &p->tev_rest}; }
 
+// dbslmm_options.debug_delay_us (tests): a spin kernel at the head of a stream segment.  side > 0:
+// the concurrent side (bulk trailing launches, the rest sequence, the main stream after the lead
+// fork) runs late; side < 0: the critical side (chain launches, the lead sequence).
+static void debug_spin(const dbslmm_plan* p, hipStream_t st, int side) {
+    const int32_t d = p->debug_delay_us;
+    if (d == 0 || (d > 0) != (side > 0)) return;
+    const int64_t ticks = 100 * static_cast<int64_t>(d > 0 ? d : -d);   // 100 MHz counter
+    hipLaunchKernelGGL(dbslmm_debug_spin, dim3(1), dim3(64), 0, st, ticks);
+}
+
 // Enqueue a tiled launch list on its stream pair.
 // copy: the list is a single-copy list applied to factorisation copy `copy` (its matrix, sigma
 // scalar, scratch, betas and status); multi-copy lists address the copies themselves (copy 0).
@@ -1216,6 +1261,7 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
         if (L.items == 0) continue;
         const int32_t* act = d_tlist + L.off;
         const dim3 g(static_cast<unsigned>(L.items)), blk(chol::kLargeThreads);
+        if (p->debug_delay_us) debug_spin(p, st, L.strm ? 1 : -1);
         switch (L.kind) {
         case 4: hipLaunchKernelGGL(dbslmm_tchol_region, g, blk, kRegionLds, st, ta, act, L.items); break;
         case 1: hipLaunchKernelGGL(dbslmm_tchol_panel, g, blk, kTiledLds, st, ta, act, L.items); break;
@@ -1239,12 +1285,13 @@ static int ensure_copies(dbslmm_plan* p, int n) {
     p->d_status = nullptr;
     const size_t nn = static_cast<size_t>(n);
     HIP_TRY(ctx, hipMalloc(&p->d_M, std::max<size_t>(1, nn * p->M_elems) * sizeof(double)));
-    HIP_TRY(ctx, hipMemset(p->d_M, 0, std::max<size_t>(1, nn * p->M_elems) * sizeof(double)));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_M, 0, std::max<size_t>(1, nn * p->M_elems) * sizeof(double), ctx->stream));
     HIP_TRY(ctx, hipMalloc(&p->d_dshift, nn * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_y, nn * std::max<int64_t>(1, p->n_slots) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_beta_s, nn * std::max<int64_t>(1, p->n_s) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_beta_l, nn * std::max<int64_t>(1, p->n_l) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_status, nn * p->nbk * sizeof(int32_t)));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     p->n_copies = n;
     // captured graphs hold the old pointers
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
@@ -1318,6 +1365,7 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     a.mode = 1;
     if (++p->trsv_epoch == INT32_MAX) {
         HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
+        HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), st));
         p->trsv_epoch = 1;
     }
     a.epoch = p->trsv_epoch;
@@ -1464,7 +1512,8 @@ static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
         HIP_TRY(ctx, hipMalloc(&p->d_coef, cp.coef.size() * sizeof(double)));
         p->coef_cap = static_cast<int32_t>(cp.coef.size());
     }
-    HIP_TRY(ctx, hipMemcpy(p->d_coef, cp.coef.data(), cp.coef.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpyAsync(p->d_coef, cp.coef.data(), cp.coef.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx, hipStreamSynchronize(st));
     p->h_coef = cp.coef;
     return DBSLMM_OK;
 }
@@ -1507,8 +1556,8 @@ static void build_cheb_items(const dbslmm_plan* p, int K, std::vector<int32_t>& 
     }
 }
 
-// Passes: one launch per forward / backward pass (default), or, with DBSLMM_CHEB_FUSED=1 in the
-// environment (experimental: measured slower at config 4, 15.9 vs 13.9 ms -- every pass there is
+// Passes: one launch per forward / backward pass (default), or, with dbslmm_options.cheb_fused = 1
+// (experimental: measured slower at config 4, 15.9 vs 13.9 ms -- every pass there is
 // bound by the largest block's 150-tile chain and by the streaming bandwidth alike, and the fused
 // items' own-input waits and update hand-offs cost more than the launch boundaries they remove),
 // all 2K passes of a group in one dbslmm_trsv_cheb launch over the whole plan (grp = tgroup_all).
@@ -1516,8 +1565,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
     dbslmm_ctx* ctx = p->ctx;
     hipStream_t st = grp.st;
     if (grp.n_items == 0) return DBSLMM_OK;
-    const char* fenv = getenv("DBSLMM_CHEB_FUSED");
-    const bool fused = fenv && fenv[0] == '1' && grp.item_off == 0 && grp.n_items == p->n_titems;
+    const bool fused = p->cheb_fused && grp.item_off == 0 && grp.n_items == p->n_titems;
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
     const int64_t blk = trsv::kMaxR * vs;
     double *Y = p->d_cheb, *Z = Y + blk, *X = Z + blk, *R = X + blk, *D = R + blk, *S = D + blk;
@@ -1535,7 +1583,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
             HIP_TRY(ctx, hipStreamSynchronize(st));
             if (p->d_cheb_items) (void)hipFree(p->d_cheb_items);
             p->d_cheb_items = nullptr;
-            HIP_TRY(ctx, dev_upload(&p->d_cheb_items, items));
+            HIP_TRY(ctx, dev_upload(&p->d_cheb_items, items, ctx->stream));
             p->n_cheb_items = static_cast<int32_t>(items.size() / 2);
             p->cheb_items_K = K;
         }
@@ -1591,6 +1639,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
                     const bool fwd = pass == 0;
                     if (++p->trsv_epoch == INT32_MAX) {   // flags restart from a clean slate
                         HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
+                        HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), st));
                         p->trsv_epoch = 1;
                     }
                     a.epoch = p->trsv_epoch;
@@ -1642,7 +1691,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             build_tiled(p->h_m, p->h_tb, n, p->n_nonempty, p->tl_multi, tlist);
             if (p->d_tlist_multi) (void)hipFree(p->d_tlist_multi);
             p->d_tlist_multi = nullptr;
-            HIP_TRY(ctx, dev_upload(&p->d_tlist_multi, tlist));
+            HIP_TRY(ctx, dev_upload(&p->d_tlist_multi, tlist, ctx->stream));
             if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
             p->graph_multi = nullptr;
             p->multi_n = n;
@@ -1655,8 +1704,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     const int32_t tcopy = cheb ? cp.base : -1;   // Gram epilogues: iterated blocks write this copy only
     // ... the blocks with m >= tmin_copy: the tiled ones and the single-workgroup ones (ld > 64),
     // whose other h2f copies iterate on the base factor too (dbslmm_chol_cheb)
-    const char* lenv = getenv("DBSLMM_LARGE_CHEB");   // A/B switch: 0 = factor every copy
-    const bool large_cheb = cheb && !(lenv && lenv[0] == '0');
+    const bool large_cheb = cheb && p->large_cheb_ok;
     const int32_t tmin_copy = large_cheb ? chol::kSmallLd : p->tiled_min;
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
@@ -1723,7 +1771,10 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     // the lead sequence (stream2, high priority: the critical path) waits for this point of the
     // main stream; its graph is launched after every main-stream kernel is enqueued (a graph
     // launch of a few hundred nodes keeps the host busy for milliseconds)
-    if (lead) HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
+    if (lead) {
+        HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
+        debug_spin(p, s, 1);
+    }
     if (split_unpack) {   // the other slots
         unpack(p->d_slot_order + p->n_slots_lead, p->n_slots - p->n_slots_lead);
         HIP_TRY(ctx, hipGetLastError());
@@ -1763,6 +1814,12 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     }
     // (the factorisation overwrites its matrix: the Gram epilogues write all n copies)
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
+    if (p->debug_stop == 1) {   // tests: the block matrices hold Sigma (dbslmm_plan_block_matrix)
+        for (int k : {3, 4, 5, 6, 8, 7})
+            if (ev) HIP_TRY(ctx, hipEventRecord(ev[k], s));
+        p->ran = true;
+        return DBSLMM_OK;
+    }
     if (p->n_nonempty > 0) {
         // fork: the tiled sequence (or, with a lead group, the rest sequence on stream4) runs
         // beside the single-workgroup and single-wave kernels of the main stream
@@ -1819,6 +1876,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         if (lead) {
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
             if (ev) HIP_TRY(ctx, hipEventRecord(ev[6], ctx->stream2));
+            debug_spin(p, ctx->stream2, -1);
+            debug_spin(p, ctx->stream4, 1);
             int rc = run_tiled_copy(p, isn, fcopy);
             if (rc == DBSLMM_OK) rc = run_rest_copy(p, isn, fcopy);
             if (rc != DBSLMM_OK) return rc;
@@ -1888,7 +1947,10 @@ static int check_trsv(dbslmm_plan* p) {
         std::lock_guard<std::mutex> lk(g_capture_mu);   // synchronous copy / memset below
         int32_t werr = 0;
         HIP_TRY(ctx, hipMemcpy(&werr, p->d_tflags + p->n_tflags + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
-        if (werr) HIP_TRY(ctx, hipMemset(p->d_tflags + p->n_tflags + 1, 0, sizeof(int32_t)));
+        if (werr) {
+            HIP_TRY(ctx, hipMemsetAsync(p->d_tflags + p->n_tflags + 1, 0, sizeof(int32_t), ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
         p->trsv_pending = false;
         p->trsv_failed = p->trsv_failed || werr != 0;
     }
@@ -2051,6 +2113,35 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     return DBSLMM_OK;
 }
 
+int dbslmm_plan_block_matrix(dbslmm_plan* p, int32_t block, int32_t copy, double* out, int32_t* ld_out) {
+    if (!p) return DBSLMM_E_ARG;
+    dbslmm_ctx* ctx = p->ctx;
+    ARG_CHECK(ctx, block >= 0 && block < p->num_block, "block out of range");
+    if (p->mp) {   // the shard that solves the block (sub-plan block id = its position in the shard)
+        for (auto& sh : p->mp->shards)
+            for (size_t j = 0; j < sh.blocks.size(); ++j)
+                if (sh.blocks[j] == block) {
+                    const int rc = dbslmm_plan_block_matrix(sh.plan, static_cast<int32_t>(j), copy, out, ld_out);
+                    if (rc != DBSLMM_OK) ctx->err = sh.plan->ctx->err;
+                    return rc;
+                }
+        ARG_CHECK(ctx, false, "block has no SNPs");
+    }
+    ARG_CHECK(ctx, copy >= 0 && copy < p->n_copies, "copy out of range");
+    const auto it = std::find(p->h_blk_id.begin(), p->h_blk_id.end(), block);
+    ARG_CHECK(ctx, it != p->h_blk_id.end(), "block has no SNPs");
+    const size_t nb = static_cast<size_t>(it - p->h_blk_id.begin());
+    const int64_t ld = p->h_ld[nb];
+    if (ld_out) *ld_out = static_cast<int32_t>(ld);
+    if (!out) return DBSLMM_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::lock_guard<std::mutex> lk(g_capture_mu);   // device-wide sync + synchronous copy
+    HIP_TRY(ctx, hipDeviceSynchronize());
+    HIP_TRY(ctx, hipMemcpy(out, p->d_M + static_cast<int64_t>(copy) * p->M_elems + p->h_matoff[nb],
+                           ld * ld * sizeof(double), hipMemcpyDeviceToHost));
+    return DBSLMM_OK;
+}
+
 int dbslmm_plan_download(dbslmm_plan* p, double* beta_s, double* beta_l, int32_t* block_status) {
     if (!p) return DBSLMM_E_ARG;
     if (p->mp) {
@@ -2134,12 +2225,12 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     do {
         hipError_t e;
         if ((e = hipMalloc(&d_tbed, tp->bed_len + 16)) != hipSuccess ||
-            (e = hipMemset(d_tbed, 0, tp->bed_len + 16)) != hipSuccess ||
-            (e = hipMemcpy(d_tbed, tp->bed, tp->bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
-            (e = dev_upload(&d_tpos, tpos)) != hipSuccess || (e = dev_upload(&d_sel, sel)) != hipSuccess ||
-            (e = dev_upload(&d_cpos, cpos)) != hipSuccess ||
+            (e = hipMemsetAsync(d_tbed, 0, tp->bed_len + 16, st)) != hipSuccess ||
+            (e = upload_staged(d_tbed, tp->bed, tp->bed_len, st)) != hipSuccess ||
+            (e = dev_upload(&d_tpos, tpos, ctx->stream)) != hipSuccess || (e = dev_upload(&d_sel, sel, ctx->stream)) != hipSuccess ||
+            (e = dev_upload(&d_cpos, cpos, ctx->stream)) != hipSuccess ||
             (e = hipMalloc(&d_cbed, cbytes)) != hipSuccess ||
-            (e = hipMemset(d_cbed, 0, cbytes)) != hipSuccess ||
+            (e = hipMemsetAsync(d_cbed, 0, cbytes, st)) != hipSuccess ||
             (e = hipMalloc(&d_mu, std::max<int32_t>(1, p->n_slots) * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_rsd, std::max<int32_t>(1, p->n_slots) * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_Y, std::max<int64_t>(1, p->n_slots) * nt_pad * sizeof(double))) != hipSuccess ||
@@ -2194,7 +2285,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
         const bool cached = ctx->d_bed_cache && bed == ctx->bed_host && bed_len == ctx->bed_host_len;
         if ((!cached && ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
                          (e = bed_to_device(ctx, d_bed, bed, bed_len)) != hipSuccess)) ||
-            (e = dev_upload(&d_pos, pos)) != hipSuccess ||
+            (e = dev_upload(&d_pos, pos, ctx->stream)) != hipSuccess ||
             (e = hipMalloc(&d_mu, n_snp * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_maf, n_snp * sizeof(double))) != hipSuccess) {
             ctx->err = std::string("bed_maf alloc/upload: ") + hipGetErrorString(e);
@@ -2242,9 +2333,9 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
     do {
         hipError_t e;
         if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
-            (e = hipMemset(d_bed, 0, bed_len + 16)) != hipSuccess ||
-            (e = hipMemcpy(d_bed, bed, bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
-            (e = dev_upload(&d_pos, hp)) != hipSuccess ||
+            (e = hipMemsetAsync(d_bed, 0, bed_len + 16, ctx->stream)) != hipSuccess ||
+            (e = upload_staged(d_bed, bed, bed_len, ctx->stream)) != hipSuccess ||
+            (e = dev_upload(&d_pos, hp, ctx->stream)) != hipSuccess ||
             (e = hipMalloc(&d_mu, n_rows * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_rsd, n_rows * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_maf, n_rows * sizeof(double))) != hipSuccess ||
@@ -2314,10 +2405,10 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
     do {
         hipError_t e;
         if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
-            (e = hipMemset(d_bed, 0, bed_len + 16)) != hipSuccess ||
-            (e = hipMemcpy(d_bed, bed, bed_len, hipMemcpyHostToDevice)) != hipSuccess ||
-            (e = dev_upload(&d_pos, hp)) != hipSuccess || (e = dev_upload(&d_ptr, hptr)) != hipSuccess ||
-            (e = dev_upload(&d_z1, hz)) != hipSuccess ||
+            (e = hipMemsetAsync(d_bed, 0, bed_len + 16, ctx->stream)) != hipSuccess ||
+            (e = upload_staged(d_bed, bed, bed_len, ctx->stream)) != hipSuccess ||
+            (e = dev_upload(&d_pos, hp, ctx->stream)) != hipSuccess || (e = dev_upload(&d_ptr, hptr, ctx->stream)) != hipSuccess ||
+            (e = dev_upload(&d_z1, hz, ctx->stream)) != hipSuccess ||
             (e = hipMalloc(&d_mu, nr * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_rsd, nr * sizeof(double))) != hipSuccess ||
             (e = hipMalloc(&d_part, static_cast<size_t>(num_block) * n_chunks * sizeof(double))) != hipSuccess ||

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 8
+#define DBSLMM_ABI_VERSION 9
 
 enum {
     DBSLMM_OK = 0,
@@ -75,6 +75,18 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                group, and the tiled sequence starts after the whole Gram instead of right
  *                after the tiled blocks' Gram tiles).  Scheduling only: the results are
  *                bit-identical either way.
+ * large_cheb     plan_run_multi with Chebyshev h2f: the single-workgroup blocks (64 <= m+1, m
+ *                below tiled_min) iterate on the base copy's factor too (0 = on when every such
+ *                block fits the iteration kernel, ld <= 512; -1 = off: every copy factored)
+ * cheb_fused     1 = all Chebyshev passes of a copy group in one persistent launch (experimental,
+ *                bit-identical, slower at config 4); 0 = one launch per pass
+ * debug_delay_us testing only: a spin kernel of this many microseconds at the head of every
+ *                concurrently running stream segment (the bulk trailing launches of each tiled
+ *                sequence, the rest sequence, the main stream after the lead fork, the lead
+ *                sequence), so a missing cross-stream dependency fails deterministically
+ *                instead of by timing.  Results must be bit-identical to a run without it.
+ * debug_stop     testing only: 1 = stop every run after the Gram (the block matrices then hold
+ *                Sigma, dbslmm_plan_block_matrix); 0 = the full solve
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -83,6 +95,10 @@ typedef struct dbslmm_options {
     int32_t h2f_mode;
     double cheb_tol;
     int32_t lead_min;
+    int32_t large_cheb;
+    int32_t cheb_fused;
+    int32_t debug_delay_us;
+    int32_t debug_stop;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.
@@ -215,6 +231,16 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * iterations of the latest run_multi (0: none), [15] its base copy (-1: none). */
 #define DBSLMM_WORKLOAD_LEN 16
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
+
+/* Diagnostics (parity tests): after plan_sync, the working matrix of block `block` (original
+ * block id) in factorisation copy `copy`: ld x ld fp64, row-major, ld = *ld_out (out == NULL:
+ * only ld).  Layout: rows / columns [small | large | z row m | padding];
+ * after a debug_stop = 1 run the lower triangle (i < m, j <= i) holds Sigma (no 1/(sigma_s n)
+ * shift); after a full run of a block on the multi-workgroup path (m >= tiled_min) the strict
+ * lower triangle holds L (M = L L^T), row m holds y = L^{-1} z, and each 64 x 64 diagonal tile's
+ * diagonal and upper triangle hold its inverse transposed.  Synchronous.  (ABI 9) */
+int dbslmm_plan_block_matrix(dbslmm_plan* plan, int32_t block, int32_t copy, double* out,
+                             int32_t* ld_out);
 
 /* Test-set variance (the `diags` matrix DBSLMMFIT::est saves to variance.txt,
  * scr/dbslmmfit.cpp:116,191-214,242; calcBlock :366-626 with calc_nt_by_nt_matrix,

@@ -135,7 +135,7 @@ def test_cheb_error_within_target(cheb_tol):
 
 @pytest.mark.parametrize("factors", [(0.8, 1.0, 1.2), (0.5, 0.7, 1.0, 1.3, 1.6, 2.0)])
 def test_fused_cheb_launch_bit_identical(monkeypatch, factors):
-    """DBSLMM_CHEB_FUSED=1 runs all 2K passes of a copy group in one dbslmm_trsv_cheb launch
+    """dbslmm_options.cheb_fused = 1 runs all 2K passes of a copy group in one dbslmm_trsv_cheb launch
     (items of every pass interleaved across blocks, own-input waits on flags); the arithmetic is
     the per-pass kernels' own, so the betas are bit-identical (groups of 2 and of 1 copy)."""
     from dbslmm_amd import Context, Plan
@@ -143,10 +143,33 @@ def test_fused_cheb_launch_bit_identical(monkeypatch, factors):
     prob.opts["tiled_min"] = 64
     sig = [prob.sigma_s * f for f in factors]
     ref = Plan(Context(0), prob).run_multi(sig)
-    monkeypatch.setenv("DBSLMM_CHEB_FUSED", "1")
+    prob.opts["cheb_fused"] = 1
     plan = Plan(Context(0), prob)
     for _ in range(2):   # the cached work list is reused
         got = plan.run_multi(sig)
         for x, y in zip(got, ref):
             np.testing.assert_array_equal(_cat(x), _cat(y))
             np.testing.assert_array_equal(x[2], y[2])
+
+
+@pytest.mark.parametrize("large_cheb", [0, -1])
+def test_large_blocks_above_cheb_kernel_size(large_cheb):
+    """with tiled_min above 512, blocks of 512 <= m < tiled_min stay on the
+    single-workgroup path (dbslmm_chol_large) but no longer fit the h2f iteration kernel
+    (dbslmm_chol_cheb keeps ld <= 512 vectors in LDS): their h2f copies must then be factored, not
+    iterated.  Every copy against a fresh single-sigma solve at CHEB_TOL (the base copy bit for
+    bit), and large_cheb = -1 (every copy factored) against the same."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=21, sizes=[300, 520, 700, 999, 130])
+    prob.opts.update(tiled_min=100000, large_cheb=large_cheb)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    multi = Plan(Context(0), prob).run_multi(sig)
+    fresh = _fresh(prob, sig)
+    base = int(np.argsort(sig, kind="stable")[len(sig) // 2])
+    for c, (got, ref) in enumerate(zip(multi, fresh)):
+        np.testing.assert_array_equal(got[2], ref[2])
+        assert np.all(got[2] == 0)
+        if c == base:
+            np.testing.assert_array_equal(_cat(got), _cat(ref))
+        else:
+            assert normwise(_cat(got), _cat(ref)) < CHEB_TOL, c

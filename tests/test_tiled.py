@@ -16,11 +16,11 @@ BASE_SIZES = [128, 129, 159, 160, 161, 191, 192, 575, 640, 703, 1000]
 SIZES = BASE_SIZES + [4100]   # 4100: 512-column super steps (blocks of m >= 4096)
 
 
-def _problem(seed=11, n_ref=256, with_large=True, mono_block=None, sizes=BASE_SIZES):
+def _problem(seed=11, n_ref=256, with_large=True, mono_block=None, sizes=BASE_SIZES, miss_rate=0.002):
     from dbslmm_amd import BlockProblem, synth
     SIZES = sizes
     total = sum(SIZES)
-    p = synth.simulate(total + 50, n_ref, pop="EUR", chroms=[1, 2], seed=seed, miss_rate=0.002,
+    p = synth.simulate(total + 50, n_ref, pop="EUR", chroms=[1, 2], seed=seed, miss_rate=miss_rate,
                        large_every=0)
     rng = np.random.default_rng(seed)
     rows = np.arange(total)
@@ -249,3 +249,63 @@ def test_block_at_tiled_size_cap():
     over = _problem(seed=19, n_ref=128, sizes=[cap])
     with pytest.raises(DbslmmError, match="m must be < 32640"):
         Plan(ctx, over)
+
+
+# config 3 (500k x 5k) failed once on the driver's box -- block 1453 (m = 2659), in a
+# lead group that mixes 512-column (m >= 4096) and 256-column super steps -- and passed on others.
+LEAD_MIX = [4500, 2600, 800, 900, 1200, 300, 150, 40]
+
+
+@pytest.mark.parametrize("delay_us", [0, 300, -300])
+def test_lead_group_mixed_widths_under_delays(delay_us):
+    """A lead group mixing super-step widths (4500 SNPs: R = 4, 2600: R = 2) beside rest blocks on
+    the other streams, each run on a FRESH plan (its first run, right after plan_create's
+    memsets).  dbslmm_options.debug_delay_us holds one side of every cross-stream dependency back
+    (> 0: the bulk trailing launches, the rest sequence and the main stream after the lead fork;
+    < 0: the chain launches and the lead sequence), so a missing event fails deterministically
+    instead of on one box in four.  Betas must be bit-identical to the undelayed run and match the
+    oracle's direct solve per block."""
+    from dbslmm_amd import Context, Plan
+    # (no missing calls: the Gram takes the LDS-DMA path of dbslmm_gram_huge, as at configs 3-5)
+    prob = _problem(seed=23, n_ref=512, sizes=LEAD_MIX, miss_rate=0.0)
+    prob.opts["debug_delay_us"] = 0
+    plan = Plan(Context(0), prob)
+    plan.run()
+    ref_gpu = plan.download()
+    plan.close()
+    assert np.all(ref_gpu[2] == 0)
+    if delay_us == 0:
+        ref, _ = _oracle(prob)
+        got = np.concatenate(ref_gpu[:2])
+        for b in range(len(LEAD_MIX)):
+            sl = np.r_[prob.s_ptr[b]:prob.s_ptr[b + 1]]
+            ll = prob.n_s + np.r_[prob.l_ptr[b]:prob.l_ptr[b + 1]]
+            idx = np.concatenate([sl, ll])
+            assert normwise(got[idx], ref[idx]) < 1e-10, (b, LEAD_MIX[b])
+        return
+    prob.opts["debug_delay_us"] = delay_us
+    for _ in range(2):
+        plan = Plan(Context(0), prob)
+        plan.run()
+        got = plan.download()
+        plan.close()
+        for x, y in zip(got, ref_gpu):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_phase_diagnosis_of_a_good_block():
+    """The per-phase diagnosis tests/test_fullscale.py prints on a mismatch (Sigma after the Gram,
+    L, y = L^-1 z, beta; dbslmm_options.debug_stop + dbslmm_plan_block_matrix) must itself hold
+    on a correct block: every phase within 1e-10 of the oracle."""
+    from test_fullscale import _diagnose, _threads
+    prob = _problem(seed=29, n_ref=384, sizes=[2600, 700])
+    thr = _threads()
+    O.use_blas(True)
+    O.blas_threads(thr)
+    try:
+        for b in range(2):
+            d = _diagnose(prob, b, prob.sigma_s, thr)
+            assert set(d) == {"sigma", "L", "L_diag", "y", "beta"}, d
+            assert max(d.values()) < 1e-10, (b, d)
+    finally:
+        O.blas_threads(1)
