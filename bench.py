@@ -41,7 +41,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PEAK_I8_TOPS = 5000.0        # dense i8 MFMA = 2x the ~2.5 PF dense bf16 rate
+PEAK_FP4_TOPS = 10000.0      # dense FP4 MFMA (MI355X_MICROARCH.md: ~10 PF dense; the Gram's instruction)
+PEAK_I8_TOPS = 5000.0        # dense i8 MFMA (the natural roof of exact integer work; reported beside)
 PEAK_F64_TFLOPS = 78.6       # fp64 (vector = matrix rate on gfx950)
 
 # BASELINE.json configs (1-based): synthetic panels; 3-5 are the scale configs
@@ -81,6 +82,8 @@ def parse():
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="dbslmm_options field (path thresholds; experiments), repeatable")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true",
+                    help="N > 1: skip the big-block beta check of the merged betas")
     ap.add_argument("--no-isolated", action="store_true",
                     help="skip the untimed lead-group-off run that times the Gram without overlap")
     ap.add_argument("--e2e-only", action="store_true", help=argparse.SUPPRESS)
@@ -113,11 +116,13 @@ def kernel_roofline(name, ms, wl, n_solve=1):
                     frac=a / PEAK_HBM_GBS, algorithmic=b, ms=ms)
     if name == "dbslmm_gram_i8":
         a = wl["gram_ops_alg"] / s / 1e12
-        return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_I8_TOPS, unit="TFLOP/s",
-                    frac=a / PEAK_I8_TOPS, algorithmic=wl["gram_ops_alg"], ms=ms,
+        return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_FP4_TOPS, unit="TFLOP/s",
+                    frac=a / PEAK_FP4_TOPS, frac_vs_i8_peak=a / PEAK_I8_TOPS,
+                    algorithmic=wl["gram_ops_alg"], ms=ms,
                     executed_tops=wl["gram_ops_exec"] / s / 1e12,
-                    note="int8 ops (2/MAC), algorithmic sum_b n_ref*m_b*(m_b+1); executed = "
-                         "padded tiles x padded individuals")
+                    note="ops (2/MAC) of the exact integer Gram, algorithmic sum_b n_ref*m_b*(m_b+1), vs "
+                         "the dense FP4 peak of the instruction it issues (v_mfma_scale_f32_32x32x64_f8f6f4, "
+                         "dosages as e2m1); executed = padded tiles x padded individuals")
     if name == "dbslmm_trsv":
         # h2f Chebyshev iterations: per iteration one forward + one backward substitution, each
         # streaming the base copy's factor once (HBM-bound; chained over 64-row tiles)
@@ -264,7 +269,15 @@ def cpu_leg(args, prob, res, sigmas, wl):
         sample_snps_per_s=snps_t / sec_t,
         t1=dict(value=m_all / t_one, cores=1, sample_snps=snps_1, seconds=sec_1,
                 sample_snps_per_s=snps_1 / sec_1),
-        host=hi, est_seconds_per_step=t_all)
+        host=hi, est_seconds_per_step=t_all,
+        cores_note=(f"{thr} threads = this GPU box's CPU share: the pool exports OMP_NUM_THREADS="
+                    f"{os.environ.get('OMP_NUM_THREADS', '?')} for one GPU and asks jobs to size worker "
+                    f"pools to it; the affinity mask ({hi['affinity']} threads) spans the whole host, "
+                    f"which other jobs share, so it is not this job's to use"),
+        node_linear_estimate=dict(
+            value=m_all / t_all * (hi["nproc"] / 2) / thr, cores=hi["nproc"] // 2,
+            note="upper bound for the reference on every physical core of this host: the measured "
+                 "rate scaled linearly from the threads used (not measured)"))
     # beta check 1: the timed sample vs the reference-faithful PCG (every h2f solve)
     mx, nw, ncmp = 0.0, 0.0, 0
     for s_idx, l_idx, o in outs_t:
@@ -659,7 +672,7 @@ def main():
     dbeta = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         cpu, dbeta = cpu_leg(args, prob, res, sigmas, wl)
-    elif rank == 0 and full_res is not None and not args.replicas and not args.no_cpu_baseline:
+    elif rank == 0 and full_res is not None and not args.replicas and not args.no_check:
         dbeta = dict(big_blocks=big_block_check(full, full_res, sigmas),
                      note=f"merged betas of the {n_gpus}-GPU solve (cpu_baseline is timed at N = 1 only)")
     e2e = e2e_pre
@@ -688,7 +701,9 @@ def main():
                        "h2f": args.h2f, "options": dict(full.opts),
                        "snps_rank0": wl["snps"], "snps_total": total_snps, "n_ref": args.n_ref,
                        "blocks_rank0": wl["blocks"], "devices": devices if world == 1 else None,
-                       "gram": "exact int8 dosages on v_mfma_i32_32x32x32_i8, fp64 epilogue",
+                       "gram": "exact integer dosages as FP4 (e2m1, unit block scales) on "
+                               "v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation exact below 2^24, "
+                               "fp64 epilogue",
                        "solve": "fp64 Cholesky of the joint per-block matrix" + (
                            "; h2f: tiled blocks factored once (base h2f), the other h2f solves by "
                            "%d Chebyshev iterations on that factor" % wl["cheb_iters"]

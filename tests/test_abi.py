@@ -85,3 +85,21 @@ def test_options_struct_matches_header():
     body = re.search(r"typedef struct dbslmm_problem \{(.*?)\} dbslmm_problem;", src, re.S).group(1)
     names = re.findall(r"(\w+);", body)
     assert names == [f[0] for f in _lib.Problem._fields_]
+
+
+def test_no_null_stream_transfers_in_library():
+    """Round-3 parity failure (config 3, first run of a fresh plan): plan_create zeroed the matrix
+    buffer with a null-stream hipMemset, which returns before it completes and is not ordered
+    against the context's non-blocking streams, so it zeroed Sigma entries the lead group's Gram
+    had just written.  Every memset and host -> device copy of the library must be stream-ordered
+    (hipMemsetAsync / hipMemcpyAsync on the stream its consumers run on or are forked from)."""
+    import pathlib
+    import re
+    root = pathlib.Path(__file__).resolve().parents[1] / "dbslmm_amd" / "csrc"
+    bad = []
+    for f in sorted(root.glob("*.hip")):
+        for i, line in enumerate(f.read_text().splitlines(), 1):
+            code = line.split("//")[0]
+            if re.search(r"\bhipMemset\s*\(", code) or re.search(r"\bhipMemcpy\s*\([^;]*HostToDevice", code):
+                bad.append(f"{f.name}:{i}: {line.strip()}")
+    assert not bad, "null-stream transfers:\n" + "\n".join(bad)
