@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <future>
 #include <iostream>
 #include <sstream>
 #include <string>
@@ -56,6 +57,7 @@ struct Param {                     // PARAM, scr/dbslmm.hpp:29-45 (initialised h
     double tau = 0.8;
     bool precise = false, dry_run = false, h2f_merged = false, timing = false;
     int repeat = 0;                 // --repeat N: N more solves of the resident problem (timing)
+    int parse_threads = 8;          // --parse-threads N: host parser threads beside the GPU set-up
     string h2f;                     // "0.8,1,1.2": h2 factors of software/DBSLMM.R tuning
 };
 
@@ -74,6 +76,26 @@ double walltime() {
     struct timeval tv;
     gettimeofday(&tv, nullptr);
     return static_cast<double>(tv.tv_sec) + tv.tv_usec * 1e-6;
+}
+
+// --timing: seconds from the process start (kernel start time, clock ticks) to now -- the loader
+// and static initialisers before main
+double since_process_start() {
+    FILE* f = fopen("/proc/self/stat", "r");
+    if (!f) return -1.0;
+    char buf[1024];
+    const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    const char* q = strrchr(buf, ')');          // fields after the command name
+    if (!q) return -1.0;
+    unsigned long long start = 0;
+    int field = 2;
+    for (const char* c = q + 1; *c; ++c)
+        if (*c == ' ' && ++field == 22) { start = strtoull(c + 1, nullptr, 10); break; }
+    struct timespec ts;
+    clock_gettime(CLOCK_BOOTTIME, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9 - static_cast<double>(start) / sysconf(_SC_CLK_TCK);
 }
 
 void print_header() {
@@ -102,6 +124,7 @@ void print_help() {
               << " --tau     [num]        LD shrinkage, default 0.8 (extension)\n"
               << " --precise-out          17 significant digits in <eff>.txt (extension)\n"
               << " --timing               phase wall times as one JSON line on stderr (extension)\n"
+              << " --parse-threads [num]  host parser threads while the GPU is set up (default 8; extension)\n"
               << " --repeat  [num]        with --timing: num more solves of the resident problem, their\n"
               << "                        wall times in the JSON line as solve_repeat (extension)\n"
               << " -h2f      [list]       h2 factors, e.g. 0.8,1,1.2: one Gram, one solve per factor,\n"
@@ -147,6 +170,7 @@ void assign(int argc, char** argv, Param& p) {
         else if (!strcmp(a, "--dry-run")) p.dry_run = true;
         else if (!strcmp(a, "--timing")) p.timing = true;
         else if (!strcmp(a, "--repeat")) { if ((v = take(i))) p.repeat = std::max(0, atoi(v)); }
+        else if (!strcmp(a, "--parse-threads")) { if ((v = take(i))) p.parse_threads = std::max(1, atoi(v)); }
     }
 }
 
@@ -219,23 +243,34 @@ vector<Summ> read_summ(const MappedText& f) {
     return out;
 }
 
+// the .bim row of every summary SNP (-1: absent): the hashed half of matchRef, which needs no MAF,
+// so it runs while the GPU thread still uploads the .bed and computes the MAF pass
+vector<int32_t> lookup_ref(const vector<Summ>& summ, const Bim& bim) {
+    vector<int32_t> row(summ.size());
+    auto key = [&](size_t i) { return bim.snp[i]; };
+    parallel_chunks(summ.size(), host_threads(), [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) row[i] = bim.idx.find(summ[i].snp, key);
+    });
+    return row;
+}
+
 // SNPPROC::matchRef (scr/dtpr.cpp:383-408): strict allele equality, |maf_ref - maf| < mafMax.
 // A SNP absent from the .bim compares against a default ALLELE ("", "", 0.0) as the reference's
 // operator[] does, and is never kept.
-vector<Pos> match_ref(const vector<Summ>& summ, const Bim& bim, double maf_max, vector<char>& good) {
+vector<Pos> match_ref(const vector<Summ>& summ, const Bim& bim, const vector<int32_t>& rows, double maf_max,
+                      vector<char>& good) {
     good.assign(summ.size(), 0);
     const unsigned T = host_threads();
     vector<vector<Pos>> part(T);
     vector<int> dis_t(T, 0), maf_t(T, 0);
     vector<size_t> lo_t(T + 1, 0);
     for (unsigned t = 0; t <= T; ++t) lo_t[t] = summ.size() * t / T;
-    auto key = [&](size_t i) { return bim.snp[i]; };
     vector<std::thread> th;
     for (unsigned t = 0; t < T; ++t)
         th.emplace_back([&, t] {
             for (size_t i = lo_t[t]; i < lo_t[t + 1]; ++i) {
                 const Summ& s = summ[i];
-                const int32_t r = bim.idx.find(s.snp, key);
+                const int32_t r = rows[i];
                 const string_view b1 = r >= 0 ? bim.a1[r] : string_view(), b2 = r >= 0 ? bim.a2[r] : string_view();
                 const double bm = r >= 0 && !bim.maf.empty() ? bim.maf[r] : 0.0;
                 const bool a1 = b1 == s.a1, a2 = b2 == s.a2;
@@ -385,6 +420,7 @@ int fail(const string& msg) {
 
 // --timing: wall time of each phase (seconds), printed as one JSON line on stderr at exit
 struct Phases {
+    double pre_main = since_process_start();
     double t0 = walltime(), last = t0;
     string json;
     void put(const char* name, double sec) {
@@ -535,24 +571,19 @@ int main(int argc, char** argv) {
     rf.close();
     bf.close();
 
-    std::cout << "Reading reference PLINK FAM file from [" << p.r << ".fam]\n";
-    const int n_ref = get_row(p.r + ".fam");
-    std::cout << n_ref << " individuals to be included from reference FAM file.\n";
-    std::cout << "Reading reference PLINK BIM file from [" << p.r << ".bim]\n";
-    MappedText bim_txt;
-    bim_txt.open(p.r + ".bim");
-    const int64_t n_snp_bim = count_lines(bim_txt.text);
+    // The GPU side runs on its own host thread from here on, while this one parses the text
+    // inputs: HIP context (runtime and device initialisation), one staged upload of the .bed cached
+    // on the context (it serves the MAF pass and the plan), then -- once this thread has counted
+    // the .fam and .bim lines -- the MAF pass of readBim.
     const bool constr = !(std::fabs(p.mafMax - 1.0) < 1e-10);
-
-    // The GPU side runs on its own host thread while this one parses the text inputs: HIP context
-    // (device initialisation), one staged upload of the .bed cached on the context (it serves the
-    // MAF pass and the plan), the MAF pass of readBim.
     dbslmm_ctx* ctx = nullptr;
     Mapped bed;
     vector<double> maf;
     vector<int32_t> ids;
     string gpu_err;
     double t_ctx = 0.0, t_up = 0.0, t_maf = 0.0;
+    std::promise<std::pair<int, int64_t>> dims;     // (n_ref, .bim lines) for the MAF pass
+    std::future<std::pair<int, int64_t>> dims_f = dims.get_future();
     std::thread gpu;
     if (!p.dry_run) {
         if (!bed.open(p.r + ".bed")) return fail(p.r + ".bed cannot be opened");
@@ -576,10 +607,11 @@ int main(int argc, char** argv) {
                 }
                 t_ctx = walltime() - t;
             }
+            const std::pair<int, int64_t> nd = dims_f.get();
             if (constr) {
                 t = walltime();
-                maf.resize(n_snp_bim);
-                if (dbslmm_bed_maf(ctx, bed.p, static_cast<int64_t>(bed.n), n_ref, n_snp_bim, maf.data()) != DBSLMM_OK) {
+                maf.resize(nd.second);
+                if (dbslmm_bed_maf(ctx, bed.p, static_cast<int64_t>(bed.n), nd.first, nd.second, maf.data()) != DBSLMM_OK) {
                     gpu_err = string("MAF pass: ") + dbslmm_last_error(ctx);
                     return;
                 }
@@ -589,6 +621,18 @@ int main(int argc, char** argv) {
     } else if (constr) {
         return fail("--dry-run needs -mafMax 1 (the MAF pass runs on the GPU)");
     }
+
+    // the parsers run on fewer threads until the GPU thread's set-up is done: the HIP runtime's
+    // initialisation and the .bed upload's pread pool are the critical path, not the parsing
+    g_host_threads_cap = static_cast<unsigned>(p.parse_threads);
+    std::cout << "Reading reference PLINK FAM file from [" << p.r << ".fam]\n";
+    const int n_ref = get_row(p.r + ".fam");
+    std::cout << n_ref << " individuals to be included from reference FAM file.\n";
+    std::cout << "Reading reference PLINK BIM file from [" << p.r << ".bim]\n";
+    MappedText bim_txt;
+    bim_txt.open(p.r + ".bim");
+    const int64_t n_snp_bim = count_lines(bim_txt.text);
+    dims.set_value({n_ref, n_snp_bim});
 
     // host parsing (overlaps the GPU thread)
     Bim bim;
@@ -603,13 +647,17 @@ int main(int argc, char** argv) {
         l_txt.open(p.l);
         summ_l = read_summ(l_txt);
     }
+    const vector<int32_t> rows_s = lookup_ref(summ_s, bim);
+    const vector<int32_t> rows_l = has_lfile ? lookup_ref(summ_l, bim) : vector<int32_t>();
     const double t_parse = walltime() - ph.t0;
     if (gpu.joinable()) gpu.join();
+    g_host_threads_cap = 16;
     if (!gpu_err.empty()) return fail(gpu_err);
     if (!ids.empty()) std::cout << "Sharding the LD blocks over " << ids.size() << " GPUs.\n";
     if (constr) std::cout << "Calculating MAF of reference panel ...\n";
     else std::cout << "[WARNING] Do not consider the difference between reference panel and summary data ...\n";
     bim.maf = std::move(maf);
+    ph.put("pre_main", ph.pre_main);
     ph.put("ctx", t_ctx);
     ph.put("bed_upload", t_up);
     ph.put("maf", t_maf);
@@ -620,7 +668,7 @@ int main(int argc, char** argv) {
 
     std::cout << "Reading summary data of small effect SNPs from [" << p.s << "]\n";
     vector<char> good_s;
-    const vector<Pos> inter_s = match_ref(summ_s, bim, p.mafMax, good_s);
+    const vector<Pos> inter_s = match_ref(summ_s, bim, rows_s, p.mafMax, good_s);
     std::cout << "After filtering, " << inter_s.size() << " small effect SNPs are selected.\n";
     const vector<Info> info_s = add_block(inter_s, blocks);
     string badtxt;
@@ -633,7 +681,7 @@ int main(int argc, char** argv) {
     if (has_lfile) {
         std::cout << "Reading summary data of large effect SNPs from [" << p.l << "]\n";
         vector<char> good_l;
-        inter_l = match_ref(summ_l, bim, p.mafMax, good_l);
+        inter_l = match_ref(summ_l, bim, rows_l, p.mafMax, good_l);
         if (!inter_l.empty()) {
             info_l = add_block(inter_l, blocks);
             std::cout << "After filtering, " << inter_l.size() << " large effect SNPs are selected.\n";
@@ -792,7 +840,10 @@ int main(int argc, char** argv) {
     }
     if (!write_eff_files(names, lists, p.precise ? 17 : 6)) return fail(names[0] + ".txt cannot be written");
     ph.mark("write");
-    if (p.timing) ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));
+    if (p.timing) {
+        ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));
+        fprintf(stderr, "EXIT_AT %.6f\n", walltime());
+    }
     // the parsed inputs (views of the mappings, hash index, host arrays) need no teardown
     std::cout.flush();
     fflush(stderr);

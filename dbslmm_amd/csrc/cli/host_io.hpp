@@ -83,8 +83,11 @@ inline void parallel_chunks(size_t n, unsigned threads, F f) {
         th.emplace_back(f, n * t / threads, n * (t + 1) / threads);
     for (auto& x : th) x.join();
 }
+// worker threads of the host parsers / writer: at most 16 (the CPU share of one GPU on the box);
+// the dbslmm CLI lowers the cap while its GPU thread initialises the device and uploads the .bed
+inline unsigned g_host_threads_cap = 16;
 inline unsigned host_threads() {
-    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    return std::max(1u, std::min(g_host_threads_cap, std::thread::hardware_concurrency()));
 }
 
 // IO::getRow (scr/dtpr.cpp:71-80)

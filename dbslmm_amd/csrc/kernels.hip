@@ -141,7 +141,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
     const int k = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (k >= n_slots) return;
     const int slot = slot_list ? slot_list[k] : k;   // a subset of the slots (n_slots of them)
-    const int32_t pos = slot_pos[slot];
+    const int32_t pos = slot_pos ? slot_pos[slot] : slot;   // (null: slot k reads bed row k)
     const int64_t n_words = kpad / 16;          // 16 individuals per lane-word
     uint32_t* grow = Gp ? Gp + static_cast<int64_t>(slot) * n_words : nullptr;
     if (pos < 0) {                              // padding slot
@@ -186,7 +186,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
         if (S_out) S_out[slot] = ds;
         if (mu_out) mu_out[slot] = mu;
         if (rsd_out) rsd_out[slot] = 1.0 / sd;                      // +inf when monomorphic
-        if (nmiss > 0 && block_flags) atomicOr(block_flags + slot_block[slot], 1);
+        if (nmiss > 0 && block_flags) atomicOr(block_flags + (slot_block ? slot_block[slot] : slot), 1);
     }
 }
 
@@ -199,13 +199,21 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
 // mafMax, strict) can flip on them.  One thread per row: a sequential chain of n_ref fp64 adds,
 // rounded exactly like the host's (no reassociation).
 // ------------------------------------------------------------------------------------------
+// Rows without a missing call (miss[k] == 0; miss / S from dbslmm_unpack_stats, optional) hold
+// only integer dosages: every partial sum of that order is an exact integer, so a1 + a2 equals
+// the exact observed sum S and the chain is skipped (bit-identical).
 extern "C" __global__ __launch_bounds__(256) void dbslmm_maf_arma(
     const uint8_t* __restrict__ bed, int32_t n_ref, int64_t bytes_per_snp,
     const int32_t* __restrict__ pos, int32_t n_rows, const double* __restrict__ mu,
-    double* __restrict__ maf_out) {
+    double* __restrict__ maf_out, const double* __restrict__ S, const int32_t* __restrict__ miss) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_rows) return;
-    const int64_t row_off = 3 + static_cast<int64_t>(pos[k]) * bytes_per_snp;
+    if (miss && S && miss[k] == 0) {
+        const double af = 0.5 * S[k] / static_cast<double>(n_ref);
+        maf_out[k] = (1.0 - af) < af ? 1.0 - af : af;
+        return;
+    }
+    const int64_t row_off = 3 + static_cast<int64_t>(pos ? pos[k] : k) * bytes_per_snp;
     const double m = mu[k];
     double a1 = 0.0, a2 = 0.0;
     for (int32_t i0 = 0; i0 < n_ref; i0 += 16) {

@@ -51,6 +51,19 @@ def test_bed_maf_matches_oracle(fit):
         got = bed_maf(fit.ctx, bed, n_ref, n_snp)
         ref = O.bed_maf(bed, n_ref, n_snp, threads=4)
         np.testing.assert_array_equal(got, ref)     # Armadillo accumulate order, bit for bit
+    # rows with and without missing calls side by side: the no-missing rows take the exact-sum
+    # shortcut, the others the sequential Armadillo-order chain (n_ref odd: a ragged last word)
+    from dbslmm_amd import synth
+    p = synth.simulate(3000, 1003, chroms=[1], seed=4, miss_rate=0.0004, large_every=0)
+    has_miss = np.zeros(p.m, dtype=bool)
+    nb = (1003 + 3) // 4
+    rows = p.bed[3:].reshape(p.m, nb)
+    for j in range(4):
+        has_miss |= np.any(((rows >> (2 * j)) & 3) == 1, axis=1) if j < 3 else \
+            np.any((((rows[:, :-1] >> 6) & 3) == 1), axis=1)
+    assert 0.1 < has_miss.mean() < 0.9, has_miss.mean()
+    got = bed_maf(fit.ctx, p.bed, 1003, p.m)
+    np.testing.assert_array_equal(got, O.bed_maf(p.bed, 1003, p.m, threads=4))
 
 
 def test_read_snp_std_matches_oracle(fit):
