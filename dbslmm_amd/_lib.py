@@ -36,7 +36,8 @@ class Options(C.Structure):
         ("tiled_min", C.c_int32), ("gram_big_min", C.c_int32), ("gram_huge_min", C.c_int32),
         ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double), ("lead_min", C.c_int32),
         ("large_cheb", C.c_int32), ("cheb_fused", C.c_int32), ("debug_delay_us", C.c_int32),
-        ("debug_stop", C.c_int32),
+        ("debug_stop", C.c_int32), ("sub_split", C.c_int32), ("sub_grid_lead", C.c_int32),
+        ("sub_grid_rest", C.c_int32),
     ]
 
 

@@ -207,6 +207,10 @@ struct dbslmm_plan {
     int32_t debug_delay_us = 0;              // dbslmm_options.debug_delay_us (tests)
     int32_t debug_stop = 0;                  // dbslmm_options.debug_stop (tests)
     int64_t n_runs = 0;                      // completed run enqueues (graphs are captured from the second)
+    // dbslmm_options.sub_split: the substitution lists are ordered [lead group | rest group], each
+    // group a contiguous item range of d_tri_f / d_tri_b and block range of d_tb
+    bool sub_split = false;
+    int32_t n_titems_lead = 0, n_tb_lead = 0, sub_grid_lead = 0, sub_grid_rest = 0;
     bool trsv_pending = false;               // a persistent substitution ran since the last error check
     bool trsv_failed = false;                // ... and one of its hand-off waits gave up (sticky until the next run)
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (DBSLMM_DIAG) only
@@ -819,7 +823,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    (op.h2f_mode == 0 || op.h2f_mode == 1) && op.cheb_tol >= 0.0 &&
                    (op.large_cheb == 0 || op.large_cheb == -1) && (op.cheb_fused == 0 || op.cheb_fused == 1) &&
                    op.debug_delay_us >= -100000 && op.debug_delay_us <= 100000 &&
-                   (op.debug_stop == 0 || op.debug_stop == 1), "bad dbslmm_options");
+                   (op.debug_stop == 0 || op.debug_stop == 1) && op.sub_split >= -1 && op.sub_split <= 1 &&
+                   op.sub_grid_lead >= 0 && op.sub_grid_rest >= 0, "bad dbslmm_options");
     p->h2f_mode = op.h2f_mode;
     p->cheb_fused = op.cheb_fused == 1;
     p->debug_delay_us = op.debug_delay_us;
@@ -1070,19 +1075,34 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         (void)tmax;
         // ticket order: tile position relative to the block's length minus alpha T / Tmax (bigger
         // blocks' tiles are claimed earlier: their chains are longer; ties: longer block first),
-        // monotone in the position within each block, so every dependency comes earlier
-        struct It { double key; int T; int32_t b, I; };
+        // monotone in the position within each block, so every dependency comes earlier.  Split
+        // substitutions (sub_split): the lead group's items first, then the rest group's, each
+        // group in that order (and d_tb = [lead blocks | rest blocks])
+        // (config 4, same box: one sequence 45.1-45.5 ms per step; split on 64 / 192 workgroups
+        // 43.9-44.1; 96 / 160 44.9; 128 / 128 47.1; a rest grid of every CU 51-56 -- its
+        // persistent workgroups then hold the CUs the lead factorisation's tail still needs)
+        p->sub_split = op.sub_split >= 0 && !p->tl_rest.empty();
+        p->sub_grid_lead = op.sub_grid_lead > 0 ? op.sub_grid_lead : std::max(1, ctx->n_cu / 4);
+        p->sub_grid_rest = op.sub_grid_rest > 0 ? op.sub_grid_rest : std::max(1, ctx->n_cu - p->sub_grid_lead);
+        auto grp_of = [&](int32_t b) { return p->sub_split && mv[b] < lead_min ? 1 : 0; };
+        struct It { int grp; double key; int T; int32_t b, I; };
         std::vector<It> v;
         constexpr double alpha = 0.25;
         int tmx = 1;
         for (int32_t b : p->h_tb) tmx = std::max(tmx, (mv[b] + trsv::kT - 1) / trsv::kT);
         for (int32_t b : p->h_tb) {
             const int T = (mv[b] + trsv::kT - 1) / trsv::kT;
-            for (int I = 0; I < T; ++I) v.push_back({static_cast<double>(I) / T - alpha * T / tmx, T, b, I});
+            for (int I = 0; I < T; ++I) v.push_back({grp_of(b), static_cast<double>(I) / T - alpha * T / tmx, T, b, I});
         }
         std::stable_sort(v.begin(), v.end(), [&](const It& x, const It& y) {
-            return x.key != y.key ? x.key < y.key : x.T > y.T;
+            return x.grp != y.grp ? x.grp < y.grp : x.key != y.key ? x.key < y.key : x.T > y.T;
         });
+        p->n_titems_lead = static_cast<int32_t>(std::count_if(v.begin(), v.end(), [](const It& x) { return x.grp == 0; }));
+        if (p->sub_split) {
+            std::stable_partition(p->h_tb.begin(), p->h_tb.end(), [&](int32_t b) { return grp_of(b) == 0; });
+            p->n_tb_lead = static_cast<int32_t>(std::count_if(p->h_tb.begin(), p->h_tb.end(),
+                                                              [&](int32_t b) { return grp_of(b) == 0; }));
+        }
         for (const It& x : v) {
             tri_f.push_back(x.b);
             tri_f.push_back(x.I);
@@ -1330,6 +1350,19 @@ struct TGroup {
 static TGroup tgroup_all(const dbslmm_plan* p) {
     return TGroup{0, p->n_titems, 0, p->n_tiled, p->ctx->stream2, p->d_tflags + p->n_tflags,
                   std::max(1, std::min(p->ctx->n_cu, p->n_titems))};
+}
+// split substitutions: the lead group on stream2 (ticket counter after the flags), the rest group
+// on the rest sequence's stream (its own counter: the spare word after the error word)
+static TGroup tgroup_lead(const dbslmm_plan* p) {
+    const int g = p->sub_grid_lead;
+    return TGroup{0, p->n_titems_lead, 0, p->n_tb_lead, p->ctx->stream2, p->d_tflags + p->n_tflags,
+                  std::max(1, std::min(g, p->n_titems_lead))};
+}
+static TGroup tgroup_rest(const dbslmm_plan* p) {
+    const int g = p->sub_grid_rest;
+    const int32_t ni = p->n_titems - p->n_titems_lead;
+    return TGroup{p->n_titems_lead, ni, p->n_tb_lead, p->n_tiled - p->n_tb_lead, p->ctx->stream4,
+                  p->d_tflags + p->n_tflags + 2, std::max(1, std::min(g, ni))};
 }
 static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     dbslmm_ctx* ctx = p->ctx;
@@ -1896,18 +1929,34 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             if (n == 1 || cheb) {
                 // h2f: factor only the base copy, iterate the others on its factor
                 int rc = lead ? DBSLMM_OK : run_tiled_copy(p, isn, fcopy);
-                if (lead) {   // the rest sequence is done before the substitutions (one launch
-                              // sequence over all tiled blocks: per-group substitutions measured
-                              // slower)
+                if (lead && p->sub_split) {
+                    // per-group substitutions: the rest group's on its own stream right after its
+                    // factorisation, the lead group's on stream2 after the lead factorisation
+                    const TGroup gr = tgroup_rest(p), gl = tgroup_lead(p);
+                    if (rc == DBSLMM_OK && gr.n_items > 0) rc = run_pbwd(p, isn, fcopy, gr);
+                    if (rc == DBSLMM_OK && cheb && gr.n_items > 0) rc = run_cheb(p, isn, cp, gr);
+                    if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, gl);
+                    if (rc != DBSLMM_OK) return rc;
+                    if (cheb) {
+                        if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                        rc = run_cheb(p, isn, cp, gl);
+                        if (rc != DBSLMM_OK) return rc;
+                    }
                     HIP_TRY(ctx, hipEventRecord(ctx->join4, ctx->stream4));
                     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->join4, 0));
-                }
-                if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, tgroup_all(p));
-                if (rc != DBSLMM_OK) return rc;
-                if (cheb) {
-                    if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
-                    rc = run_cheb(p, isn, cp, tgroup_all(p));
+                } else {
+                    if (lead) {   // the rest sequence is done before the substitutions (one launch
+                                  // sequence over all tiled blocks)
+                        HIP_TRY(ctx, hipEventRecord(ctx->join4, ctx->stream4));
+                        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->join4, 0));
+                    }
+                    if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, tgroup_all(p));
                     if (rc != DBSLMM_OK) return rc;
+                    if (cheb) {
+                        if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                        rc = run_cheb(p, isn, cp, tgroup_all(p));
+                        if (rc != DBSLMM_OK) return rc;
+                    }
                 }
             } else {
                 // merged copies: one sequence factors every copy, then one backward launch each

@@ -87,6 +87,13 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                instead of by timing.  Results must be bit-identical to a run without it.
  * debug_stop     testing only: 1 = stop every run after the Gram (the block matrices then hold
  *                Sigma, dbslmm_plan_block_matrix); 0 = the full solve
+ * sub_split      scheduling, plans with a lead group: 0 / 1 = the substitutions (backward solve and
+ *                h2f Chebyshev passes) run per group -- the rest group's right after its own
+ *                factorisation, beside the lead group's, on sub_grid_rest / sub_grid_lead
+ *                persistent workgroups (default); -1 = one launch sequence over all tiled blocks
+ *                after both factorisations.  Scheduling only: bit-identical results.
+ * sub_grid_lead, sub_grid_rest   their persistent grids (0 = default: a quarter of the CUs for
+ *                the lead group, the other three quarters for the rest)
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -99,6 +106,9 @@ typedef struct dbslmm_options {
     int32_t cheb_fused;
     int32_t debug_delay_us;
     int32_t debug_stop;
+    int32_t sub_split;
+    int32_t sub_grid_lead;
+    int32_t sub_grid_rest;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.

@@ -309,3 +309,31 @@ def test_phase_diagnosis_of_a_good_block():
             assert max(d.values()) < 1e-10, (b, d)
     finally:
         O.blas_threads(1)
+
+
+@pytest.mark.parametrize("delay_us", [0, 300, -300])
+def test_split_substitutions_bit_identical(delay_us):
+    """dbslmm_options.sub_split = 1: the rest group's backward solve and h2f Chebyshev passes run
+    on its own stream right after its factorisation, the lead group's on stream2, each with its own
+    ticket counter and grid (here 8 / 24 persistent workgroups, fewer than the groups' items).  The
+    tile arithmetic is the same, so single solves and h2f copies equal the one-sequence
+    substitutions bit for bit -- also with one side of every cross-stream dependency delayed."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=37, n_ref=512, sizes=LEAD_MIX, miss_rate=0.0)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    res = {}
+    for split in (-1, 1):
+        prob.opts = dict(sub_split=split, sub_grid_lead=8, sub_grid_rest=24,
+                         debug_delay_us=delay_us if split == 1 else 0)
+        plan = Plan(Context(0), prob)
+        plan.run()
+        one = plan.download()
+        multi = plan.run_multi(sig)
+        plan.close()
+        res[split] = (one, multi)
+    for x, y in zip(res[1][0], res[-1][0]):
+        np.testing.assert_array_equal(x, y)
+    for c in range(3):
+        for x, y in zip(res[1][1][c], res[-1][1][c]):
+            np.testing.assert_array_equal(x, y)
+    assert np.all(res[1][0][2] == 0)
