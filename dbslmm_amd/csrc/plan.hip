@@ -49,8 +49,11 @@ constexpr size_t kCholChebLds = sizeof(double) * chol::kChebLdsDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
 constexpr size_t kRegionLds = sizeof(double) * chol::kRegionDoubles;
 constexpr size_t kTrail3Lds = sizeof(double) * chol::kTrail3k16Doubles;   // the K = 16 variant (2 per CU)
-constexpr int kTiledMinDefault = 512;   // blocks with m >= this take the multi-workgroup path
-constexpr int kTiledMinSmall = 256;     // the same when no block reaches kTiledMinDefault
+constexpr int kTiledMinDefault = 384;   // blocks with m >= this take the multi-workgroup path
+                                        // (round 4, with the per-group substitutions: config 4
+                                        // 44.1-44.3 -> 43.2-43.3 ms, one run in four 45.0; configs
+                                        // 3 / 5 -0.1 / -0.2 ms; 512 before, 320 no better)
+constexpr int kTiledMinSmall = 256;     // the same when no block reaches 512 SNPs (config 2)
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
 constexpr int kLeadMinDefault = 2048;    // lead group: m >= max(this, m_max / 2) (dbslmm_options.lead_min)
@@ -858,7 +861,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         for (int b = 0; b < pr->num_block; ++b)
             mmax = std::max<int64_t>(mmax, pr->s_ptr[b + 1] - pr->s_ptr[b] +
                                                (has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0));
-        if (mmax < kTiledMinDefault) tiled_min = kTiledMinSmall;
+        if (mmax < 512) tiled_min = kTiledMinSmall;
     }
     p->tiled_min = static_cast<int32_t>(std::min<int64_t>(tiled_min, INT32_MAX));
     // lead group: the tiled blocks with the longest factorisation chains (m >= lead_min); their

@@ -58,7 +58,7 @@ typedef struct dbslmm_plan dbslmm_plan;
  * sizes).  Zero-initialise for the defaults; every field's 0 means "default".
  *
  * tiled_min      blocks with m >= tiled_min take the multi-workgroup tiled factorisation
- *                (default 512, or 256 when no block reaches 512; minimum 64)
+ *                (default 384, or 256 when no block reaches 512; minimum 64)
  * gram_big_min   blocks with m >= this use the 128 x 128-tile Gram kernel (default 96)
  * gram_huge_min  ... and the 256 x 256-tile one from here (default 384, 768 when n_ref < 4096)
  * h2f_mode       plan_run_multi: 0 = tiled blocks factored once, the other sigmas solved by
@@ -153,7 +153,7 @@ enum {
     DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
                                  (concurrent with CHOL_LARGE when there are no tiled blocks) */
     DBSLMM_K_CHOL_TILED = 4,  /* dbslmm_tchol_*: blocks with m >= the tiled threshold
-                                 (dbslmm_options.tiled_min; default 512, or 256 when no block
+                                 (dbslmm_options.tiled_min; default 384, or 256 when no block
                                  reaches 512), many workgroups per block,
                                  one launch per panel phase (third stream); the whole sequence */
     DBSLMM_K_TRSV = 5,        /* dbslmm_trsv_fwd/bwd: h2f tuning's Chebyshev iterations of the

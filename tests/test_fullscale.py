@@ -130,7 +130,7 @@ def _diagnose(prob, b, sg, thr, devices=0):
     del M, S
     y = solve_triangular(L, z, lower=True)
     x = solve_triangular(L.T, y, lower=False) / np.sqrt(prob.n_obs)
-    if m >= 512:     # the tiled layout (default tiled_min)
+    if m >= 384:     # the tiled layout (default tiled_min at full scale)
         st = np.tril_indices(m, -1)
         out["L"] = float(np.max(np.abs(A[:m, :m][st] - L[st])) / np.max(np.abs(L)))
         out["L_diag"] = normwise(1.0 / np.diag(A)[:m], np.diag(L))
