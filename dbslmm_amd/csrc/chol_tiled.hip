@@ -188,9 +188,11 @@ __device__ __forceinline__ void tile_regs_store(const double (&v)[16], double* S
 
 // 32 x 32 tile in LDS (stride kTS, lower triangle valid, rows beyond m zero): factor and invert
 // it in one pass (the scheme of factor_diag: row lanes factor, lanes 32..63 carry the columns of
-// X = L^{-1}).  L goes back into T (strict upper zeroed), X row-major into Xo.
-__device__ __forceinline__ bool factor_tile_lds(double* T, double* Xo, double* colb, int c0, int m,
-                                                int ms, double dshift, int lane) {
+// X = L^{-1}).  Both go back into T in the layout of the stored matrix: strict lower = L, diagonal
+// + upper (r, c >= r) = X[c][r] (L's diagonal is not kept: nothing reads it), so the region needs
+// no LDS of its own for the inverses.
+__device__ __forceinline__ bool factor_tile_lds(double* T, double* colb, int c0, int m, int ms, double dshift,
+                                                int lane) {
     const int r = lane & 31;
     const bool xlane = lane >= kT;
     const int jmax = min(kT, m - c0);
@@ -230,29 +232,34 @@ __device__ __forceinline__ bool factor_tile_lds(double* T, double* Xo, double* c
             }
         }
     }
-    if (!xlane) {
+    // row lane r: L[r][c < r]; inverse lane r (column r of X): X[q][r] for q >= r at (r, q)
 #pragma unroll
-        for (int c = 0; c < kT; ++c) T[r * kTS + c] = c <= r ? v[c] : 0.0;
-    } else {
-#pragma unroll
-        for (int q = 0; q < kT; ++q) Xo[q * kTS + r] = q >= jmax ? (q == r ? 1.0 : 0.0) : v[q];
+    for (int c = 0; c < kT; ++c) {
+        if (!xlane && c < r) T[r * kTS + c] = v[c];
+        if (xlane && c >= r) T[r * kTS + c] = c >= jmax ? (c == r ? 1.0 : 0.0) : v[c];
     }
     wave_sync();
     return fail;
 }
 
-// acc (2 x 2 of 16 x 16) += sign * P Q^T with Q given TRANSPOSED in LDS (Qt[k][ri], stride kTS)
-__device__ __forceinline__ void mfma_tile_qt(v4d (&acc)[2][2], const double* P, const double* Qt,
-                                             double sign, int lane) {
+// X[a][b] of a diagonal sub-tile factored by factor_tile_lds (lower triangular: 0 above)
+__device__ __forceinline__ double x_at(const double* T, int a, int b) {
+    return b <= a ? T[b * kTS + a] : 0.0;
+}
+
+// acc (2 x 2 of 16 x 16) += sign * P Q^T over K = 32, operand elements P(row, k), Q(row, k) from
+// the accessors (the reads and MFMA order of mfma_tile)
+template <class PF, class QF>
+__device__ __forceinline__ void mfma_tile_f(v4d (&acc)[2][2], PF pget, QF qget, double sign, int lane) {
     const int ri = lane & 15, kq = lane >> 4;
     double p0[kT / 4], p1[kT / 4], q0[kT / 4], q1[kT / 4];
 #pragma unroll
     for (int kk = 0; kk < kT / 4; ++kk) {
         const int k = 4 * kk + kq;
-        p0[kk] = P[ri * kTS + k];
-        p1[kk] = P[(16 + ri) * kTS + k];
-        q0[kk] = Qt[k * kTS + ri];
-        q1[kk] = Qt[k * kTS + 16 + ri];
+        p0[kk] = pget(ri, k);
+        p1[kk] = pget(16 + ri, k);
+        q0[kk] = qget(ri, k);
+        q1[kk] = qget(16 + ri, k);
     }
 #pragma unroll
     for (int kk = 0; kk < kT / 4; ++kk) {
@@ -311,7 +318,10 @@ __device__ __forceinline__ void store64_both(const double* S, double* A, int ld,
 
 // lower sub-tiles (a >= b) of a 128 x 128 region, 4 x 4 of 32
 __device__ __forceinline__ int rsub(int a, int b) { return a * (a + 1) / 2 + b; }
-constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X10 (2) + colb
+// LDS of the region kernel: R (10 sub-tiles; the diagonal ones also hold their inverses, the
+// pending-update staging and the 64-level inverse temporaries reuse R) + colb + flag = 87.6 KiB,
+// so a region workgroup fits on a CU beside one trailing workgroup (64 KiB)
+constexpr int kRegionDoubles = 10 * kSub + 2 * kT + 8;
 
 }  // namespace chol
 
@@ -322,10 +332,12 @@ constexpr int kRegionDoubles = 16 * kSub + 2 * kT + 8;   // R (10) + X32 (4) + X
 // slice at a time) --
 // then four 32-column steps (wave 0: factor_tile_lds; all waves: MFMA panel and trailing updates
 // inside the region), the 64-level inverse blocks X10 = -X11 L10 X00 of its two 64 x 64
-// diagonal tiles, and one write-back: strict lower = L, each 64 x 64 diagonal tile's diagonal +
+// diagonal tiles, and the write-back: strict lower = L, each 64 x 64 diagonal tile's diagonal +
 // upper = its X^T (what the panel and the backward solve read).  Region 0 without update also
-// writes the z row and flags monomorphic SNPs.
-extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_region(
+// writes the z row and flags monomorphic SNPs.  87.6 KiB of LDS and <= 256 registers per lane
+// (2 waves per SIMD), so the workgroup needs half a CU, not a whole one: the lead chain's region
+// launches start beside the bulk trailing workgroups instead of waiting for a CU to drain.
+extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tchol_region(
     chol::TiledArgs a0, const int32_t* __restrict__ blocks, int32_t n) {
     using namespace chol;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -342,9 +354,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     STAMP_DECL
     STAMP_BEGIN();
     double* R = lds;
-    double* X32 = lds + 10 * kSub;
-    double* X10 = lds + 14 * kSub;
-    double* colb = lds + 16 * kSub;
+    double* colb = lds + 10 * kSub;
     int* fflag = reinterpret_cast<int*>(colb + 2 * kT);
     if (tid == 0) *fflag = 0;
     if (reg == 0 && !update) {
@@ -365,7 +375,8 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
         if (q < 10) load_acc(acc[u], A, ld, c0 + kT * qa[u], c0 + kT * qb[u], lane);
     }
     if (update) {
-        double* P = X32;   // staging of one 32-column slice of the panel rows (4 sub-tiles)
+        double* P = R;     // staging of one 32-column slice of the panel rows (4 sub-tiles; R is
+                           // not populated before the accumulators are stored below)
         const int cp = c0 - 2 * kBT * update, nk = 4 * update;
         double nv[kT * kT / chol::kWave];
         tile32_load(nv, A, ld, c0 + kT * wave, cp, lane);
@@ -378,6 +389,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             for (int u = 0; u < 3; ++u)
                 if (wave + 4 * u < 10) mfma_tile(acc[u], P + qa[u] * kSub, P + qb[u] * kSub, -1.0, lane);
         }
+        __syncthreads();                      // every wave is done with the staging (= R)
     }
 #pragma unroll
     for (int u = 0; u < 3; ++u)
@@ -389,8 +401,7 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     for (int t = 0; t < 4; ++t) {
         if (c0 + kT * t >= m) break;
         if (wave == 0) {
-            const bool f = factor_tile_lds(R + rsub(t, t) * kSub, X32 + t * kSub, colb, c0 + kT * t,
-                                           m, ms, dshift, lane);
+            const bool f = factor_tile_lds(R + rsub(t, t) * kSub, colb, c0 + kT * t, m, ms, dshift, lane);
             if (f && lane == 0) *fflag = 1;
         }
         __syncthreads();
@@ -402,7 +413,10 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
             if (i <= 3 && c0 + kT * i <= m) {
                 v4d pc[2][2];
                 zero_acc(pc);
-                mfma_tile(pc, R + rsub(i, t) * kSub, X32 + t * kSub, 1.0, lane);
+                const double* P = R + rsub(i, t) * kSub;
+                const double* X = R + rsub(t, t) * kSub;
+                mfma_tile_f(pc, [&](int r, int k) { return P[r * kTS + k]; },
+                            [&](int r, int k) { return x_at(X, r, k); }, 1.0, lane);
                 acc_to_lds(pc, R + rsub(i, t) * kSub, lane);
             }
         }
@@ -428,55 +442,65 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads) void dbslmm_tchol_r
     }
     STAMP_END(1);
     STAMP_BEGIN();
-    // 3) 64-level inverse blocks: X10_p = -X_{2p+1} (L_{2p+1,2p} X_{2p}), p = wave (0, 1)
-    if (wave < 2 && c0 + kBT * wave + kT <= m) {
-        const int p = wave;
-        {
-            v4d tt[2][2];
-            zero_acc(tt);
-            mfma_tile_qt(tt, R + rsub(2 * p + 1, 2 * p) * kSub, X32 + 2 * p * kSub, 1.0, lane);   // T = L10 X00
-            acc_to_lds(tt, X10 + p * kSub, lane);
-            chol::wave_sync();
-            zero_acc(tt);
-            mfma_tile_qt(tt, X32 + (2 * p + 1) * kSub, X10 + p * kSub, -1.0, lane);          // -X11 T
-            chol::wave_sync();
-            acc_to_lds(tt, X10 + p * kSub, lane);
-        }
-    }
-    __syncthreads();
-    STAMP_END(2);
-    STAMP_BEGIN();
-    // 4) write-back
-    for (int q = 0; q < 10; ++q) {
-        int aa = 0;
-        while ((aa + 1) * (aa + 2) / 2 <= q) ++aa;
-        const int bb = q - aa * (aa + 1) / 2;
-        const double* S = R + q * kSub;
+    // 3a) write-back of the region's off-diagonal 64 x 64 tile L10 (sub-tiles (2|3, 0|1)), as-is and
+    //     transposed: its LDS then holds the 64-level inverse temporaries
+    for (int u = 0; u < 4; ++u) {
+        const int aa = 2 + (u >> 1), bb = u & 1;
+        const double* S = R + rsub(aa, bb) * kSub;
         for (int e = tid; e < kT * kT; e += kLargeThreads) {
             const int rr = e >> 5, cc = e & 31;
             const int gr = c0 + kT * aa + rr, gc = c0 + kT * bb + cc;
-            if (gr > m || gc >= m) continue;
-            if (aa == bb && cc >= rr) continue;
-            A[static_cast<int64_t>(gr) * ld + gc] = S[rr * kTS + cc];
+            if (gr <= m && gc < m) A[static_cast<int64_t>(gr) * ld + gc] = S[rr * kTS + cc];
         }
-    }
-    for (int u = 0; u < 4; ++u) {      // the region's off-diagonal 64 x 64 tile L10, transposed
-        const int aa = 2 + (u >> 1), bb = u & 1;
-        const double* S = R + rsub(aa, bb) * kSub;
         for (int e = tid; e < kT * kT; e += kLargeThreads) {
             const int rr = e & 31, cc = e >> 5;
             const int gr = c0 + kT * aa + rr, gc = c0 + kT * bb + cc;
             if (gr < m && gc < m) A[static_cast<int64_t>(gc) * ld + gr] = S[rr * kTS + cc];
         }
     }
-    for (int t = 0; t < 4; ++t) {      // diagonal + upper of the 32-level diagonal sub-tiles: X^T
-        const int jm = min(kT, m - (c0 + kT * t));
-        if (jm <= 0) break;
-        const double* X = X32 + t * kSub;
+    __syncthreads();
+    STAMP_END(2);
+    STAMP_BEGIN();
+    // 3b) 64-level inverse blocks: X10_p = -X_{2p+1} (L_{2p+1,2p} X_{2p}), p = wave (0, 1), in the
+    //     LDS of sub-tile (2, p)
+    double* X10 = R + rsub(2, 0) * kSub;   // X10 + p * kSub = sub-tile (2, p)
+    if (wave < 2 && c0 + kBT * wave + kT <= m) {
+        const int p = wave;
+        const double* L10 = R + rsub(2 * p + 1, 2 * p) * kSub;
+        const double* X0 = R + rsub(2 * p, 2 * p) * kSub;
+        const double* X1 = R + rsub(2 * p + 1, 2 * p + 1) * kSub;
+        double* W = X10 + p * kSub;
+        v4d tt[2][2];
+        zero_acc(tt);
+        mfma_tile_f(tt, [&](int r, int k) { return L10[r * kTS + k]; },
+                    [&](int r, int k) { return x_at(X0, k, r); }, 1.0, lane);              // T = L10 X00
+        acc_to_lds(tt, W, lane);
+        chol::wave_sync();
+        zero_acc(tt);
+        mfma_tile_f(tt, [&](int r, int k) { return x_at(X1, r, k); },
+                    [&](int r, int k) { return W[k * kTS + r]; }, -1.0, lane);               // -X11 T
+        chol::wave_sync();
+        acc_to_lds(tt, W, lane);
+    }
+    __syncthreads();
+    // 4) write-back of the rest: the other lower sub-tiles, the diagonal sub-tiles (strict lower =
+    //    L, diagonal + upper = X^T, both already in place), and X10^T
+    for (int q = 0; q < 10; ++q) {
+        int aa = 0;
+        while ((aa + 1) * (aa + 2) / 2 <= q) ++aa;
+        const int bb = q - aa * (aa + 1) / 2;
+        if (aa >= 2 && bb <= 1) continue;      // L10: written above
+        const double* S = R + q * kSub;
+        const int jm = min(kT, m - (c0 + kT * aa));
         for (int e = tid; e < kT * kT; e += kLargeThreads) {
             const int rr = e >> 5, cc = e & 31;
-            if (cc >= rr && rr < jm)
-                A[static_cast<int64_t>(c0 + kT * t + rr) * ld + c0 + kT * t + cc] = X[cc * kTS + rr];
+            const int gr = c0 + kT * aa + rr, gc = c0 + kT * bb + cc;
+            if (aa == bb && cc >= rr) {
+                if (rr < jm) A[static_cast<int64_t>(gr) * ld + gc] = S[rr * kTS + cc];
+                continue;
+            }
+            if (gr > m || gc >= m) continue;
+            A[static_cast<int64_t>(gr) * ld + gc] = S[rr * kTS + cc];
         }
     }
     for (int p = 0; p < 2; ++p) {      // upper-right sub-tile of each 64 x 64 diagonal tile: X10^T
