@@ -56,6 +56,7 @@ constexpr int kTiledMinDefault = 384;   // blocks with m >= this take the multi-
 constexpr int kTiledMinSmall = 256;     // the same when no block reaches 512 SNPs (config 2)
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
+constexpr int kTChebMaxM = 4096;         // whole-block Chebyshev passes: blocks of <= 64 tiles
 constexpr int kLeadMinDefault = 2048;    // lead group: m >= max(this, m_max / 2) (dbslmm_options.lead_min)
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
@@ -214,6 +215,11 @@ struct dbslmm_plan {
     // group a contiguous item range of d_tri_f / d_tri_b and block range of d_tb
     bool sub_split = false;
     int32_t n_titems_lead = 0, n_tb_lead = 0, sub_grid_lead = 0, sub_grid_rest = 0;
+    // sub_split = 2: the rest group's h2f Chebyshev passes as whole-block launches (dbslmm_tcheb):
+    // its blocks, largest first, and the LDS stride of the work vector (64 x the most tiles)
+    bool sub_block = false;
+    int32_t* d_tcheb_blocks = nullptr;
+    int32_t n_tcheb = 0, tcheb_vld = 0;
     bool trsv_pending = false;               // a persistent substitution ran since the last error check
     bool trsv_failed = false;                // ... and one of its hand-off waits gave up (sticky until the next run)
     unsigned long long* d_stamps = nullptr;  // diagnostic builds (DBSLMM_DIAG) only
@@ -602,6 +608,9 @@ static hipError_t set_trsv_lds() {
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_cheb<NR>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
     if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tcheb<NR>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>((NR * kTChebMaxM + trsv::kT * NR) * sizeof(double)));
+    if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_trsv_bwd<NR>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(trsv::kLdsBytes));
 }
@@ -778,7 +787,8 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_blk_id, p->d_row0, p->d_m, p->d_ms, p->d_ld, p->d_matoff, p->d_tiles,
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
-                    p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items};
+                    p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items,
+                    p->d_tcheb_blocks};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -826,7 +836,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    (op.h2f_mode == 0 || op.h2f_mode == 1) && op.cheb_tol >= 0.0 &&
                    (op.large_cheb == 0 || op.large_cheb == -1) && (op.cheb_fused == 0 || op.cheb_fused == 1) &&
                    op.debug_delay_us >= -100000 && op.debug_delay_us <= 100000 &&
-                   (op.debug_stop == 0 || op.debug_stop == 1) && op.sub_split >= -1 && op.sub_split <= 1 &&
+                   (op.debug_stop == 0 || op.debug_stop == 1) && op.sub_split >= -1 && op.sub_split <= 2 &&
                    op.sub_grid_lead >= 0 && op.sub_grid_rest >= 0, "bad dbslmm_options");
     p->h2f_mode = op.h2f_mode;
     p->cheb_fused = op.cheb_fused == 1;
@@ -1065,7 +1075,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     // substitution work lists (trsv.hip): 64-row tiles of the tiled blocks; forward in order of
     // (tile, block), backward in order of (tiles from the end, block) -- every dependency of an
     // item comes earlier in its list
-    std::vector<int32_t> tri_f, tri_b, foff(std::max(1, p->n_nonempty), 0);
+    std::vector<int32_t> tri_f, tri_b, foff(std::max(1, p->n_nonempty), 0), tcheb_list;
     {
         int32_t nf = 0, tmax = 0;
         for (int32_t b : p->h_tb) {
@@ -1105,6 +1115,20 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             std::stable_partition(p->h_tb.begin(), p->h_tb.end(), [&](int32_t b) { return grp_of(b) == 0; });
             p->n_tb_lead = static_cast<int32_t>(std::count_if(p->h_tb.begin(), p->h_tb.end(),
                                                               [&](int32_t b) { return grp_of(b) == 0; }));
+        }
+        // whole-block Chebyshev passes for the rest group (sub_split = 2): every rest block within
+        // kTChebMaxM (the work vector of NR copies in LDS; one workgroup streams the block alone)
+        if (p->sub_split && op.sub_split == 2) {
+            std::vector<int32_t> rb(p->h_tb.begin() + p->n_tb_lead, p->h_tb.end());
+            int32_t tmax_r = 0;
+            for (int32_t b : rb) tmax_r = std::max(tmax_r, (mv[b] + trsv::kT - 1) / trsv::kT);
+            if (!rb.empty() && tmax_r * trsv::kT <= kTChebMaxM) {
+                std::stable_sort(rb.begin(), rb.end(), [&](int32_t x, int32_t y) { return mv[x] > mv[y]; });
+                tcheb_list = rb;
+                p->sub_block = true;
+                p->n_tcheb = static_cast<int32_t>(rb.size());
+                p->tcheb_vld = tmax_r * trsv::kT;
+            }
         }
         for (const It& x : v) {
             tri_f.push_back(x.b);
@@ -1182,6 +1206,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     if ((e = dev_upload(&p->d_foff, foff, ctx->stream)) != hipSuccess) return fail("upload trsv lists");
     if ((e = dev_upload(&p->d_tb, p->h_tb, ctx->stream)) != hipSuccess) return fail("upload trsv lists");
     if (!slot_order.empty() && (e = dev_upload(&p->d_slot_order, slot_order, ctx->stream)) != hipSuccess) return fail("upload slot order");
+    if (!tcheb_list.empty() && (e = dev_upload(&p->d_tcheb_blocks, tcheb_list, ctx->stream)) != hipSuccess)
+        return fail("upload trsv lists");
     // [tile flags | ticket counter | error word | spare]
     if ((e = hipMalloc(&p->d_tflags, (p->n_tflags + 3) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc trsv flags");
     if ((e = hipMemsetAsync(p->d_tflags, 0, (p->n_tflags + 3) * sizeof(int32_t), ctx->stream)) != hipSuccess) return fail("hipMemset trsv flags");
@@ -1718,6 +1744,54 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
     return DBSLMM_OK;
 }
 
+// The rest group's Chebyshev copies as whole-block launches (sub_split = 2, trsv.hip dbslmm_tcheb):
+// per copy group one launch, one workgroup per block, every iteration inside; same state vectors,
+// coefficients and outputs as run_cheb's passes.
+static int run_tcheb(dbslmm_plan* p, double isn, const ChebPlan& cp, hipStream_t st) {
+    dbslmm_ctx* ctx = p->ctx;
+    const int64_t vs = std::max<int64_t>(1, p->n_slots);
+    const int64_t blk = trsv::kMaxR * vs;
+    double *X = p->d_cheb + 2 * blk, *R = X + blk, *D = R + blk, *S = D + blk;
+    for (size_t g = 0; g < cp.iters.size(); ++g) {
+        const size_t g0 = g * trsv::kMaxR;
+        const int nr = static_cast<int>(std::min<size_t>(trsv::kMaxR, cp.others.size() - g0));
+        TChebArgs a{};
+        a.M = p->d_M + static_cast<int64_t>(cp.base) * p->M_elems;
+        a.matoff = p->d_matoff;
+        a.ld = p->d_ld;
+        a.m = p->d_m;
+        a.ms = p->d_ms;
+        a.row0 = p->d_row0;
+        a.blk_id = p->d_blk_id;
+        a.slot_out = p->d_slot_out;
+        a.blocks = p->d_tcheb_blocks;
+        a.n_blocks = p->n_tcheb;
+        a.iters = cp.iters[g];
+        a.vld = p->tcheb_vld;
+        a.vs = vs;
+        a.x_base = p->d_y + static_cast<int64_t>(cp.base) * p->n_slots;
+        a.X = X;
+        a.R = R;
+        a.D = D;
+        a.S = S;
+        a.coef = p->d_coef + cp.coef_off[g];
+        a.inv_sqrt_n = isn;
+        a.beta_s = p->d_beta_s;
+        a.beta_l = p->d_beta_l;
+        a.ns_stride = p->n_s;
+        a.nl_stride = p->n_l;
+        for (int j = 0; j < trsv::kMaxR; ++j) a.cix[j] = j < nr ? cp.others[g0 + j] : cp.others[g0];
+        a.st_base = p->d_status + cp.base * p->nbk;
+        a.status = p->d_status;
+        a.st_stride = p->nbk;
+        const size_t lds = (static_cast<size_t>(nr) * a.vld + trsv::kT * nr) * sizeof(double);
+        if (nr == 1) hipLaunchKernelGGL(dbslmm_tcheb<1>, dim3(p->n_tcheb), dim3(trsv::kBThreads), lds, st, a);
+        else hipLaunchKernelGGL(dbslmm_tcheb<2>, dim3(p->n_tcheb), dim3(trsv::kBThreads), lds, st, a);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return DBSLMM_OK;
+}
+
 // One run: unpack + Gram (front; else the Gram of the previous front run is reused), then n
 // factorisations + solves of it, copy c with sigma_s = sigmas[c] (n > 1: h2f tuning; copies
 // 1.. are device copies of the Gram, all factored by one merged tiled sequence).
@@ -1937,7 +2011,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                     // factorisation, the lead group's on stream2 after the lead factorisation
                     const TGroup gr = tgroup_rest(p), gl = tgroup_lead(p);
                     if (rc == DBSLMM_OK && gr.n_items > 0) rc = run_pbwd(p, isn, fcopy, gr);
-                    if (rc == DBSLMM_OK && cheb && gr.n_items > 0) rc = run_cheb(p, isn, cp, gr);
+                    if (rc == DBSLMM_OK && cheb && gr.n_items > 0)
+                        rc = p->sub_block ? run_tcheb(p, isn, cp, gr.st) : run_cheb(p, isn, cp, gr);
                     if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, gl);
                     if (rc != DBSLMM_OK) return rc;
                     if (cheb) {

@@ -499,3 +499,224 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_cheb_init(
     }
     if (threadIdx.x < nr) st[(threadIdx.x == 0 ? c0 : c1) * st_stride + blk_id[b]] = st_base[blk_id[b]];
 }
+
+// ---------------------------------------------------------------- whole-block Chebyshev passes
+// The rest group's tiled blocks (m < the lead threshold, at most ~40 tiles of 64) iterate with one
+// workgroup per block and every pass of the Chebyshev group in ONE launch: no ticket, flag or
+// hand-off per 64-row tile -- the tile item's fixed cost (ticket, drain, flag, poll, about as long
+// as streaming a small block's tile row) is what held those blocks' per-pass launches to ~14 GB/s
+// per CU.  The block's substitutions stream its factor row by row (the layout of trsv.hip's tile
+// items: 8 waves x 8 rows of a 64-row tile, lane = column) as one flat sequence of (row tile,
+// column tile) pairs with kPF pairs in flight per wave across row-tile boundaries; a row tile ends
+// with a butterfly reduction of the 8 x NR lane partial sums (no LDS transpose), the diagonal
+// inverse block product and a workgroup barrier.  The vectors: the work vector v in LDS, the
+// Chebyshev state x / r / d / s in the group's slot vectors (as dbslmm_cheb_init / the tile items'
+// epilogue, same recurrence and coefficients).
+namespace trsv {
+constexpr int kBThreads = kSW * 64;          // 8 streaming waves, no control wave
+constexpr int kBPF = 4;                      // column tiles in flight per wave
+
+// sum of a[0 .. NV) over the wave's 64 lanes; lane l ends with value l >> (6 - log2 NV)
+// (fixed order: deterministic)
+template <int NV>
+__device__ __forceinline__ double wave_sums(double (&a)[NV], int lane) {
+    constexpr int kSteps = NV == 16 ? 4 : NV == 8 ? 3 : NV == 4 ? 2 : 1;
+#pragma unroll
+    for (int st = 0; st < kSteps; ++st) {
+        const int h = NV >> (st + 1), bit = 5 - st;
+        const bool hi = (lane >> bit) & 1;
+#pragma unroll
+        for (int j = 0; j < h; ++j) {
+            const double send = hi ? a[j] : a[j + h];
+            const double keep = hi ? a[j + h] : a[j];
+            a[j] = keep + __shfl_xor(send, 1 << bit);
+        }
+    }
+    double s = a[0];
+#pragma unroll
+    for (int bit = 5 - kSteps; bit >= 0; --bit) s += __shfl_xor(s, 1 << bit);
+    return s;
+}
+
+// one substitution pass of a block (forward L y = v or backward L^T z = v, in place on v).  Row
+// tiles in substitution order; row tile I streams its column tiles (forward J = 0 .. I-1, backward
+// J = T-1 .. I+1) kBPF in flight per wave, and issues the next row tile's first kBPF column tiles
+// before its own reduction, so the stream does not restart at the row-tile boundary.
+template <int NR, bool BWD>
+__device__ __forceinline__ void block_pass(const double* __restrict__ A, int ld, int m, int T, double* v, int vld,
+                                           double* ws, int tid) {
+    const int wave = tid >> 6, lane = tid & 63, row = tid >> 3, part = tid & 7;
+    constexpr int NV = 8 * NR;
+    const double* Lw = A + static_cast<int64_t>(8 * wave) * ld + lane;
+    auto cnt_of = [&](int I) { return BWD ? T - 1 - I : I; };
+    auto col_of = [&](int I, int t) { return BWD ? T - 1 - t : t; };
+    double lr[kBPF][8];
+    auto issue = [&](int u, int I, int t) {
+        const int cj = kT * col_of(I, t);
+        const double* p = Lw + static_cast<int64_t>(kT * I) * ld + cj;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double x = p[static_cast<int64_t>(k) * ld];
+            lr[u][k] = cj + lane < m ? x : 0.0;   // past m: bordered row / padding
+        }
+    };
+    double acc[NV];
+    double xd[8];
+    const int I0 = BWD ? T - 1 : 0, dI = BWD ? -1 : 1;
+#pragma unroll
+    for (int u = 0; u < kBPF; ++u)
+        if (u < cnt_of(I0)) issue(u, I0, u);
+    for (int I = I0; BWD ? I >= 0 : I < T; I += dI) {
+        const int r0 = kT * I, jmax = min(kT, m - r0), cnt = cnt_of(I);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {   // this row tile's diagonal inverse block (used at its end)
+            const int q = 8 * part + k;
+            const int64_t o = BWD ? static_cast<int64_t>(r0 + row) * ld + r0 + q
+                                  : static_cast<int64_t>(r0 + q) * ld + r0 + row;
+            const double x = A[o];
+            xd[k] = (BWD ? (q >= row && q < jmax) : (q <= row && row < jmax)) ? x : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NV; ++q) acc[q] = 0.0;
+        for (int t0 = 0; t0 < cnt; t0 += kBPF) {
+#pragma unroll
+            for (int u = 0; u < kBPF; ++u) {
+                const int t = t0 + u;
+                if (t < cnt) {
+                    const double* vv = v + kT * col_of(I, t) + lane;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+#pragma unroll
+                        for (int c = 0; c < NR; ++c) acc[k * NR + c] += lr[u][k] * vv[c * vld];
+                    if (t + kBPF < cnt) issue(u, I, t + kBPF);
+                }
+            }
+        }
+        const int In = I + dI;
+        if (BWD ? In >= 0 : In < T) {
+            const int cn = cnt_of(In);
+#pragma unroll
+            for (int u = 0; u < kBPF; ++u)
+                if (u < cn) issue(u, In, u);
+        }
+        // w = v_I - sum_J L_IJ v_J (lanes: butterfly sums), then v_I = X_I w / X_I^T w
+        const double s = wave_sums<NV>(acc, lane);
+        constexpr int kSh = NV == 16 ? 2 : NV == 8 ? 3 : 4;
+        if ((lane & ((1 << kSh) - 1)) == 0) {
+            const int vi = lane >> kSh, k = vi / NR, c = vi - k * NR, r = 8 * wave + k;
+            ws[r * NR + c] = r < jmax ? v[c * vld + r0 + r] - s : 0.0;
+        }
+        __syncthreads();
+        double y[NR];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) y[c] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int c = 0; c < NR; ++c) y[c] += xd[k] * ws[(8 * part + k) * NR + c];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) y[c] = red8(y[c]);
+        if (part == 0 && row < jmax)
+#pragma unroll
+            for (int c = 0; c < NR; ++c) v[c * vld + r0 + row] = y[c];
+        __syncthreads();
+    }
+}
+}  // namespace trsv
+
+// All K iterations of a Chebyshev copy group for the listed tiled blocks, one workgroup per block
+// (blocks[g], largest first).  x_base: the base copy's solution (slot vectors); X / R / D / S: the
+// group's state vectors (stride vs per copy); coef [K][NR][3]; betas of copies cix[c]; status of
+// the copies = the base's.
+struct TChebArgs {
+    const double* M;
+    const int64_t* matoff;
+    const int32_t* ld;
+    const int32_t* m;
+    const int32_t* ms;
+    const int32_t* row0;
+    const int32_t* blk_id;
+    const int32_t* slot_out;
+    const int32_t* blocks;
+    int32_t n_blocks;
+    int32_t iters;
+    int32_t vld;                 // LDS stride of the work vector (>= 64 T of every listed block)
+    int64_t vs;
+    const double* x_base;
+    double* X;
+    double* R;
+    double* D;
+    double* S;
+    const double* coef;
+    double inv_sqrt_n;
+    double* beta_s;
+    double* beta_l;
+    int64_t ns_stride, nl_stride;
+    int32_t cix[trsv::kMaxR];
+    const int32_t* st_base;
+    int32_t* status;
+    int64_t st_stride;
+};
+
+template <int NR>
+__global__ __launch_bounds__(trsv::kBThreads, 2) void dbslmm_tcheb(TChebArgs a) {
+    using namespace trsv;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (static_cast<int>(blockIdx.x) >= a.n_blocks) return;
+    const int b = a.blocks[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int m = a.m[b], ms = a.ms[b], ld = a.ld[b], g0 = a.row0[b];
+    const int T = (m + kT - 1) / kT;
+    const double* A = a.M + a.matoff[b];
+    double* v = lds;                            // [NR][vld]
+    double* ws = v + NR * a.vld;                // [64][NR]
+    const int32_t st = a.st_base[a.blk_id[b]];
+    const bool fail = st >= DBSLMM_BLOCK_NOT_PD;
+    if (tid < NR) a.status[a.cix[tid] * a.st_stride + a.blk_id[b]] = st;
+    // start: x = x_b, r = -delta P_s x_b, d = s = 0 (dbslmm_cheb_init)
+    for (int e = tid; e < NR * m; e += kBThreads) {
+        const int c = e / m, i = e - c * m;
+        const int64_t o = c * a.vs + g0 + i;
+        const double xb = a.x_base[g0 + i];
+        a.X[o] = xb;
+        a.R[o] = i < ms ? -a.coef[3 * c + 2] * xb : 0.0;
+        a.D[o] = 0.0;
+        a.S[o] = 0.0;
+    }
+    for (int k = 0; k < a.iters && !fail; ++k) {
+        for (int e = tid; e < NR * a.vld; e += kBThreads) {
+            const int c = e / a.vld, i = e - c * a.vld;
+            v[e] = i < m ? a.R[c * a.vs + g0 + i] : 0.0;
+        }
+        __syncthreads();
+        block_pass<NR, false>(A, ld, m, T, v, a.vld, ws, tid);
+        block_pass<NR, true>(A, ld, m, T, v, a.vld, ws, tid);
+        // d = alpha d + beta z; s = alpha s + beta r; x += d; r -= s + delta P_s d
+        const double* cf = a.coef + static_cast<int64_t>(k) * NR * 3;
+        const bool last = k == a.iters - 1;
+        for (int e = tid; e < NR * m; e += kBThreads) {
+            const int c = e / m, i = e - c * m;
+            const int64_t o = c * a.vs + g0 + i;
+            const double al = cf[3 * c], be = cf[3 * c + 1], de = cf[3 * c + 2];
+            const double d = al * a.D[o] + be * v[c * a.vld + i];
+            const double x = a.X[o] + d;
+            a.X[o] = x;
+            if (!last) {
+                const double r = a.R[o];
+                const double s2 = al * a.S[o] + be * r;
+                a.D[o] = d;
+                a.S[o] = s2;
+                a.R[o] = r - s2 - (i < ms ? de * d : 0.0);
+            }
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < NR * m; e += kBThreads) {
+        const int c = e / m, i = e - c * m;
+        const double x = a.X[c * a.vs + g0 + i];
+        const double bv = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
+        const int so = a.slot_out[g0 + i];
+        if (so >= 0) a.beta_s[a.cix[c] * a.ns_stride + so] = bv;
+        else a.beta_l[a.cix[c] * a.nl_stride - 1 - so] = bv;
+    }
+}

@@ -92,6 +92,9 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                factorisation, beside the lead group's, on sub_grid_rest / sub_grid_lead
  *                persistent workgroups (default); -1 = one launch sequence over all tiled blocks
  *                after both factorisations.  Scheduling only: bit-identical results.
+ *                2 = as 0 / 1, but the rest group's h2f copies iterate with one workgroup per
+ *                block (every Chebyshev pass in one launch, dbslmm_tcheb; blocks up to 4096 SNPs,
+ *                otherwise as 0): results within cheb_tol, not bit-identical to 0 / 1.
  * sub_grid_lead, sub_grid_rest   their persistent grids (0 = default: a quarter of the CUs for
  *                the lead group, the other three quarters for the rest)
  */

@@ -173,3 +173,37 @@ def test_large_blocks_above_cheb_kernel_size(large_cheb):
             np.testing.assert_array_equal(_cat(got), _cat(ref))
         else:
             assert normwise(_cat(got), _cat(ref)) < CHEB_TOL, c
+
+
+@pytest.mark.parametrize("factors", [(0.8, 1.0, 1.2), (1.2, 0.8), (0.5, 0.7, 1.0, 1.3, 1.6)])
+def test_whole_block_cheb_for_rest_group(factors):
+    """dbslmm_options.sub_split = 2: the rest group's h2f copies iterate in dbslmm_tcheb (one
+    workgroup per block, all passes in one launch, butterfly row sums) instead of the per-pass tile
+    items.  A lead group (4500, 2600) and a rest group of tiled blocks (800, 900, 1200, one with a
+    monomorphic SNP) with tiled_min 256.  Every copy against a fresh single-sigma solve at
+    CHEB_TOL, the base copy and the lead group's blocks bit for bit against sub_split = 1, statuses
+    (and the monomorphic SNP's NaN) identical."""
+    from dbslmm_amd import Context, Plan
+    from test_tiled import LEAD_MIX
+    prob = _problem(seed=41, n_ref=512, sizes=LEAD_MIX, miss_rate=0.0, mono_block=3)
+    prob.opts = dict(tiled_min=256)
+    sig = [prob.sigma_s * f for f in factors]
+    res = {}
+    for split in (1, 2):
+        prob.opts["sub_split"] = split
+        plan = Plan(Context(0), prob)
+        res[split] = plan.run_multi(sig)
+        plan.close()
+    prob.opts = dict(tiled_min=256)
+    fresh = _fresh(prob, sig)
+    base = int(np.argsort(sig, kind="stable")[len(sig) // 2])
+    n_lead = LEAD_MIX[0] + LEAD_MIX[1]
+    for c, (got, old, ref) in enumerate(zip(res[2], res[1], fresh)):
+        np.testing.assert_array_equal(got[2], old[2])
+        np.testing.assert_array_equal(got[2], ref[2])
+        if c == base:
+            np.testing.assert_array_equal(_cat(got), _cat(old))
+        else:
+            assert _finite_normwise(_cat(got), _cat(ref)) < CHEB_TOL, c
+            # the lead group's small-effect betas (its blocks come first) are unchanged
+            np.testing.assert_array_equal(got[0][:n_lead - 8], old[0][:n_lead - 8])
