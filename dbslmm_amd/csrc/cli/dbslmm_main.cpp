@@ -463,8 +463,10 @@ int64_t count_lines(string_view t) {
 // rows, "snp a1 beta beta_noscl flag"; ostream's default double format = printf %g at precision 6
 // (17 with --precise-out), produced by std::to_chars (the same digits, ~3x faster than snprintf).
 // All files and row chunks are formatted on the host threads, then written at their offsets.
+// Returns -1 on success, else the index of the first file that could not be opened, written or
+// closed; every output of the call is then removed (none is left truncated or partly written).
 struct EffList { const vector<Info>* info; const vector<Summ>* summ; const double* beta; int flag; };
-bool write_eff_files(const vector<string>& names, const vector<std::array<EffList, 2>>& lists, int prec) {
+long write_eff_files(const vector<string>& names, const vector<std::array<EffList, 2>>& lists, int prec) {
     const unsigned T = host_threads();
     struct Task { size_t file; int list; size_t lo, hi; string out; };
     vector<Task> tasks;
@@ -506,18 +508,19 @@ bool write_eff_files(const vector<string>& names, const vector<std::array<EffLis
     }
     vector<int> fd(names.size(), -1);
     vector<off_t> off(tasks.size(), 0);
-    bool ok = true;
+    long bad = -1;                       // first file that failed
     for (size_t f = 0; f < names.size(); ++f) {
         fd[f] = ::open((names[f] + ".txt").c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        ok = ok && fd[f] >= 0;
+        if (fd[f] < 0 && bad < 0) bad = static_cast<long>(f);
     }
+    const bool ok = bad < 0;
     off_t pos = 0;
     for (size_t t = 0; t < tasks.size(); ++t) {
         if (t > 0 && tasks[t].file != tasks[t - 1].file) pos = 0;
         off[t] = pos;
         pos += static_cast<off_t>(tasks[t].out.size());
     }
-    std::atomic<bool> wok{true};
+    std::atomic<long> wbad{static_cast<long>(names.size())};   // smallest file index a write failed on
     if (ok) {
         next = 0;
         auto wr = [&] {
@@ -526,7 +529,12 @@ bool write_eff_files(const vector<string>& names, const vector<std::array<EffLis
                 size_t done = 0;
                 while (done < o.size()) {
                     const ssize_t w = pwrite(fd[tasks[t].file], o.data() + done, o.size() - done, off[t] + done);
-                    if (w <= 0) { wok = false; break; }
+                    if (w <= 0) {
+                        long cur = wbad.load();
+                        const long f = static_cast<long>(tasks[t].file);
+                        while (f < cur && !wbad.compare_exchange_weak(cur, f)) {}
+                        break;
+                    }
                     done += static_cast<size_t>(w);
                 }
             }
@@ -536,9 +544,13 @@ bool write_eff_files(const vector<string>& names, const vector<std::array<EffLis
         wr();
         for (auto& x : th) x.join();
     }
-    for (int d : fd)
-        if (d >= 0) ok = (::close(d) == 0) && ok;
-    return ok && wok;
+    if (bad < 0 && wbad.load() < static_cast<long>(names.size())) bad = wbad.load();
+    for (size_t f = 0; f < names.size(); ++f)
+        if (fd[f] >= 0 && ::close(fd[f]) != 0 && bad < 0) bad = static_cast<long>(f);
+    if (bad >= 0)
+        for (size_t f = 0; f < names.size(); ++f)
+            if (fd[f] >= 0) ::unlink((names[f] + ".txt").c_str());   // ours: opened (created) above
+    return bad;
 }
 }  // namespace
 
@@ -838,7 +850,8 @@ int main(int argc, char** argv) {
         lists.push_back({EffList{&info_l, &summ_l, beta_l.data() + static_cast<size_t>(f) * info_l.size(), 1},
                          EffList{&info_s, &summ_s, beta_s.data() + static_cast<size_t>(f) * info_s.size(), 0}});
     }
-    if (!write_eff_files(names, lists, p.precise ? 17 : 6)) return fail(names[0] + ".txt cannot be written");
+    if (const long bad = write_eff_files(names, lists, p.precise ? 17 : 6); bad >= 0)
+        return fail(names[static_cast<size_t>(bad)] + ".txt cannot be written");
     ph.mark("write");
     if (p.timing) {
         ph.print(static_cast<int64_t>(info_s.size() + info_l.size()));

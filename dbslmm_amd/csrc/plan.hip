@@ -26,6 +26,7 @@
 #include <string>
 #include <memory>
 #include <mutex>
+#include <chrono>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -273,6 +274,17 @@ static int mp_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int32_t n_ref, int64_
         }                                                                \
     } while (0)
 
+// wait until pred(): a short spin (a chunk is ~0.35 ms of work), then 20 us sleeps, so waiting
+// threads do not take the cores of the host threads the caller runs meanwhile (the CLI parses
+// its text files during the upload) on a machine with fewer cores than the pool
+template <class P>
+static void backoff_wait(P pred) {
+    for (int i = 0; !pred(); ++i) {
+        if (i < 256) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 // Host -> device copy of a large buffer through pinned staging buffers: a pool of host threads
 // fills the chunks (memcpy from the caller's memory, or pread from a file) as far ahead as free
 // buffers allow while earlier chunks' DMAs run; kStageBufs buffers, each reused once its copy's
@@ -305,10 +317,11 @@ static hipError_t upload_pipelined(void* dst, size_t n, hipStream_t st, Fill fil
         for (unsigned t = 0; t < T; ++t)
             th.emplace_back([&, t] {
                 for (size_t k = 0; k < nchunk; ++k) {
-                    while (go.load(std::memory_order_acquire) < static_cast<int64_t>(k)) {
-                        if (stop.load(std::memory_order_relaxed)) return;
-                        std::this_thread::yield();
-                    }
+                    backoff_wait([&] {
+                        return go.load(std::memory_order_acquire) >= static_cast<int64_t>(k) ||
+                               stop.load(std::memory_order_relaxed);
+                    });
+                    if (go.load(std::memory_order_acquire) < static_cast<int64_t>(k)) return;   // stopped
                     const size_t off = k * kChunk, len = std::min(kChunk, n - off);
                     const size_t part = (len + T - 1) / T, a0 = std::min(len, t * part), z = std::min(len, a0 + part);
                     if (!(a0 >= z || fill(static_cast<char*>(stage[k % kStageBufs]) + a0, off + a0, z - a0)))
@@ -333,7 +346,7 @@ static hipError_t upload_pipelined(void* dst, size_t n, hipStream_t st, Fill fil
             released = static_cast<int64_t>(k) - 1;
         }
         release_free(k);
-        while (parts[k].load(std::memory_order_acquire) != T) std::this_thread::yield();
+        backoff_wait([&] { return parts[k].load(std::memory_order_acquire) == T; });
         if (bad.load(std::memory_order_relaxed)) { e = hipErrorInvalidValue; break; }
         const size_t off = k * kChunk, len = std::min(kChunk, n - off);
         e = hipMemcpyAsync(static_cast<char*>(dst) + off, stage[b], len, hipMemcpyHostToDevice, st);

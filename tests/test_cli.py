@@ -151,6 +151,23 @@ def test_cli_h2f_tuning_matches_separate_runs(tmp_path, monkeypatch, cheb):
 
 
 @pytest.mark.gpu
+def test_cli_h2f_unwritable_output_named_and_cleaned(tmp_path):
+    """when one of the -h2f outputs cannot be written (here a directory holds its
+    name), the error names that file, not the first one, and no other output is left behind
+    truncated or partly written."""
+    s, l = split_summary(tmp_path)
+    prefix = str(tmp_path / "chr1")
+    blocked = f"{prefix}_h2f1.dbslmm.txt"
+    os.mkdir(blocked)
+    r = run(["-s", s, "-l", l, "-r", REF, "-b", BLOCKS_EUR1, "-n", "2400", "-nsnp", "996",
+             "-mafMax", "0.2", "-h", "0.5", "-h2f", "0.8,1,1.2", "-eff", prefix + ".dbslmm"])
+    assert r.returncode != 0
+    assert "_h2f1.dbslmm.txt cannot be written" in r.stderr, r.stderr
+    for hh in ("0.8", "1.2"):
+        assert not os.path.exists(f"{prefix}_h2f{hh}.dbslmm.txt")
+
+
+@pytest.mark.gpu
 def test_cli_gpu_ids_shards_match_single_gpu(tmp_path):
     """--gpu-ids 0,0,0 (the LD blocks of chromosome 1 sharded over three contexts; on a node
     --gpus N uses devices 0..N-1) writes the same <eff>.txt byte for byte as one GPU."""
