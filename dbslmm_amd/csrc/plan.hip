@@ -58,7 +58,7 @@ constexpr int kTiledMinSmall = 256;     // the same when no block reaches 512 SN
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
 constexpr int kTChebMaxM = 4096;         // whole-block Chebyshev passes: blocks of <= 64 tiles
-constexpr int kLeadMinDefault = 2048;    // lead group: m >= max(this, m_max / 2) (dbslmm_options.lead_min)
+constexpr int kLeadMinDefault = 1536;    // lead group: m >= max(this, m_max / 8) (dbslmm_options.lead_min)
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
@@ -896,7 +896,11 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
             mmax = std::max<int64_t>(mmax, pr->s_ptr[b + 1] - pr->s_ptr[b] +
                                                (has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0));
         if (op.lead_min >= 0) {
-            lead_min = op.lead_min > 0 ? op.lead_min : std::max<int64_t>(kLeadMinDefault, mmax / 2);
+            // (round 4, config 4 same box, with the substitution grids below: lead >= 1536 on
+            // 80 / 176 workgroups 42.02 / 42.11 ms against 42.85-42.97 for max(2048, m_max / 2) on
+            // 64 / 192; 1280 42.47, 1792 42.44, 1536 on 64 / 192 43.10, on 72 / 184 42.35,
+            // on 96 / 160 43.29 -- profiles/r04/ab/lead_grids.txt)
+            lead_min = op.lead_min > 0 ? op.lead_min : std::max<int64_t>(kLeadMinDefault, mmax / 8);
             lead_min = std::max({lead_min, tiled_min, gram_huge_min});
             for (int b = 0; b < pr->num_block; ++b) {
                 const int64_t m = pr->s_ptr[b + 1] - pr->s_ptr[b] + (has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0);
@@ -1108,7 +1112,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         // 43.9-44.1; 96 / 160 44.9; 128 / 128 47.1; a rest grid of every CU 51-56 -- its
         // persistent workgroups then hold the CUs the lead factorisation's tail still needs)
         p->sub_split = op.sub_split >= 0 && !p->tl_rest.empty();
-        p->sub_grid_lead = op.sub_grid_lead > 0 ? op.sub_grid_lead : std::max(1, ctx->n_cu / 4);
+        p->sub_grid_lead = op.sub_grid_lead > 0 ? op.sub_grid_lead : std::max(1, ctx->n_cu * 5 / 16);
         p->sub_grid_rest = op.sub_grid_rest > 0 ? op.sub_grid_rest : std::max(1, ctx->n_cu - p->sub_grid_lead);
         auto grp_of = [&](int32_t b) { return p->sub_split && mv[b] < lead_min ? 1 : 0; };
         struct It { int grp; double key; int T; int32_t b, I; };

@@ -71,7 +71,7 @@ typedef struct dbslmm_plan dbslmm_plan;
  * lead_min       tiled blocks with m >= lead_min form the lead group: their Gram tiles run first
  *                and their factorisation (the longest dependency chains) starts right after
  *                them, beside the rest of the Gram and the other blocks' factorisation (default
- *                max(2048, m_max / 2) when tiled blocks lie on both sides of it; < 0: no lead
+ *                max(1536, m_max / 8) when tiled blocks lie on both sides of it; < 0: no lead
  *                group, and the tiled sequence starts after the whole Gram instead of right
  *                after the tiled blocks' Gram tiles).  Scheduling only: the results are
  *                bit-identical either way.
@@ -95,7 +95,7 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                2 = as 0 / 1, but the rest group's h2f copies iterate with one workgroup per
  *                block (every Chebyshev pass in one launch, dbslmm_tcheb; blocks up to 4096 SNPs,
  *                otherwise as 0): results within cheb_tol, not bit-identical to 0 / 1.
- * sub_grid_lead, sub_grid_rest   their persistent grids (0 = default: a quarter of the CUs for
+ * sub_grid_lead, sub_grid_rest   their persistent grids (0 = default: 5/16 of the CUs for
  *                the lead group, the other three quarters for the rest)
  */
 typedef struct dbslmm_options {
