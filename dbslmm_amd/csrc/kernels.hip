@@ -9,9 +9,10 @@
 //                        (popcounts) and the fp64 mean and 1/sd (N-1).  HBM-bound, one wave per
 //                        slot.
 //   dbslmm_gram_i8 /     estBlock's LD matrices (scr/dbslmmfit.cpp:697-709, 751-756) as ONE
-//   dbslmm_gram_big /    joint Gram per block over [small | large] SNPs on i8 MFMA
-//   dbslmm_gram_huge     (v_mfma_i32_32x32x32_i8, exact int32 accumulation; each Gp dword is
-//                        expanded to 16 int8 codes in registers / LDS) with an fp64 epilogue that
+//   dbslmm_gram_big /    joint Gram per block over [small | large] SNPs on the FP4 matrix cores
+//   dbslmm_gram_huge     (v_mfma_scale_f32_32x32x64_f8f6f4, exact integer sums in fp32; each Gp
+//                        dword is expanded to FP4 operands in registers -- fp4_chunk below; the
+//                        _i8 kernel keeps its round-2 name) with an fp64 epilogue that
 //                        centres, standardises and applies tau:
 //                          Sigma_ij = tau/n_ref * C_ij /(s_i s_j) + (1-tau) delta_ij,
 //                          C_ij = G_ij - S_i S_j / n   (no missing calls in the block)
@@ -64,22 +65,12 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* __restrict__ bas
 // The Gram operand Gp: per slot, kpad / 16 dwords of 2-bit DOSAGE codes (0, 1, 2; 3 = missing;
 // padding individuals 0), re-coded from the PLINK codes of one .bed dword (individual j in bits
 // 2j..2j+1; 00 -> 2, 10 -> 1, 11 -> 0, 01 -> missing: d0 = lo ^ hi, d1 = ~hi).  A quarter of the
-// bytes of an int8 operand; the Gram kernels expand it on the fly (expand_dose).
+// bytes of an int8 operand; the Gram kernels expand it to FP4 on the fly (fp4_chunk).
 __device__ __forceinline__ uint32_t dose_code16(uint32_t w, uint32_t valid_mask_2bit) {
     const uint32_t lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
     const uint32_t d0 = (lo ^ hi) & valid_mask_2bit, d1 = ~hi & valid_mask_2bit;
     return d0 | (d1 << 1);
 }
-// One Gp dword -> 16 int8 codes.  Output word k holds individuals {k, 4+k, 8+k, 12+k} in bytes
-// 0..3: a fixed within-16 permutation, which every Gram entry is invariant to (both operands of
-// a product are expanded the same way).  Blocks without missing calls: the codes are the dosages.
-__device__ __forceinline__ v4i expand_dose(uint32_t w) {
-    v4i out;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = static_cast<int>((w >> (2 * k)) & 0x03030303u);
-    return out;
-}
-
 // The Gram kernels multiply on the FP4 matrix cores: dosages 0 / 1 / 2 (and the 0 / 1 masks of
 // the missing-call form) are exact e2m1 values, every product is exact and every partial sum an
 // integer below 4 n_ref < 2^24, so v_mfma_scale_f32_32x32x64_f8f6f4 gives the integer Gram bit for
@@ -234,10 +225,10 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_maf_arma(
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 2: grouped joint Gram on i8 MFMA.  One wave = one 32x32 output tile (block, ti, tj),
-// ti >= tj, K loop over the padded individuals 32 at a time.  Lane l loads 16 contiguous bytes
-// of row (l & 31) at k-offset 16*(l >> 5) for both operands (identical k-permutation on the A
-// and B side, so any lane->k assignment the instruction uses is summed consistently).
+// Kernel 2: grouped joint Gram on FP4 MFMA.  One wave = one 32x32 output tile (block, ti, tj),
+// ti >= tj, K loop over the padded individuals 128 at a time (gram_tile32 below: each lane
+// loads 4 Gp dwords of its row per operand and feeds two FP4 MFMAs; identical k-permutation on
+// the A and B side, so any lane->k assignment the instruction uses is summed consistently).
 // Output: row-major lower triangle of the block's joint matrix
 //     Sigma (no d shift; the Cholesky kernel adds 1/(sigma_s n) on the small diagonal).
 // ------------------------------------------------------------------------------------------
