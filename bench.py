@@ -95,6 +95,10 @@ def parse():
                     help="process group backend (nccl = RCCL over xGMI; gloo only for rehearsals)")
     ap.add_argument("--rank-device", type=int, default=None,
                     help="rehearsal on a 1-GPU box: every rank on this device instead of LOCAL_RANK")
+    ap.add_argument("--predict", default=None, metavar="N[,N..]",
+                    help="N = 1 only: one-GPU rehearsal of an N-GPU strong-scaling step -- each device's "
+                         "units of the N-device shard plan timed alone on this GPU; predicted step = the "
+                         "slowest device (reported beside the line, never as value)")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: independent replicas of the workload per rank (weak scaling) instead "
                          "of one problem sharded over the ranks (strong scaling)")
@@ -342,6 +346,45 @@ def big_block_check(prob, res, sigmas):
                    "every block >= 2000 SNPs" + (", every h2f solve" if sigmas else ""))
 
 
+def predict_leg(args, full, sigmas, m_b, ctx):
+    """One-GPU rehearsal of the N-GPU strong-scaling step: for each N the
+    library's shard plan (dbslmm_shard_plan) splits the problem into N devices' units; each
+    device's units plan (dbslmm_plan_create_units, exactly what rank d of `torch.distributed.run
+    --nproc-per-node N bench.py` runs) is timed ALONE on this GPU -- 2 warm-up + `k` timed solves,
+    synchronous like the timed step -- and the predicted step is the slowest device (plus the
+    time model's own prediction beside it).  The RCCL gather of <= 3 x 8 MB over xGMI is not
+    included (~0.1 ms)."""
+    import numpy as np
+    from dbslmm_amd import Plan
+    from dbslmm_amd.dist import shard_units
+    K = len(sigmas) if sigmas else 1
+    sig = sigmas if sigmas else [full.sigma_s]
+    k = 5
+    out = {}
+    for N in [int(x) for x in args.predict.split(",")]:
+        ud, model = shard_units(m_b, full.n_ref, N, K)
+        split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
+        per = []
+        for d in range(N):
+            plan = Plan.units(ctx, full, ud, d)
+            o = (np.zeros((K, full.n_s)), np.zeros((K, full.n_l)), np.zeros((K, full.num_block), dtype=np.int32))
+            for _ in range(2):
+                plan.run_multi(sig, out=o)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                plan.run_multi(sig, out=o)
+            per.append((time.perf_counter() - t0) / k * 1e3)
+            plan.close()
+        step = max(per)
+        out[str(N)] = dict(step_ms=step, value=float(m_b.sum()) / (step * 1e-3), per_device_ms=per,
+                           model_ms=model.tolist(),
+                           split_blocks=[dict(block=int(b), snps=int(m_b[b]), devices=ud[b].tolist()) for b in split])
+    return dict(results=out, unit="SNPs/s", note=(
+        "one-GPU rehearsal: each device's units plan of the N-device shard plan timed alone (2 warm-up + "
+        f"{k} synchronous solves); predicted N-GPU step = the slowest device; value = the problem's SNPs / "
+        "that step.  Excludes the per-step RCCL gather of the betas to rank 0."))
+
+
 def e2e_leg(args, panel):
     """End to end through the drop-in CLI: the workload's synthetic panel written as PLINK
     ref.{bed,bim,fam} + GEMMA summaries + block file (page cache), then `dbslmm` (mmap'd .bed ->
@@ -543,7 +586,7 @@ def main():
     cdev = "cuda" if args.dist_backend == "nccl" else "cpu"    # collective tensors
 
     from dbslmm_amd import Context, KERNEL_NAMES, Plan, synth
-    from dbslmm_amd.dist import ShardGather, shard_blocks, sub_problem
+    from dbslmm_amd.dist import UnitGather, shard_units
 
     def barrier():
         if dist is not None:
@@ -562,35 +605,35 @@ def main():
         full.opts[k] = float(v) if k == "cheb_tol" else int(v)
     del panel   # (the end-to-end leg generated its own copy in its child process)
     sigmas = [full.sigma_s * f for f in args.h2f] if args.h2f else None
+    n_copies = len(sigmas) if sigmas else 1
+    m_b = np.diff(full.s_ptr) + (np.diff(full.l_ptr) if full.l_ptr is not None else 0)
+    if n_copies > 1:
+        full.opts["shard_copies"] = n_copies   # multi-device context: h2f copies may be split
     gather = None
-    if sharded:
-        m_b = np.diff(full.s_ptr) + (np.diff(full.l_ptr) if full.l_ptr is not None else 0)
-        shards = shard_blocks(m_b, full.n_ref, world)
-        prob, s_idx, l_idx = sub_problem(full, shards[rank], compact=True)
-    else:
-        prob = full
+    prob = full
     ctx = Context(devices if in_proc else devices[0])
-    plan = Plan(ctx, prob)
-    wl = plan.workload()
     if sharded:
-        gather = ShardGather(full.n_s, full.n_l, s_idx, l_idx, k=len(sigmas) if sigmas else 1,
-                             device=cdev)
+        # this rank's (block, h2f copy) units of the library's shard plan (dbslmm_shard_plan),
+        # gathered to rank 0 by one RCCL gather per step
+        ud, _ = shard_units(m_b, full.n_ref, world, n_copies)
+        plan = Plan.units(ctx, full, ud, rank)
+        gather = UnitGather(full, ud, device=cdev)
+    else:
+        plan = Plan(ctx, prob)
+    wl = plan.workload()
+    sig_run = sigmas if sigmas else [full.sigma_s]
 
     outs = None
-    if sigmas:   # the caller's result buffers, reused every step (as an application would)
-        outs = (np.zeros((len(sigmas), prob.n_s)), np.zeros((len(sigmas), prob.n_l)),
-                np.zeros((len(sigmas), prob.num_block), dtype=np.int32))
+    if sigmas or sharded:   # the caller's result buffers, reused every step (as an application would)
+        outs = (np.zeros((n_copies, prob.n_s)), np.zeros((n_copies, prob.n_l)),
+                np.zeros((n_copies, prob.num_block), dtype=np.int32))
 
     def step():
-        if sigmas:
-            res = plan.run_multi(sigmas, out=outs)   # one Gram, len(sigmas) solves (synchronous)
+        if sigmas or sharded:
+            res = plan.run_multi(sig_run, out=outs)   # one Gram, len(sigmas) solves (synchronous)
             if gather:
-                return gather([(r[0], r[1]) for r in res])
+                return gather(outs[0], outs[1])
             return res
-        if gather:
-            plan.run()
-            bs, bl, _ = plan.download()
-            return gather([(bs, bl)])
         plan.run()
         return None
 
@@ -613,15 +656,18 @@ def main():
     kms, nlaunch = plan.kernel_ms()
     kms = kms * nlaunch / args.steps          # per step (a tuning step is len(h2f) runs)
     # the results of one more step, compared with the CPU reference below (every h2f solve)
-    if sigmas:
-        res = plan.run_multi(sigmas)
+    if sigmas or sharded:
+        res = plan.run_multi(sig_run, out=outs)
+        res = [(a.copy(), b.copy(), c.copy()) for a, b, c in res]
     else:
         plan.run()
         res = [plan.download()]
     status = res[0][2]
+    if sharded:   # this rank's units only: the other blocks' status entries are not its own
+        status = status[np.any(ud == rank, axis=1)]
     full_res = res if world == 1 else None    # the full problem's betas (rank 0)
     if gather:
-        merged = gather([(r[0], r[1]) for r in res])
+        merged = gather(np.stack([r[0] for r in res]), np.stack([r[1] for r in res]))
         if rank == 0:
             full_res = [(bs, bl, None) for bs, bl in merged]
     st = torch.tensor([int(np.sum((status != 0) & (status != 1)))], dtype=torch.int64, device=cdev)
@@ -676,6 +722,9 @@ def main():
         dbeta = dict(big_blocks=big_block_check(full, full_res, sigmas),
                      note=f"merged betas of the {n_gpus}-GPU solve (cpu_baseline is timed at N = 1 only)")
     e2e = e2e_pre
+    pred = None
+    if args.predict and n_gpus == 1 and rank == 0:
+        pred = predict_leg(args, full, sigmas, m_b, ctx)
 
     if rank == 0:
         if in_proc:
@@ -713,6 +762,7 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "predicted_multi_gpu": pred,
             "max_dbeta_vs_cpu_ref": dbeta,
             "status_nonzero_blocks": int(st.item()),
         }

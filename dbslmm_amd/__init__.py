@@ -146,6 +146,25 @@ class Plan:
         ctx.check(ctx.lib.dbslmm_plan_create(ctx.h, C.byref(self._cs), C.byref(h)), "plan_create")
         self.h = h
 
+    @classmethod
+    def units(cls, ctx: Context, prob: BlockProblem, unit_device, device_index: int):
+        """dbslmm_plan_create_units: the (block, h2f copy) units of `prob` that a shard plan
+        (dist.shard_units -> unit_device [num_block, n_copies]) gives device `device_index`, on
+        this single-device context.  run_multi(sigmas) with len(sigmas) == n_copies writes only
+        those units' entries of the full-size outputs."""
+        self = cls.__new__(cls)
+        self.ctx, self.prob = ctx, prob
+        ud = np.ascontiguousarray(unit_device, dtype=np.int32)
+        if ud.ndim != 2 or ud.shape[0] != prob.num_block:
+            raise ValueError("unit_device: [num_block, n_copies]")
+        self._cs = prob.c_struct()
+        self._ud = ud
+        h = C.c_void_p()
+        ctx.check(ctx.lib.dbslmm_plan_create_units(ctx.h, C.byref(self._cs), ud.shape[1], _ptr(ud),
+                                                   int(device_index), C.byref(h)), "plan_create_units")
+        self.h = h
+        return self
+
     def run(self):
         self.ctx.check(self.ctx.lib.dbslmm_plan_run(self.h), "plan_run")
 

@@ -20,9 +20,10 @@ EXPORTS = (
     "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
     "dbslmm_ctx_create_multi", "dbslmm_ctx_num_devices", "dbslmm_plan_shard_info",
     "dbslmm_ctx_cache_bed", "dbslmm_ctx_cache_bed_fd", "dbslmm_plan_block_matrix",
+    "dbslmm_shard_plan", "dbslmm_plan_create_units",
 )
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv")
@@ -37,7 +38,7 @@ class Options(C.Structure):
         ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double), ("lead_min", C.c_int32),
         ("large_cheb", C.c_int32), ("cheb_fused", C.c_int32), ("debug_delay_us", C.c_int32),
         ("debug_stop", C.c_int32), ("sub_split", C.c_int32), ("sub_grid_lead", C.c_int32),
-        ("sub_grid_rest", C.c_int32),
+        ("sub_grid_rest", C.c_int32), ("shard_copies", C.c_int32),
     ]
 
 
@@ -103,6 +104,8 @@ def load(path: str | None = None):
     L.dbslmm_plan_variance.argtypes = [V, P(TestPanel), V, V]
     L.dbslmm_ctx_cache_bed.argtypes = [V, V, C.c_int64]
     L.dbslmm_ctx_cache_bed_fd.argtypes = [V, C.c_int, C.c_int64, V]
+    L.dbslmm_shard_plan.argtypes = [C.c_int32, V, C.c_int32, C.c_int32, C.c_int32, V, V]
+    L.dbslmm_plan_create_units.argtypes = [V, P(Problem), C.c_int32, V, C.c_int32, P(V)]
     if hasattr(L, "dbslmm_plan_block_matrix"):   # (tools/race_probe.py loads older builds for A/B)
         L.dbslmm_plan_block_matrix.argtypes = [V, C.c_int32, C.c_int32, V, V]
     if L.dbslmm_abi_version() != ABI_VERSION:

@@ -773,6 +773,7 @@ int main(int argc, char** argv) {
         factors.push_back(1.0);
     }
     const int nf = static_cast<int>(factors.size());
+    opts.shard_copies = nf;   // --gpus N: the shard plan may split the h2f copies of the largest blocks
     vector<double> sigmas(nf);
     for (int i = 0; i < nf; ++i) sigmas[i] = p.h * factors[i] / static_cast<double>(p.nsnp);
     vector<double> beta_s(static_cast<size_t>(nf) * info_s.size()), beta_l(static_cast<size_t>(nf) * info_l.size());

@@ -3,25 +3,149 @@
 //
 // The reference parallelises only over LD blocks (OpenMP schedule(dynamic) over batches of 60,
 // scr/dbslmmfit.cpp:191-220): blocks are independent, so a multi-GPU solve needs no exchange during
-// compute.  A multi-device context (dbslmm_ctx_create_multi) holds one single-device context per
-// device; plan_create on it:
-//   1. shards the non-empty LD blocks over the devices, longest-processing-time first on
-//      cost_b = n_ref m_b (m_b + 1) + m_b^3 / 3 (Gram + factorisation), deterministic;
-//   2. builds each shard's sub-problem: its blocks in block order and a COMPACT .bed image holding
-//      only their rows (each device receives only the packed rows it needs: 1/G of the upload);
-//   3. creates the shard plans concurrently, one host thread per device (the uploads overlap on
-//      the devices' own PCIe links).
-// Every later call (run / run_multi / sync / download / variance / timing) fans out over the
-// shards, one host thread each, and scatters the shard outputs into the caller's arrays (beta,
-// status, variance columns) in the original order -- the only "exchange", straight from each
-// device's HBM to the caller's host buffers.  (The ABI's outputs are host memory, so a device-side
-// gather over xGMI before the copy-out would only add a hop)
+// compute.  The unit of work here is an (LD block, h2f copy) pair -- the reference itself runs the
+// h2f solves as independent dbslmm processes (software/DBSLMM.R:204-219):
+//   1. dbslmm_shard_plan assigns the units to devices with a time model of one device (below):
+//      a block's h2f copies stay together (one Gram, one factorisation, Chebyshev iterations for the
+//      other copies on that factor) unless its dependency chain alone exceeds the fair share of the
+//      step; then each copy is a unit of its own, factored directly on a different device, so the
+//      largest blocks' chains run side by side instead of bounding the step;
+//   2. a plan over a device's units is a set of JOBS on that device: one plan over its whole blocks
+//      (all copies) plus one single-copy plan per split unit, each on its own context (streams) so
+//      they run concurrently; the sub-problems carry COMPACT .bed images holding only their rows;
+//   3. every call (run / run_multi / sync / download / variance / timing) fans out over the jobs,
+//      one host thread each, and scatters the job outputs into the caller's arrays (beta, status,
+//      variance columns) in the original order -- the only "exchange", straight from each device's
+//      HBM to the caller's host buffers.  (The ABI's outputs are host memory, so a device-side gather
+//      over xGMI before the copy-out would only add a hop)
+// A multi-device context (dbslmm_ctx_create_multi) builds the jobs of every device;
+// dbslmm_plan_create_units builds those of one device on a single-device context (one process per
+// GPU: bench.py under torch.distributed, whose ranks gather the betas with RCCL).
 #include <thread>
 
-// Run f(i) for every shard index on its own host thread; the first failing rc wins and its
-// sub-context message is copied to the parent context.
+// ---------------------------------------------------------------- time model of one device
+// Calibrated on config 4 (1M SNPs x 10k): chip-time of each kernel class from a
+// serialised SQ_WAVE_CYCLES pass (round 4: trailing 13.2, substitutions 12.0, panels 3.2, Gram 2.9,
+// regions 1.75, unpack 1.4, chol_large 1.0 chip-ms) over its algorithmic work, and the block chains
+// from the 9.6k-SNP block alone (tools/micro/tchol_alone.py) and the substitution stamps.
+namespace shard {
+constexpr double kUnpackBps = 3.6e12;       // unpack: packed + operand bytes per second
+constexpr double kGramOps = 3.1e15;         // Gram: ops (2 per MAC) per second
+constexpr double kTrailFlops = 62e12;       // tiled factorisation bulk (trailing update)
+constexpr double kPanelFlops = 68e12;       // panels: 2 x 128 x m^2 flops per block
+constexpr double kRegionChipUs = 0.17;      // regions: chip-us per 128 columns (86 us on half a CU)
+constexpr double kCholLargeFlops = 2e12;    // single-workgroup blocks (latency-bound)
+constexpr double kSubBps = 4.3e12;          // substitution passes: factor bytes per second
+constexpr double kChainRegionUs = 135.0;    // factorisation chain per 128 columns, block alone
+constexpr double kChainSubUs = 4.5;         // substitution chain per 64-row tile, per pass
+constexpr double kBusy = 0.85;              // fraction of the chip the overlapped phases keep busy
+constexpr int kChebIters = 7;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 (plan.hip cheb_plan)
+constexpr int kTiledMin = 384;              // plan.hip kTiledMinDefault
+
+struct Cost {
+    double work;    // chip-ms
+    double chain;   // ms: the block's dependency chain when it runs alone
+};
+
+// Block of m SNPs, `copies` h2f solves; direct = every copy factored (a split unit is one direct
+// copy), else one factorisation + Chebyshev iterations for the other copies
+static Cost block_cost(double m, double n_ref, int copies, bool direct) {
+    Cost c{0.0, 0.0};
+    if (m <= 0) return c;
+    const double kp = std::ceil(n_ref / 128.0) * 128.0;
+    const double unpack = m * (std::ceil(n_ref / 4.0) + kp / 4.0) / kUnpackBps * 1e3;
+    const double gram = n_ref * m * (m + 1.0) / kGramOps * 1e3;
+    const int nfac = direct ? copies : 1;
+    const double T = std::ceil(m / 64.0);
+    const double pass_bytes = T * (T + 1.0) / 2.0 * 64.0 * 64.0 * 8.0;
+    const int passes = direct ? copies : 1 + (copies > 1 ? 2 * kChebIters : 0);
+    c.work = unpack + gram;
+    if (m >= kTiledMin) {
+        const double fac = m * m * m / 3.0 / kTrailFlops * 1e3 + 256.0 * m * m / kPanelFlops * 1e3 +
+                           m / 128.0 * kRegionChipUs * 1e-3;
+        c.work += nfac * fac + passes * pass_bytes / kSubBps * 1e3;
+        c.chain = gram + m / 128.0 * kChainRegionUs * 1e-3 + (direct ? 1 : passes) * T * kChainSubUs * 1e-3;
+    } else {
+        c.work += (direct ? copies : 1) * m * m * m / 3.0 / kCholLargeFlops * 1e3;
+        c.chain = gram + m * 0.2e-3;   // ~0.2 us per column of the single-workgroup factorisation
+    }
+    return c;
+}
+
+// Units -> devices.  unit_device[b * K + c] (K = copies per run) = device of copy c of block b, -1
+// for an empty block; dev_ms[d] = predicted step of device d.  Deterministic.
+static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, int32_t K,
+                       std::vector<int32_t>& unit_device, std::vector<double>& dev_ms) {
+    K = std::max(1, K);
+    unit_device.assign(static_cast<size_t>(nb) * K, -1);
+    dev_ms.assign(G, 0.0);
+    std::vector<char> split(nb, 0);
+    std::vector<Cost> whole(nb), unit(nb);
+    double total = 0.0, chain_floor = 0.0;
+    for (int b = 0; b < nb; ++b) {
+        whole[b] = block_cost(m[b], n_ref, K, false);
+        unit[b] = block_cost(m[b], n_ref, 1, true);
+        total += whole[b].work;
+    }
+    // split the h2f copies of the blocks whose whole chain exceeds the fair share of the step (one
+    // copy per device, so at least K devices), longest chain first; every split adds the extra
+    // factorisations to the total, so the share is re-evaluated after each
+    if (K > 1 && G >= K) {
+        std::vector<int32_t> byc;
+        for (int b = 0; b < nb; ++b)
+            if (m[b] > 0) byc.push_back(b);
+        std::stable_sort(byc.begin(), byc.end(), [&](int32_t x, int32_t y) { return whole[x].chain > whole[y].chain; });
+        for (int32_t b : byc) {
+            const double share = total / (kBusy * G);
+            if (whole[b].chain <= share || unit[b].chain >= whole[b].chain) break;
+            split[b] = 1;
+            total += K * unit[b].work - whole[b].work;
+        }
+    }
+    for (int b = 0; b < nb; ++b) chain_floor = std::max(chain_floor, split[b] ? unit[b].chain : whole[b].chain);
+    // LPT on the predicted device time max(work / busy, longest chain): units by that cost, each to
+    // the device where it ends earliest; a split block's copies on distinct devices
+    struct U { int32_t b, c; Cost k; double key; };
+    std::vector<U> us;
+    for (int b = 0; b < nb; ++b) {
+        if (m[b] <= 0) continue;
+        if (split[b])
+            for (int c = 0; c < K; ++c) us.push_back({b, c, unit[b], std::max(unit[b].work / kBusy, unit[b].chain)});
+        else
+            us.push_back({b, -1, whole[b], std::max(whole[b].work / kBusy, whole[b].chain)});
+    }
+    std::stable_sort(us.begin(), us.end(), [](const U& x, const U& y) { return x.key > y.key; });
+    std::vector<double> work(G, 0.0), chain(G, 0.0);
+    for (const U& u : us) {
+        int best = -1;
+        double bt = 0.0;
+        for (int d = 0; d < G; ++d) {
+            if (u.c >= 0) {   // a copy of this block already on d?
+                bool taken = false;
+                for (int c = 0; c < K; ++c) taken |= unit_device[static_cast<size_t>(u.b) * K + c] == d;
+                if (taken) continue;
+            }
+            const double t = std::max((work[d] + u.k.work) / kBusy, std::max(chain[d], u.k.chain));
+            if (best < 0 || t < bt - 1e-12) { best = d; bt = t; }
+        }
+        work[best] += u.k.work;
+        chain[best] = std::max(chain[best], u.k.chain);
+        if (u.c >= 0) unit_device[static_cast<size_t>(u.b) * K + u.c] = best;
+        else
+            for (int c = 0; c < K; ++c) unit_device[static_cast<size_t>(u.b) * K + c] = best;
+    }
+    for (int d = 0; d < G; ++d) dev_ms[d] = std::max(work[d] / kBusy, chain[d]);
+    (void)chain_floor;
+}
+}  // namespace shard
+
+// ---------------------------------------------------------------- jobs
+// Run f(i) for every job index on its own host thread; the first failing rc wins and its job's
+// context message is copied to the parent context.
 template <typename F>
-static int fan_out(dbslmm_ctx* ctx, int n, F f) {
+static int fan_out(dbslmm_plan* p, F f) {
+    auto& S = p->mp->shards;
+    const int n = static_cast<int>(S.size());
     std::vector<int> rc(n, DBSLMM_OK);
     std::vector<std::thread> th;
     th.reserve(n);
@@ -29,13 +153,17 @@ static int fan_out(dbslmm_ctx* ctx, int n, F f) {
     for (auto& t : th) t.join();
     for (int i = 0; i < n; ++i)
         if (rc[i] != DBSLMM_OK) {
-            ctx->err = "device " + std::to_string(ctx->subs[i]->device) + ": " + ctx->subs[i]->err;
+            dbslmm_ctx* jc = S[i].plan ? S[i].plan->ctx : S[i].ctx;
+            p->ctx->err = "device " + std::to_string(jc ? jc->device : -1) + ": " + (jc ? jc->err : std::string("?"));
             return rc[i];
         }
     return DBSLMM_OK;
 }
 
-static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out) {
+// The jobs of the devices in `devs` (device index d -> context dev_ctx[d]) for a shard plan.
+static int mp_build(dbslmm_ctx* ctx, const dbslmm_problem* pr, int32_t K, const std::vector<int32_t>& unit_device,
+                    const std::vector<int>& devs, const std::vector<dbslmm_ctx*>& dev_ctx, bool partial,
+                    dbslmm_plan** out) {
     ARG_CHECK(ctx, pr && out, "null problem/out");
     *out = nullptr;
     ARG_CHECK(ctx, pr->bed && pr->n_ref > 1 && pr->n_obs > 0 && pr->num_block >= 0, "bad sizes");
@@ -45,25 +173,6 @@ static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** ou
     const int64_t bps = pr->n_ref / 4 + (pr->n_ref % 4 ? 1 : 0);
     ARG_CHECK(ctx, pr->bed_len >= 3 + bps, "bed image shorter than one SNP row");
     const int64_t n_rows = (pr->bed_len - 3) / bps;
-    const int G = static_cast<int>(ctx->subs.size());
-    // 1. LPT shard of the non-empty blocks
-    std::vector<double> cost(pr->num_block, 0.0);
-    std::vector<int32_t> order;
-    for (int b = 0; b < pr->num_block; ++b) {
-        const int64_t ms = pr->s_ptr[b + 1] - pr->s_ptr[b], ml = has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0;
-        ARG_CHECK(ctx, ms >= 0 && ml >= 0, "CSR offsets not monotone");
-        const double m = static_cast<double>(ms + ml);
-        cost[b] = pr->n_ref * m * (m + 1.0) + m * m * m / 3.0;
-        if (ms + ml > 0) order.push_back(b);
-    }
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
-    std::vector<double> load(G, 0.0);
-    std::vector<std::vector<int32_t>> own(G);
-    for (int32_t b : order) {
-        const int d = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-        own[d].push_back(b);
-        load[d] += cost[b];
-    }
     auto* p = new dbslmm_plan();
     p->ctx = ctx;
     p->n_ref = pr->n_ref;
@@ -74,8 +183,38 @@ static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** ou
     p->n_s = pr->s_ptr[pr->num_block];
     p->n_l = has_l ? pr->l_ptr[pr->num_block] : 0;
     p->mp = new dbslmm_mplan();
-    p->mp->shards.resize(G);
-    // 2. sub-problems with compact .bed images (rows renumbered in first-use order)
+    p->mp->n_copies = K;
+    p->mp->partial = partial;
+    p->mp->unit_device = unit_device;
+    // jobs: per device its whole blocks (copy -1), then one job per split unit (copy c)
+    auto& J = p->mp->shards;
+    for (int d : devs) {
+        DeviceShard main_job;
+        main_job.device_index = d;
+        main_job.ctx = dev_ctx[d];
+        for (int b = 0; b < pr->num_block; ++b) {
+            const int32_t* ud = unit_device.data() + static_cast<size_t>(b) * K;
+            bool whole = ud[0] == d;
+            for (int c = 1; c < K; ++c) whole &= ud[c] == d;
+            if (whole) main_job.blocks.push_back(b);
+        }
+        J.push_back(std::move(main_job));
+        for (int b = 0; b < pr->num_block; ++b) {
+            const int32_t* ud = unit_device.data() + static_cast<size_t>(b) * K;
+            bool whole = true;
+            for (int c = 1; c < K; ++c) whole &= ud[c] == ud[0];
+            if (whole) continue;
+            for (int c = 0; c < K; ++c)
+                if (ud[c] == d) {
+                    DeviceShard u;
+                    u.device_index = d;
+                    u.copy = c;
+                    u.blocks.push_back(b);
+                    J.push_back(std::move(u));
+                }
+        }
+    }
+    // sub-problems with compact .bed images (rows renumbered in first-use order)
     struct Sub {
         std::vector<uint8_t> bed;
         std::vector<int64_t> s_ptr, l_ptr;
@@ -83,12 +222,10 @@ static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** ou
         std::vector<double> z_s, z_l;
         dbslmm_problem prob{};
     };
-    std::vector<Sub> subs(G);
-    for (int d = 0; d < G; ++d) {
-        DeviceShard& sh = p->mp->shards[d];
-        Sub& su = subs[d];
-        std::sort(own[d].begin(), own[d].end());   // block order within the shard
-        sh.blocks = own[d];
+    std::vector<Sub> subs(J.size());
+    for (size_t j = 0; j < J.size(); ++j) {
+        DeviceShard& sh = J[j];
+        Sub& su = subs[j];
         std::unordered_map<int32_t, int32_t> remap;
         std::vector<int32_t> rows;
         auto local = [&](int32_t r) -> int32_t {
@@ -143,33 +280,74 @@ static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** ou
         }
         q.opts = pr->opts;
     }
-    // 3. shard plans, one host thread per device
-    const int rc = fan_out(ctx, G, [&](int d) -> int {
-        return dbslmm_plan_create(ctx->subs[d], &subs[d].prob, &p->mp->shards[d].plan);
+    // job plans, one host thread each; a split unit runs on a context of its own on its device
+    // (own streams: it runs beside the device's other jobs, its chain on high-priority streams)
+    const int rc = fan_out(p, [&](int j) -> int {
+        DeviceShard& sh = J[j];
+        if (sh.copy >= 0) {
+            const int r = dbslmm_ctx_create(dev_ctx[sh.device_index]->device, &sh.own_ctx);
+            if (r != DBSLMM_OK) return r;
+            sh.ctx = sh.own_ctx;
+        }
+        if (sh.blocks.empty()) return DBSLMM_OK;   // an idle device (more devices than blocks)
+        return dbslmm_plan_create(sh.ctx, &subs[j].prob, &sh.plan);
     });
     if (rc != DBSLMM_OK) { dbslmm_plan_destroy(p); return rc; }
+    // jobs without blocks hold no plan: dropped
+    J.erase(std::remove_if(J.begin(), J.end(), [](const DeviceShard& s) { return s.plan == nullptr; }), J.end());
     p->ran = false;
     *out = p;
     return DBSLMM_OK;
 }
 
+static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out) {
+    ARG_CHECK(ctx, pr && out && pr->s_ptr && pr->num_block >= 0, "null problem/out");
+    const bool has_l = pr->l_ptr != nullptr;
+    std::vector<int32_t> m(pr->num_block);
+    for (int b = 0; b < pr->num_block; ++b) {
+        const int64_t ms = pr->s_ptr[b + 1] - pr->s_ptr[b], ml = has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0;
+        ARG_CHECK(ctx, ms >= 0 && ml >= 0, "CSR offsets not monotone");
+        m[b] = static_cast<int32_t>(ms + ml);
+    }
+    const int G = static_cast<int>(ctx->subs.size());
+    const int32_t K = pr->opts && pr->opts->shard_copies > 1 ? pr->opts->shard_copies : 1;
+    ARG_CHECK(ctx, K <= 64, "shard_copies must be <= 64");
+    std::vector<int32_t> ud;
+    std::vector<double> dev_ms;
+    shard::plan_units(pr->num_block, m.data(), pr->n_ref, G, K, ud, dev_ms);
+    std::vector<int> devs(G);
+    std::iota(devs.begin(), devs.end(), 0);
+    return mp_build(ctx, pr, K, ud, devs, ctx->subs, false, out);
+}
+
 static void mp_destroy(dbslmm_plan* p) {
-    for (DeviceShard& sh : p->mp->shards) dbslmm_plan_destroy(sh.plan);
+    for (DeviceShard& sh : p->mp->shards) {
+        dbslmm_plan_destroy(sh.plan);
+        dbslmm_ctx_destroy(sh.own_ctx);
+    }
     delete p->mp;
     p->mp = nullptr;
 }
 
-// beta / status of one solve, scattered from every shard into the caller's arrays
+// job j's plan copy holding the caller's h2f copy c in the last run (-1: none)
+static int job_copy(const DeviceShard& sh, int c) {
+    for (size_t k = 0; k < sh.run_copies.size(); ++k)
+        if (sh.run_copies[k] == c) return static_cast<int>(k);
+    return -1;
+}
+
+// beta / status of one solve, scattered from every job into the caller's arrays
 static int mp_download(dbslmm_plan* p, int copy, double* beta_s, double* beta_l, int32_t* block_status) {
-    dbslmm_ctx* ctx = p->ctx;
     auto& S = p->mp->shards;
-    if (block_status)
+    if (block_status && !p->mp->partial)
         for (int32_t b = 0; b < p->num_block; ++b) block_status[b] = DBSLMM_BLOCK_EMPTY;
-    return fan_out(ctx, static_cast<int>(S.size()), [&](int d) -> int {
+    return fan_out(p, [&](int d) -> int {
         DeviceShard& sh = S[d];
+        const int jc = job_copy(sh, copy);
+        if (jc < 0) return DBSLMM_OK;
         std::vector<double> bs(sh.s_idx.size()), bl(sh.l_idx.size());
         std::vector<int32_t> st(sh.blocks.size());
-        const int rc = download_copy(sh.plan, copy, bs.data(), bl.data(), st.data());
+        const int rc = download_copy(sh.plan, jc, bs.data(), bl.data(), st.data());
         if (rc != DBSLMM_OK) return rc;
         if (beta_s) for (size_t i = 0; i < bs.size(); ++i) beta_s[sh.s_idx[i]] = bs[i];
         if (beta_l) for (size_t i = 0; i < bl.size(); ++i) beta_l[sh.l_idx[i]] = bl[i];
@@ -178,16 +356,30 @@ static int mp_download(dbslmm_plan* p, int copy, double* beta_s, double* beta_l,
     });
 }
 
+// n solves: with n == the plan's copies every job solves its own copies (a split unit: its copy
+// alone, factored directly); otherwise a split block is solved whole by the job of its copy 0
 static int mp_run(dbslmm_plan* p, const double* sigmas, int n, bool wait) {
     auto& S = p->mp->shards;
-    const int rc = fan_out(p->ctx, static_cast<int>(S.size()), [&](int d) -> int {
-        dbslmm_plan* q = S[d].plan;
-        int r = run_impl(q, true, sigmas, n);
-        if (r == DBSLMM_OK && wait) r = dbslmm_plan_sync(q);
+    const int K = p->mp->n_copies;
+    const int rc = fan_out(p, [&](int d) -> int {
+        DeviceShard& sh = S[d];
+        sh.run_copies.clear();
+        if (sh.copy >= 0 && n == K) {
+            sh.run_copies.push_back(sh.copy);
+        } else if (sh.copy <= 0) {
+            for (int c = 0; c < n; ++c) sh.run_copies.push_back(c);
+        } else {
+            return DBSLMM_OK;     // another job solves this block's copies
+        }
+        std::vector<double> sg;
+        for (int c : sh.run_copies) sg.push_back(sigmas[c]);
+        int r = run_impl(sh.plan, true, sg.data(), static_cast<int>(sg.size()));
+        if (r == DBSLMM_OK && wait) r = dbslmm_plan_sync(sh.plan);
         return r;
     });
     if (rc == DBSLMM_OK) {
         p->ran = true;
+        p->stopped = false;
         p->var_copy = n - 1;
         p->sigma_run = sigmas[n - 1];
     }
@@ -196,7 +388,7 @@ static int mp_run(dbslmm_plan* p, const double* sigmas, int n, bool wait) {
 
 static int mp_sync(dbslmm_plan* p) {
     auto& S = p->mp->shards;
-    return fan_out(p->ctx, static_cast<int>(S.size()), [&](int d) -> int { return dbslmm_plan_sync(S[d].plan); });
+    return fan_out(p, [&](int d) -> int { return S[d].run_copies.empty() ? DBSLMM_OK : dbslmm_plan_sync(S[d].plan); });
 }
 
 static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diags, int32_t* n_test_out) {
@@ -209,19 +401,21 @@ static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diag
     if (n_test_out) *n_test_out = n_test;
     if (n_test == 0 || p->num_block == 0) return DBSLMM_OK;
     ARG_CHECK(ctx, diags, "null diags");
-    std::fill(diags, diags + static_cast<size_t>(n_test) * p->num_block, 0.0);
     auto& S = p->mp->shards;
-    // every shard's pending single-sigma re-run (graph captures) first, drained, then the variances
-    const int rc0 = fan_out(ctx, static_cast<int>(S.size()), [&](int d) -> int {
+    if (!p->mp->partial) std::fill(diags, diags + static_cast<size_t>(n_test) * p->num_block, 0.0);
+    // the jobs holding the last solve's factorisation (the caller's copy var_copy is their last)
+    auto holds = [&](const DeviceShard& sh) { return !sh.run_copies.empty() && sh.run_copies.back() == p->var_copy; };
+    // every job's pending single-sigma re-run (graph captures) first, drained, then the variances
+    const int rc0 = fan_out(p, [&](int d) -> int {
         dbslmm_plan* q = S[d].plan;
-        if (S[d].blocks.empty() || !q->cheb_pending_var) return DBSLMM_OK;
+        if (!holds(S[d]) || !q->cheb_pending_var) return DBSLMM_OK;
         const int r = variance_factor(q);
         return r == DBSLMM_OK ? dbslmm_plan_sync(q) : r;
     });
     if (rc0 != DBSLMM_OK) return rc0;
-    return fan_out(ctx, static_cast<int>(S.size()), [&](int d) -> int {
+    return fan_out(p, [&](int d) -> int {
         DeviceShard& sh = S[d];
-        if (sh.blocks.empty()) return DBSLMM_OK;
+        if (!holds(sh)) return DBSLMM_OK;
         std::vector<int32_t> sp(sh.s_idx.size()), lp(sh.l_idx.size());
         for (size_t i = 0; i < sp.size(); ++i) sp[i] = tp->s_pos[sh.s_idx[i]];
         for (size_t i = 0; i < lp.size(); ++i) lp[i] = tp->l_pos[sh.l_idx[i]];
@@ -244,11 +438,20 @@ static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diag
 static int mp_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int32_t n_ref, int64_t n_snp, double* maf) {
     const int64_t bps = n_ref / 4 + (n_ref % 4 ? 1 : 0);
     const int G = static_cast<int>(ctx->subs.size());
-    return fan_out(ctx, G, [&](int d) -> int {
-        const int64_t r0 = n_snp * d / G, r1 = n_snp * (d + 1) / G;
-        if (r1 == r0) return DBSLMM_OK;
-        return dbslmm_bed_maf(ctx->subs[d], bed + r0 * bps, 3 + (r1 - r0) * bps, n_ref, r1 - r0, maf + r0);
-    });
+    std::vector<int> rc(G, DBSLMM_OK);
+    std::vector<std::thread> th;
+    for (int d = 0; d < G; ++d)
+        th.emplace_back([&, d] {
+            const int64_t r0 = n_snp * d / G, r1 = n_snp * (d + 1) / G;
+            if (r1 > r0) rc[d] = dbslmm_bed_maf(ctx->subs[d], bed + r0 * bps, 3 + (r1 - r0) * bps, n_ref, r1 - r0, maf + r0);
+        });
+    for (auto& t : th) t.join();
+    for (int d = 0; d < G; ++d)
+        if (rc[d] != DBSLMM_OK) {
+            ctx->err = "device " + std::to_string(ctx->subs[d]->device) + ": " + ctx->subs[d]->err;
+            return rc[d];
+        }
+    return DBSLMM_OK;
 }
 
 extern "C" {
@@ -283,10 +486,50 @@ int dbslmm_plan_shard_info(const dbslmm_plan* p, int32_t* block_device) {
         for (int32_t b = 0; b < p->num_block; ++b) block_device[b] = 0;
         return DBSLMM_OK;
     }
+    const int K = p->mp->n_copies;
     for (int32_t b = 0; b < p->num_block; ++b) block_device[b] = -1;   // empty blocks
-    for (size_t d = 0; d < p->mp->shards.size(); ++d)
-        for (int32_t b : p->mp->shards[d].blocks) block_device[b] = static_cast<int32_t>(d);
+    for (const DeviceShard& sh : p->mp->shards)
+        for (int32_t b : sh.blocks)
+            if (sh.copy <= 0) block_device[b] = p->mp->unit_device[static_cast<size_t>(b) * K];
     return DBSLMM_OK;
+}
+
+int dbslmm_shard_plan(int32_t num_block, const int32_t* m, int32_t n_ref, int32_t n_dev, int32_t n_copies,
+                      int32_t* unit_device, double* dev_ms) {
+    if (num_block < 0 || (num_block > 0 && !m) || n_ref <= 1 || n_dev <= 0 || n_copies < 1 || n_copies > 64 ||
+        !unit_device)
+        return DBSLMM_E_ARG;
+    for (int32_t b = 0; b < num_block; ++b)
+        if (m[b] < 0) return DBSLMM_E_ARG;
+    std::vector<int32_t> ud;
+    std::vector<double> ms;
+    shard::plan_units(num_block, m, n_ref, n_dev, n_copies, ud, ms);
+    std::copy(ud.begin(), ud.end(), unit_device);
+    if (dev_ms) std::copy(ms.begin(), ms.end(), dev_ms);
+    return DBSLMM_OK;
+}
+
+int dbslmm_plan_create_units(dbslmm_ctx* ctx, const dbslmm_problem* pr, int32_t n_copies, const int32_t* unit_device,
+                             int32_t device_index, dbslmm_plan** out) {
+    if (!ctx) return DBSLMM_E_ARG;
+    ARG_CHECK(ctx, ctx->subs.empty(), "dbslmm_plan_create_units takes a single-device context");
+    ARG_CHECK(ctx, pr && out && unit_device && n_copies >= 1 && n_copies <= 64 && device_index >= 0,
+              "null problem/out/unit_device, or n_copies / device_index out of range");
+    if (const int rc = ctx_ready(ctx)) return rc;
+    ARG_CHECK(ctx, pr->num_block >= 0 && pr->s_ptr, "bad sizes");
+    const bool has_l = pr->l_ptr != nullptr;
+    std::vector<int32_t> ud(unit_device, unit_device + static_cast<size_t>(pr->num_block) * n_copies);
+    for (int b = 0; b < pr->num_block; ++b) {
+        const bool empty = pr->s_ptr[b + 1] == pr->s_ptr[b] && (!has_l || pr->l_ptr[b + 1] == pr->l_ptr[b]);
+        for (int c = 0; c < n_copies; ++c) {
+            const int32_t d = ud[static_cast<size_t>(b) * n_copies + c];
+            ARG_CHECK(ctx, empty ? d == -1 || d >= 0 : d >= 0, "unit_device: a non-empty block's unit without a device");
+            if (empty) ud[static_cast<size_t>(b) * n_copies + c] = -1;
+        }
+    }
+    std::vector<dbslmm_ctx*> dev_ctx(device_index + 1, nullptr);
+    dev_ctx[device_index] = ctx;
+    return mp_build(ctx, pr, n_copies, ud, {device_index}, dev_ctx, true, out);
 }
 
 }  // extern "C"

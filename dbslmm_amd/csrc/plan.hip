@@ -44,7 +44,9 @@ namespace {
 // events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large,
 // [4] / [5] around chol_small (main stream), [6] / [8] around the tiled factorisation sequence,
 // [8] / [7] around the h2f Chebyshev iterations (stream2)
-constexpr int kEvPerRun = 11;   // 9, 10: around the lead group's Gram (between the unpack halves)
+constexpr int kEvPerRun = 12;   // 9, 10: around the lead group's Gram (between the unpack halves);
+                                // 11: the rest group's factorisation + backward done (its own
+                                // stream, split substitutions; else recorded with 8)
 constexpr size_t kCholLargeLds = sizeof(double) * chol::kLargeDoubles;
 constexpr size_t kCholChebLds = sizeof(double) * chol::kChebLdsDoubles;
 constexpr size_t kTiledLds = sizeof(double) * chol::kTiledDoubles;
@@ -60,6 +62,7 @@ constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here 
 constexpr int kTChebMaxM = 4096;         // whole-block Chebyshev passes: blocks of <= 64 tiles
 constexpr int kLeadMinDefault = 1536;    // lead group: m >= max(this, m_max / 8) (dbslmm_options.lead_min)
 constexpr int kXcd = 8;                 // workgroup id e runs on XCD e % 8
+constexpr int kEpochsPerRun = 1 << 14;  // substitution epochs one run may take (next_epoch)
 
 // one launch of the tiled sequence: the active blocks and the prefix of their work items
 struct TLaunch {
@@ -119,14 +122,23 @@ struct dbslmm_ctx {
     bool setup_ok = true;
 };
 struct dbslmm_plan;
-// the shards of a multi-device plan (multi.hip)
+// the jobs of a multi-device (or units) plan (multi.hip): one plan each
 struct DeviceShard {
     dbslmm_plan* plan = nullptr;
+    dbslmm_ctx* ctx = nullptr;          // the context the job's plan runs on
+    dbslmm_ctx* own_ctx = nullptr;      // ... created for a split unit (owned by the job)
+    int device_index = 0;               // in the shard plan's device numbering
+    int copy = -1;                      // -1: every h2f copy of its blocks; c: that copy of one block
     std::vector<int32_t> blocks;        // original block ids, in sub-problem order
     std::vector<int64_t> s_idx, l_idx;  // sub small / large SNP -> original beta position
+    std::vector<int> run_copies;        // the caller's h2f copy of each of the plan's copies (last run)
 };
 struct dbslmm_mplan {
     std::vector<DeviceShard> shards;
+    int32_t n_copies = 1;               // h2f copies per run the units were planned for
+    bool partial = false;               // one device's units (dbslmm_plan_create_units): outputs of
+                                        // the other units are left untouched
+    std::vector<int32_t> unit_device;   // [block * n_copies + copy] -> device index, -1 empty
 };
 
 struct dbslmm_plan {
@@ -236,6 +248,7 @@ struct dbslmm_plan {
     double ms_acc[DBSLMM_K_COUNT] = {0, 0, 0, 0, 0, 0};
     int32_t ms_runs = 0;
     bool ran = false;
+    bool stopped = false;          // the last run stopped after the Gram (debug_stop = 1): no betas
 };
 
 #define HIP_TRY(ctx, expr)                                                               \
@@ -850,7 +863,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    (op.large_cheb == 0 || op.large_cheb == -1) && (op.cheb_fused == 0 || op.cheb_fused == 1) &&
                    op.debug_delay_us >= -100000 && op.debug_delay_us <= 100000 &&
                    (op.debug_stop == 0 || op.debug_stop == 1) && op.sub_split >= -1 && op.sub_split <= 2 &&
-                   op.sub_grid_lead >= 0 && op.sub_grid_rest >= 0, "bad dbslmm_options");
+                   op.sub_grid_lead >= 0 && op.sub_grid_rest >= 0 && op.shard_copies >= 0 &&
+                   op.shard_copies <= 64, "bad dbslmm_options");
     p->h2f_mode = op.h2f_mode;
     p->cheb_fused = op.cheb_fused == 1;
     p->debug_delay_us = op.debug_delay_us;
@@ -1111,7 +1125,8 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         // (config 4, same box: one sequence 45.1-45.5 ms per step; split on 64 / 192 workgroups
         // 43.9-44.1; 96 / 160 44.9; 128 / 128 47.1; a rest grid of every CU 51-56 -- its
         // persistent workgroups then hold the CUs the lead factorisation's tail still needs)
-        p->sub_split = op.sub_split >= 0 && !p->tl_rest.empty();
+        // (cheb_fused = 1 runs every Chebyshev pass of ALL tiled items in one launch: no groups)
+        p->sub_split = op.sub_split >= 0 && !p->tl_rest.empty() && !p->cheb_fused;
         p->sub_grid_lead = op.sub_grid_lead > 0 ? op.sub_grid_lead : std::max(1, ctx->n_cu * 5 / 16);
         p->sub_grid_rest = op.sub_grid_rest > 0 ? op.sub_grid_rest : std::max(1, ctx->n_cu - p->sub_grid_lead);
         auto grp_of = [&](int32_t b) { return p->sub_split && mv[b] < lead_min ? 1 : 0; };
@@ -1267,12 +1282,14 @@ static int collect_timing(dbslmm_plan* p) {
     dbslmm_ctx* ctx = p->ctx;
     for (int r = 0; r < p->runs_pending; ++r) {
         hipEvent_t* e = &p->ev[kEvPerRun * r];
-        const int from[DBSLMM_K_COUNT] = {0, 1, 2, 4, 6, 8}, to[DBSLMM_K_COUNT] = {1, 2, 3, 5, 8, 7};
-        for (int k = 0; k < DBSLMM_K_COUNT; ++k) {
-            float ms = 0.f;
-            HIP_TRY(ctx, hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
-            p->ms_acc[k] += ms;
-        }
+        // event times from the run's start; with split substitutions the tiled factorisation +
+        // backward of the two groups ends on two streams (8: lead, 11: rest) and the Chebyshev
+        // passes start there: tiled = 6 -> max(8, 11), trsv = min(8, 11) -> 7 (the spans overlap)
+        float t[kEvPerRun] = {0.f};
+        for (int k = 1; k < kEvPerRun; ++k) HIP_TRY(ctx, hipEventElapsedTime(&t[k], e[0], e[k]));
+        const float fend = std::max(t[8], t[11]), cstart = std::min(t[8], t[11]);
+        const float span[DBSLMM_K_COUNT] = {t[1], t[2] - t[1], t[3] - t[2], t[5] - t[4], fend - t[6], t[7] - cstart};
+        for (int k = 0; k < DBSLMM_K_COUNT; ++k) p->ms_acc[k] += span[k];
         // the lead group's Gram (9 -> 10) sits between the two unpack launches (0 -> 1)
         float lg = 0.f;
         HIP_TRY(ctx, hipEventElapsedTime(&lg, e[9], e[10]));
@@ -1410,6 +1427,18 @@ static TGroup tgroup_rest(const dbslmm_plan* p) {
     return TGroup{p->n_titems_lead, ni, p->n_tb_lead, p->n_tiled - p->n_tb_lead, p->ctx->stream4,
                   p->d_tflags + p->n_tflags + 2, std::max(1, std::min(g, ni))};
 }
+// The substitution epochs of one run (tile-flag values, trsv.hip): run_impl resets the flags ahead
+// of the fork whenever the counter is within kEpochsPerRun of wrapping, so inside a run the counter
+// only grows.  Bound: 64 copies' backward solves + 2 groups x 32 copy groups x 2 x 60 passes.
+static int next_epoch(dbslmm_plan* p, int k) {
+    if (p->trsv_epoch > INT32_MAX - k) {   // unreachable unless a run exceeds kEpochsPerRun
+        p->ctx->err = "substitution epoch counter overflow within one run";
+        return DBSLMM_E_STATE;
+    }
+    p->trsv_epoch += k;
+    return DBSLMM_OK;
+}
+
 static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     dbslmm_ctx* ctx = p->ctx;
     hipStream_t st = grp.st;
@@ -1446,11 +1475,7 @@ static int run_pbwd(dbslmm_plan* p, double isn, int copy, const TGroup& grp) {
     a.cix[0] = copy;
     a.status = p->d_status + c * p->nbk;
     a.mode = 1;
-    if (++p->trsv_epoch == INT32_MAX) {
-        HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
-        HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), st));
-        p->trsv_epoch = 1;
-    }
+    if (const int rc = next_epoch(p, 1)) return rc;
     a.epoch = p->trsv_epoch;
     if (a.n_items > 0) {
         launch_trsv<1>(false, a.grid, st, a);
@@ -1723,11 +1748,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
             for (int k = 0; k < K; ++k)
                 for (int pass = 0; pass < 2; ++pass) {
                     const bool fwd = pass == 0;
-                    if (++p->trsv_epoch == INT32_MAX) {   // flags restart from a clean slate
-                        HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
-                        HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), st));
-                        p->trsv_epoch = 1;
-                    }
+                    if (const int rc = next_epoch(p, 1)) return rc;
                     a.epoch = p->trsv_epoch;
                     a.items = (fwd ? p->d_tri_f : p->d_tri_b) + 2 * grp.item_off;
                     a.src = fwd ? R : Y;
@@ -1746,13 +1767,8 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
         a.n_items = p->n_cheb_items;
         a.grid = std::max(1, std::min(ctx->n_cu, p->n_cheb_items));
         // passes 0 .. 2K-1 run at epochs epoch .. epoch + 2K - 1 (flags and update flags only grow)
-        if (p->trsv_epoch + 2 * K + 2 >= INT32_MAX) {
-            HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), st));
-            HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), st));
-            p->trsv_epoch = 0;
-        }
         a.epoch = p->trsv_epoch + 1;
-        p->trsv_epoch += 2 * K;
+        if (const int rc = next_epoch(p, 2 * K)) return rc;
         if (nr == 1) hipLaunchKernelGGL(dbslmm_trsv_cheb<1>, dim3(a.grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
         else hipLaunchKernelGGL(dbslmm_trsv_cheb<2>, dim3(a.grid), dim3(trsv::kThreads), trsv::kLdsBytes, st, a);
         HIP_TRY(ctx, hipGetLastError());
@@ -1852,6 +1868,18 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         p->runs_pending++;
     }
     const size_t nbk = static_cast<size_t>(p->nbk);
+    // Substitution tile flags are epochs (trsv.hip): a run takes at most kEpochsPerRun of them
+    // (backward solves and Chebyshev passes of every group and copy).  When the counter could wrap
+    // during this run, the flags restart from a clean slate HERE, on the main stream: every stream
+    // of the run forks from it after this point and every stream of the previous run has joined
+    // it, so no substitution launch of either group can still be running (a reset inside a group
+    // would race the other group's launch on its own stream).
+    if (p->n_tflags > 0 && p->trsv_epoch > INT32_MAX - kEpochsPerRun) {
+        HIP_TRY(ctx, hipMemsetAsync(p->d_tflags, 0, p->n_tflags * sizeof(int32_t), s));
+        HIP_TRY(ctx, hipMemsetAsync(p->d_tepi, 0, p->n_tflags * sizeof(int32_t), s));
+        p->trsv_epoch = 0;
+    }
+    p->stopped = false;
     if (front) HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
     HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, n * nbk * sizeof(int32_t), s));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], s));
@@ -1948,9 +1976,10 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     // (the factorisation overwrites its matrix: the Gram epilogues write all n copies)
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], s));
     if (p->debug_stop == 1) {   // tests: the block matrices hold Sigma (dbslmm_plan_block_matrix)
-        for (int k : {3, 4, 5, 6, 8, 7})
+        for (int k : {3, 4, 5, 6, 8, 11, 7})
             if (ev) HIP_TRY(ctx, hipEventRecord(ev[k], s));
         p->ran = true;
+        p->stopped = true;      // download / variance refuse: the betas of this run were never computed
         return DBSLMM_OK;
     }
     if (p->n_nonempty > 0) {
@@ -2028,6 +2057,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                     // factorisation, the lead group's on stream2 after the lead factorisation
                     const TGroup gr = tgroup_rest(p), gl = tgroup_lead(p);
                     if (rc == DBSLMM_OK && gr.n_items > 0) rc = run_pbwd(p, isn, fcopy, gr);
+                    if (ev && cheb) HIP_TRY(ctx, hipEventRecord(ev[11], gr.st));
                     if (rc == DBSLMM_OK && cheb && gr.n_items > 0)
                         rc = p->sub_block ? run_tcheb(p, isn, cp, gr.st) : run_cheb(p, isn, cp, gr);
                     if (rc == DBSLMM_OK) rc = run_pbwd(p, isn, fcopy, gl);
@@ -2049,6 +2079,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                     if (rc != DBSLMM_OK) return rc;
                     if (cheb) {
                         if (ev) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+                        if (ev) HIP_TRY(ctx, hipEventRecord(ev[11], ctx->stream2));
                         rc = run_cheb(p, isn, cp, tgroup_all(p));
                         if (rc != DBSLMM_OK) return rc;
                     }
@@ -2061,6 +2092,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             }
         }
         if (ev && !cheb) HIP_TRY(ctx, hipEventRecord(ev[8], ctx->stream2));
+        if (ev && !cheb) HIP_TRY(ctx, hipEventRecord(ev[11], ctx->stream2));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[7], ctx->stream2));
         HIP_TRY(ctx, hipEventRecord(ctx->join3, ctx->stream2));
         if (ss != s) HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
@@ -2072,6 +2104,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         HIP_TRY(ctx, hipEventRecord(ev[5], s));
         HIP_TRY(ctx, hipEventRecord(ev[6], s));
         HIP_TRY(ctx, hipEventRecord(ev[8], s));
+        HIP_TRY(ctx, hipEventRecord(ev[11], s));
         HIP_TRY(ctx, hipEventRecord(ev[7], s));
     }
     p->ran = true;
@@ -2118,6 +2151,7 @@ static int check_trsv(dbslmm_plan* p) {
 static int download_copies(dbslmm_plan* p, int c0, int n, double* beta_s, double* beta_l, int32_t* block_status) {
     dbslmm_ctx* ctx = p->ctx;
     if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
+    if (p->stopped) { ctx->err = "plan_download after a run stopped at the Gram (debug_stop)"; return DBSLMM_E_STATE; }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (const int rc = check_trsv(p)) return rc;
@@ -2247,13 +2281,15 @@ extern "C" int dbslmm_diag_trsv_stamps(dbslmm_plan* p, unsigned long long* out, 
 
 int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     if (!p || !out) return DBSLMM_E_ARG;
-    if (p->mp) {   // sums over the devices; [12] launches, [14] iterations: the max; [15] device 0's
+    if (p->mp) {   // sums over the jobs; [12] launches, [14] iterations: the max; [15] job 0's;
+                   // SNPs [0] and blocks [6] once per block (not per split h2f copy)
         for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = 0.0;
         for (auto& sh : p->mp->shards) {
             double w[DBSLMM_WORKLOAD_LEN];
             dbslmm_plan_workload(sh.plan, w);
             for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i)
-                out[i] = (i == 12 || i == 14) ? std::max(out[i], w[i]) : out[i] + w[i];
+                out[i] = (i == 12 || i == 14) ? std::max(out[i], w[i])
+                         : ((i == 0 || i == 6) && sh.copy > 0) ? out[i] : out[i] + w[i];
         }
         double w0[DBSLMM_WORKLOAD_LEN];
         dbslmm_plan_workload(p->mp->shards[0].plan, w0);
@@ -2334,6 +2370,7 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     if (!p) return DBSLMM_E_ARG;
     dbslmm_ctx* ctx = p->ctx;
     if (!p->ran) { ctx->err = "plan_variance before plan_run"; return DBSLMM_E_STATE; }
+    if (p->stopped) { ctx->err = "plan_variance after a run stopped at the Gram (debug_stop)"; return DBSLMM_E_STATE; }
     if (p->mp) return mp_variance(p, tp, diags, n_test_out);
     ARG_CHECK(ctx, tp && tp->bed && tp->indicator && tp->n_total > 0, "bad test panel");
     if (const int rc = variance_factor(p)) return rc;

@@ -1,40 +1,85 @@
-"""Multi-GPU solve of one problem: LD blocks sharded across ranks, beta gathered to rank 0.
+"""Multi-GPU solve of one problem: (LD block, h2f copy) units sharded across ranks, beta gathered
+to rank 0.
 
 The reference parallelises only over LD blocks (OpenMP `schedule(dynamic)` over batches of 60,
-scr/dbslmmfit.cpp:191-220); blocks are independent, so a multi-GPU solve needs no exchange
-during compute.  One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI):
+scr/dbslmmfit.cpp:189-220) and runs each h2f factor as its own dbslmm process
+(software/DBSLMM.R:204-219); both are independent, so a multi-GPU solve needs no exchange during
+compute.  One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI):
 
-1. every rank computes the same longest-processing-time assignment of blocks to ranks
-   (cost ~ n_ref*m^2 for the Gram + m^3/3 for the factorisation);
-2. each rank solves its sub-problem on its own GPU (a BlockProblem restricted to its blocks);
-3. the betas (fp64, <= 8 MB at 1M SNPs) are gathered to rank 0 in the original order -- the only
-   collective, one padded `gather` of [index, beta] pairs.
+1. every rank computes the same shard plan (`shard_units`: the library's dbslmm_shard_plan, a time
+   model of one MI355X -- per-block chip time of each kernel class plus the block's dependency
+   chain alone; a block's h2f copies are split over devices only when its chain exceeds the fair
+   share of the step);
+2. each rank solves its units on its own GPU (`Plan.units`: its whole blocks in one plan, each split
+   copy in a single-copy plan on its own streams beside it);
+3. the betas (fp64, <= 8 MB per h2f solve at 1M SNPs) are gathered to rank 0 in the original order
+   -- the only collective, one `gather` of this rank's unit values per step.
 """
 from __future__ import annotations
 
-import heapq
+import ctypes as C
 
 import numpy as np
 
 
 def block_cost(m: np.ndarray, n_ref: int) -> np.ndarray:
+    """Cost of a block for the REFERENCE's CPU path (Gram n_ref m (m+1) + factorisation m^3 / 3):
+    bench.py's CPU baseline samples blocks with it.  (The GPU shard plan uses the library's time
+    model instead: shard_units.)"""
     m = np.asarray(m, dtype=np.float64)
     return n_ref * m * (m + 1) + m ** 3 / 3.0
 
 
+def shard_units(m_per_block, n_ref: int, world: int, n_copies: int = 1):
+    """The library's shard plan (dbslmm_shard_plan; host only, deterministic): returns
+    unit_device [num_block, n_copies] (device of copy c of block b, -1 for an empty block) and the
+    model's predicted step of every device in ms."""
+    from . import _lib
+    L = _lib.load()
+    m = np.ascontiguousarray(m_per_block, dtype=np.int32)
+    ud = np.zeros((m.size, n_copies), dtype=np.int32)
+    ms = np.zeros(world, dtype=np.float64)
+    rc = L.dbslmm_shard_plan(m.size, m.ctypes.data_as(C.c_void_p), int(n_ref), int(world), int(n_copies),
+                             ud.ctypes.data_as(C.c_void_p), ms.ctypes.data_as(C.c_void_p))
+    if rc != 0:
+        raise _lib.DbslmmError(f"dbslmm_shard_plan failed rc={rc}")
+    return ud, ms
+
+
 def shard_blocks(m_per_block: np.ndarray, n_ref: int, world: int) -> list[np.ndarray]:
-    """LPT: blocks sorted by cost, each to the least-loaded rank.  Deterministic."""
-    cost = block_cost(m_per_block, n_ref)
-    order = np.lexsort((np.arange(len(cost)), -cost))
-    heap = [(0.0, r) for r in range(world)]
-    owned = [[] for _ in range(world)]
-    for b in order:
-        if m_per_block[b] == 0:
-            continue
-        load, r = heapq.heappop(heap)
-        owned[r].append(int(b))
-        heapq.heappush(heap, (load + cost[b], r))
-    return [np.array(sorted(o), dtype=np.int64) for o in owned]
+    """Single-solve shard plan: the blocks of each rank (block order)."""
+    ud, _ = shard_units(m_per_block, n_ref, world, 1)
+    return [np.flatnonzero(ud[:, 0] == r).astype(np.int64) for r in range(world)]
+
+
+def rank_jobs(unit_device: np.ndarray, rank: int):
+    """The jobs of `rank` (the decomposition dbslmm_plan_create_units builds, multi.hip mp_build):
+    [(blocks, copies)] -- first its whole blocks with every copy, then one job per split unit
+    (one block, one copy)."""
+    ud = np.asarray(unit_device)
+    K = ud.shape[1]
+    whole = np.all(ud == ud[:, :1], axis=1)
+    jobs = [(np.flatnonzero(whole & (ud[:, 0] == rank)), list(range(K)))]
+    for b in np.flatnonzero(~whole):
+        for c in range(K):
+            if ud[b, c] == rank:
+                jobs.append((np.array([b]), [c]))
+    return [j for j in jobs if j[0].size]
+
+
+def unit_index(prob, unit_device: np.ndarray, rank: int):
+    """Per copy c: the positions in the full [beta_s | beta_l] vector that `rank` solves."""
+    ud = np.asarray(unit_device)
+    n_s = prob.n_s
+    out = []
+    for c in range(ud.shape[1]):
+        idx = []
+        for b in np.flatnonzero(ud[:, c] == rank):
+            idx.append(np.arange(prob.s_ptr[b], prob.s_ptr[b + 1]))
+            if prob.l_ptr is not None:
+                idx.append(n_s + np.arange(prob.l_ptr[b], prob.l_ptr[b + 1]))
+        out.append(np.concatenate(idx).astype(np.int64) if idx else np.zeros(0, dtype=np.int64))
+    return out
 
 
 def sub_problem(prob, blocks: np.ndarray, compact: bool = False):
@@ -69,6 +114,51 @@ def sub_problem(prob, blocks: np.ndarray, compact: bool = False):
     return sub, s_idx.astype(np.int64), l_idx.astype(np.int64)
 
 
+class UnitGather:
+    """Per-step gather of this rank's unit betas to rank 0 for a fixed shard plan: the index lists
+    are exchanged once; each call is ONE `gather` of a padded fp64 buffer holding, copy after copy,
+    the values at this rank's positions -- over RCCL/xGMI with the nccl backend."""
+
+    def __init__(self, prob, unit_device, device="cpu"):
+        import torch
+        import torch.distributed as dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.n_s, self.n_l = prob.n_s, prob.n_l
+        self.k = np.asarray(unit_device).shape[1]
+        self.device = device
+        self.mine = unit_index(prob, unit_device, self.rank)
+        self.counts = [[int(x.size) for x in unit_index(prob, unit_device, r)] for r in range(self.world)]
+        if self.rank == 0:
+            self.idx = [unit_index(prob, unit_device, r) for r in range(self.world)]
+        self.width = max(1, max(sum(c) for c in self.counts))
+        self.buf = torch.zeros(self.width, dtype=torch.float64, device=device)
+        self.out = [torch.empty_like(self.buf) for _ in range(self.world)] if self.rank == 0 else None
+
+    def __call__(self, beta_s, beta_l):
+        """beta_s, beta_l: (k, n_s), (k, n_l) arrays holding this rank's units (the rest ignored)
+        -> on rank 0 the full k pairs in the original order (None elsewhere)."""
+        import torch
+        import torch.distributed as dist
+        host = np.zeros(self.width)
+        o = 0
+        for c, ix in enumerate(self.mine):
+            full = np.concatenate([beta_s[c], beta_l[c]])
+            host[o:o + ix.size] = full[ix]
+            o += ix.size
+        self.buf.copy_(torch.from_numpy(host))
+        dist.gather(self.buf, gather_list=self.out, dst=0)
+        if self.rank != 0:
+            return None
+        full = np.full((self.k, self.n_s + self.n_l), np.nan)
+        for t, ixs in zip(self.out, self.idx):
+            v = t.cpu().numpy()
+            o = 0
+            for c, ix in enumerate(ixs):
+                full[c, ix] = v[o:o + ix.size]
+                o += ix.size
+        return [(full[c, :self.n_s], full[c, self.n_s:]) for c in range(self.k)]
+
+
 def gather_beta(n_s: int, n_l: int, s_idx, l_idx, beta_s, beta_l, device="cpu"):
     """Gather every rank's (index, beta) to rank 0; returns the full beta_s, beta_l on rank 0
     (None elsewhere).  Shards are padded to the largest shard (one collective)."""
@@ -97,64 +187,37 @@ def gather_beta(n_s: int, n_l: int, s_idx, l_idx, beta_s, beta_l, device="cpu"):
     return full[:n_s], full[n_s:]
 
 
-class ShardGather:
-    """Per-step gather of this rank's betas to rank 0 for a fixed shard layout: the counts and
-    the padded width are exchanged once; each call is ONE `gather` of a [k, width] fp64 buffer
-    (k = solves per step, e.g. the h2f factors) -- over RCCL/xGMI with the nccl backend."""
+def est_distributed(prob, solve=None, device=None, sigmas=None):
+    """Solve `prob` across the ranks of the default process group; betas on rank 0.
 
-    def __init__(self, n_s, n_l, s_idx, l_idx, k=1, device="cpu"):
-        import torch
-        import torch.distributed as dist
-        self.world, self.rank = dist.get_world_size(), dist.get_rank()
-        self.n_s, self.n_l, self.k, self.device = n_s, n_l, k, device
-        self.idx = np.concatenate([s_idx, n_s + np.asarray(l_idx, dtype=np.int64)]).astype(np.int64)
-        cnt = torch.tensor([self.idx.size], dtype=torch.int64, device=device)
-        cnts = [torch.zeros_like(cnt) for _ in range(self.world)]
-        dist.all_gather(cnts, cnt)
-        self.cnts = [int(c.item()) for c in cnts]
-        self.width = max(1, max(self.cnts))
-        self.buf = torch.zeros((k, self.width), dtype=torch.float64, device=device)
-        self.out = [torch.empty_like(self.buf) for _ in range(self.world)] if self.rank == 0 else None
-        idx = torch.full((self.width,), -1, dtype=torch.int64, device=device)
-        idx[:self.idx.size] = torch.from_numpy(self.idx).to(device)
-        self.idxs = [torch.empty_like(idx) for _ in range(self.world)] if self.rank == 0 else None
-        dist.gather(idx, gather_list=self.idxs, dst=0)
-        if self.rank == 0:
-            self.idxs = [t[:c].cpu().numpy() for t, c in zip(self.idxs, self.cnts)]
-
-    def __call__(self, betas):
-        """betas: k pairs (beta_s, beta_l) of this rank's shard -> on rank 0 the full k pairs in
-        the original order (None elsewhere)."""
-        import torch
-        import torch.distributed as dist
-        host = np.zeros((self.k, self.width))
-        for c, (bs, bl) in enumerate(betas):
-            host[c, :self.idx.size] = np.concatenate([bs, bl])
-        self.buf.copy_(torch.from_numpy(host))
-        dist.gather(self.buf, gather_list=self.out, dst=0)
-        if self.rank != 0:
-            return None
-        full = np.full((self.k, self.n_s + self.n_l), np.nan)
-        for t, ix in zip(self.out, self.idxs):
-            full[:, ix] = t[:, :ix.size].cpu().numpy()
-        return [(full[c, :self.n_s], full[c, self.n_s:]) for c in range(self.k)]
-
-
-def est_distributed(prob, solve=None, device=None):
-    """Solve `prob` across the ranks of the default process group; beta on rank 0.
-
-    solve(sub_problem) -> (beta_s, beta_l, status); default = this rank's GPU through the C-ABI.
-    """
+    sigmas: h2f solves (default [prob.sigma_s]); the units are (block, copy) pairs of the shard plan.
+    solve(sub_problem, sigma_list) -> [(beta_s, beta_l)] per sigma, for a test solver (the oracle);
+    default = this rank's GPU through the C-ABI (one units plan, dbslmm_plan_create_units).
+    Returns [(beta_s, beta_l)] per sigma on rank 0 (a single pair when sigmas is None), None
+    elsewhere."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
+    sig = [prob.sigma_s] if sigmas is None else list(sigmas)
+    K = len(sig)
     m = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
-    shards = shard_blocks(m, prob.n_ref, world)
-    sub, s_idx, l_idx = sub_problem(prob, shards[rank])
+    ud, _ = shard_units(m, prob.n_ref, world, K)
+    bs = np.zeros((K, prob.n_s))
+    bl = np.zeros((K, prob.n_l))
     if solve is None:
-        from . import DBSLMMFIT
+        from . import Context, Plan
         import torch
         dev = torch.cuda.current_device() if device is None else device
-        solve = DBSLMMFIT(dev).est
-    bs, bl, _ = solve(sub)
+        plan = Plan.units(Context(dev), prob, ud, rank)
+        plan.run_multi(sig, out=(bs, bl, np.zeros((K, prob.num_block), dtype=np.int32)))
+        plan.close()
+    else:
+        for blocks, copies in rank_jobs(ud, rank):
+            sub, s_idx, l_idx = sub_problem(prob, blocks)
+            for c, (s, l) in zip(copies, solve(sub, [sig[c] for c in copies])):
+                bs[c, s_idx] = s
+                bl[c, l_idx] = l
     dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
-    return gather_beta(prob.n_s, prob.n_l, s_idx, l_idx, bs, bl, device=dev)
+    res = UnitGather(prob, ud, device=dev)(bs, bl)
+    if res is None:
+        return None
+    return res if sigmas is not None else res[0]

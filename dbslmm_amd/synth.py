@@ -72,13 +72,9 @@ class SynthPanel:
         return len(self.ps)
 
 
-def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), seed: int = 1,
-             rho: float = 0.9, miss_rate: float = 0.0, large_every: int = 20,
-             large_z: float = 8.0, n_obs: int = 100000, h2: float = 0.5,
-             block_limit: int | None = None, engine: str = "numpy", device: int = 0) -> SynthPanel:
-    """engine "numpy" (CPU, used by the parity fixtures) or "gpu" (libdbslmm_synth.so, same model
-    with a counter-hash RNG; for the 500k-1M SNP scale configs)."""
-    rng = np.random.default_rng(seed)
+def _layout(m_total, pop, chroms, rng, block_limit=None):
+    """SNP positions of a synthetic panel: per chromosome a share of m_total proportional to its
+    summed block span, positions uniform in the span, each SNP in the block containing it."""
     blocks = read_blocks(pop, chroms)
     if block_limit is not None:
         blocks = blocks[:block_limit]
@@ -112,6 +108,24 @@ def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), se
     chrom = np.concatenate(chrom)
     ps = np.concatenate(ps)
     blk = np.concatenate(blk)
+    return blocks, chrom, ps, blk
+
+
+def block_sizes(m_total: int, pop: str = "EUR", chroms=range(1, 23), seed: int = 1,
+                block_limit: int | None = None) -> np.ndarray:
+    """SNPs per LD block of simulate(m_total, ..., seed) without generating genotypes."""
+    blocks, _, _, blk = _layout(m_total, pop, chroms, np.random.default_rng(seed), block_limit)
+    return np.bincount(blk, minlength=len(blocks))
+
+
+def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), seed: int = 1,
+             rho: float = 0.9, miss_rate: float = 0.0, large_every: int = 20,
+             large_z: float = 8.0, n_obs: int = 100000, h2: float = 0.5,
+             block_limit: int | None = None, engine: str = "numpy", device: int = 0) -> SynthPanel:
+    """engine "numpy" (CPU, used by the parity fixtures) or "gpu" (libdbslmm_synth.so, same model
+    with a counter-hash RNG; for the 500k-1M SNP scale configs)."""
+    rng = np.random.default_rng(seed)
+    blocks, chrom, ps, blk = _layout(m_total, pop, chroms, rng, block_limit)
     m = len(ps)
     af = rng.uniform(0.05, 0.5, size=m)
     thr = ndtri(af).astype(np.float32)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 9
+#define DBSLMM_ABI_VERSION 10
 
 enum {
     DBSLMM_OK = 0,
@@ -78,8 +78,9 @@ typedef struct dbslmm_plan dbslmm_plan;
  * large_cheb     plan_run_multi with Chebyshev h2f: the single-workgroup blocks (64 <= m+1, m
  *                below tiled_min) iterate on the base copy's factor too (0 = on when every such
  *                block fits the iteration kernel, ld <= 512; -1 = off: every copy factored)
- * cheb_fused     1 = all Chebyshev passes of a copy group in one persistent launch (experimental,
- *                bit-identical, slower at config 4); 0 = one launch per pass
+ * cheb_fused     1 = all Chebyshev passes of a copy group in one persistent launch over every tiled
+ *                block (experimental, bit-identical, slower at config 4; turns sub_split off);
+ *                0 = one launch per pass
  * debug_delay_us testing only: a spin kernel of this many microseconds at the head of every
  *                concurrently running stream segment (the bulk trailing launches of each tiled
  *                sequence, the rest sequence, the main stream after the lead fork, the lead
@@ -97,6 +98,12 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                otherwise as 0): results within cheb_tol, not bit-identical to 0 / 1.
  * sub_grid_lead, sub_grid_rest   their persistent grids (0 = default: 5/16 of the CUs for
  *                the lead group, the other three quarters for the rest)
+ * shard_copies   multi-device plans (dbslmm_ctx_create_multi): the number of h2f solves each
+ *                run_multi call will request (0 / 1: single solves).  With K >= 2 and at least K
+ *                devices the shard plan may split the K copies of the blocks whose dependency chain
+ *                exceeds the fair share of the step into K (block, copy) units on distinct devices
+ *                (dbslmm_shard_plan).  Any n_sigma still works: with n_sigma != K a split block is
+ *                solved whole on the device of its copy 0.  Ignored by single-device plans.
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -112,6 +119,7 @@ typedef struct dbslmm_options {
     int32_t sub_split;
     int32_t sub_grid_lead;
     int32_t sub_grid_rest;
+    int32_t shard_copies;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.
@@ -178,6 +186,28 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out);
  * caller's original order.  dbslmm_bed_maf splits its rows over the devices; read_snp_std and
  * valid_blocks run on the first device.  n_dev == 1 is dbslmm_ctx_create(device_ids[0]). */
 int dbslmm_ctx_create_multi(int32_t n_dev, const int32_t* device_ids, dbslmm_ctx** out);
+/* Shard plan (ABI 10): assign the work units of a problem -- (LD block, h2f copy) pairs -- to n_dev
+ * devices.  m[b] = SNPs of block b (small + large), n_copies = h2f solves per run (1: single solves).
+ * A block's copies stay on one device (one Gram, one factorisation, the other copies iterated on
+ * it) unless the block's dependency chain exceeds the fair share of the step and n_dev >= n_copies:
+ * then each copy is a unit of its own, factored directly, on distinct devices.  Units go to devices
+ * longest-first by a time model of one MI355X (per-block chip time of each kernel class and the
+ * block's chain alone).  Out: unit_device[b * n_copies + c] = the device index
+ * of copy c of block b (-1: empty block); dev_ms (optional, n_dev entries) = the model's predicted
+ * step of each device in ms.  Host-only (no GPU needed); deterministic.  Replaces the reference's
+ * OpenMP schedule(dynamic) over blocks (scr/dbslmmfit.cpp:189-220). */
+int dbslmm_shard_plan(int32_t num_block, const int32_t* m, int32_t n_ref, int32_t n_dev, int32_t n_copies,
+                      int32_t* unit_device, double* dev_ms);
+/* A plan over ONE device's units of a shard plan (ABI 10), on a single-device context: the same
+ * problem as dbslmm_plan_create (the whole .bed image and CSR arrays), solving only the units with
+ * unit_device[b * n_copies + c] == device_index (split units on contexts of their own on the same
+ * GPU, so they run beside the device's whole blocks).  run_multi / download / variance write only
+ * those units' entries of the caller's full-size arrays; everything else is left untouched, so
+ * one process per GPU (bench.py under torch.distributed) solves its part and gathers the rest.
+ * Run it with n_sigma == n_copies (otherwise a split block is solved whole by the device of its
+ * copy 0). */
+int dbslmm_plan_create_units(dbslmm_ctx* ctx, const dbslmm_problem* p, int32_t n_copies,
+                             const int32_t* unit_device, int32_t device_index, dbslmm_plan** out);
 /* Devices a context drives (1 for dbslmm_ctx_create). */
 int dbslmm_ctx_num_devices(const dbslmm_ctx* ctx);
 /* block_device[b] (num_block entries) = the device index (0 .. n_dev-1, in device_ids order) that

@@ -23,11 +23,20 @@ def _problem():
     return synth.make_problem(p)
 
 
-def _oracle_solve(sub):
+def _oracle_solve(sub, sigmas=None):
+    """The oracle's direct solve of a sub-problem: (beta_s, beta_l, status), or with sigmas the
+    est_distributed solver callback: [(beta_s, beta_l)] per sigma."""
     import oracle as O
-    bs, bl, st, rc = O.est(sub.bed, sub.n_ref, sub.n_obs, sub.sigma_s, sub.s_ptr, sub.s_pos,
-                           sub.z_s, sub.l_ptr, sub.l_pos, sub.z_l, method="direct")
-    return bs, bl, st
+    if sigmas is None:
+        bs, bl, st, rc = O.est(sub.bed, sub.n_ref, sub.n_obs, sub.sigma_s, sub.s_ptr, sub.s_pos,
+                               sub.z_s, sub.l_ptr, sub.l_pos, sub.z_l, method="direct")
+        return bs, bl, st
+    out = []
+    for sg in sigmas:
+        bs, bl, _, _ = O.est(sub.bed, sub.n_ref, sub.n_obs, sg, sub.s_ptr, sub.s_pos, sub.z_s,
+                             sub.l_ptr, sub.l_pos, sub.z_l, method="direct")
+        out.append((bs, bl))
+    return out
 
 
 def _worker(rank, world, port, out_path):
@@ -39,23 +48,78 @@ def _worker(rank, world, port, out_path):
     from dbslmm_amd import dist as D
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     prob = _problem()
-    bs, bl = D.est_distributed(prob, solve=_oracle_solve)
+    bs, bl = D.est_distributed(prob, solve=_oracle_solve) or (None, None)
     if rank == 0:
         np.save(out_path, np.concatenate([bs, bl]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_shard_blocks_lpt_balanced_and_complete():
-    from dbslmm_amd.dist import block_cost, shard_blocks
+def test_shard_blocks_balanced_and_complete():
+    """Single-solve shard plan (dbslmm_shard_plan, host only): every non-empty block on exactly one
+    rank, empty blocks nowhere, and the time model's predicted device steps within the largest
+    block's cost of each other (LPT)."""
+    from dbslmm_amd.dist import shard_blocks, shard_units
     rng = np.random.default_rng(0)
     m = rng.integers(0, 600, size=1703)
     for world in (1, 2, 4, 8):
         sh = shard_blocks(m, 10000, world)
         allb = np.sort(np.concatenate(sh))
         assert np.array_equal(allb, np.flatnonzero(m > 0))
-        loads = [block_cost(m[s], 10000).sum() for s in sh]
-        assert max(loads) <= sum(loads) / world + block_cost(np.array([m.max()]), 10000)[0]
+        ud, ms = shard_units(m, 10000, world, 1)
+        assert np.all(ud[m == 0] == -1)
+        _, one = shard_units(m[m == m.max()][:1], 10000, 1, 1)
+        assert ms.max() - ms.min() <= one[0] + 1e-9, (world, ms)
+
+
+def _config4_blocks():
+    from dbslmm_amd import synth
+    return synth.block_sizes(1000000, pop="EUR", seed=1)
+
+
+def test_shard_units_split_largest_blocks_copies():
+    """h2f (3 copies): the blocks whose chain exceeds the fair share get one copy per device (three
+    distinct devices); every other block keeps its copies together; every unit has a device."""
+    from dbslmm_amd.dist import shard_units
+    m = _config4_blocks()
+    for world, want_split in ((1, 0), (2, 0), (4, 2), (8, 3)):
+        ud, ms = shard_units(m, 10000, world, 3)
+        assert np.all((ud >= 0) == (m > 0)[:, None])
+        split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
+        assert split.size == want_split, (world, split)
+        for b in split:
+            assert len(set(ud[b].tolist())) == 3          # distinct devices
+            assert m[b] >= np.sort(m)[-3]                  # the largest blocks
+        assert ms.size == world and np.all(ms > 0)
+
+
+def test_shard_model_predictions_config4():
+    """The time model reproduces the measured one-GPU config-4 step (42-44 ms)
+    and predicts the 8-GPU step below 16 ms once the largest blocks' h2f copies are split (VERDICT
+    r04 item 4); configs 3 / 5 at one GPU: 8.6 / 34 ms measured."""
+    from dbslmm_amd import synth
+    from dbslmm_amd.dist import shard_units
+    m4 = _config4_blocks()
+    assert 38.0 < shard_units(m4, 10000, 1, 3)[1].max() < 48.0
+    assert shard_units(m4, 10000, 8, 3)[1].max() < 16.0
+    m3 = synth.block_sizes(500000, pop="EUR", seed=1)
+    assert 7.0 < shard_units(m3, 5000, 1, 1)[1].max() < 10.5
+    m5 = synth.block_sizes(1000000, pop="AFR", seed=1)
+    assert 28.0 < shard_units(m5, 10000, 1, 1)[1].max() < 40.0
+
+
+def test_rank_jobs_cover_every_unit_once():
+    from dbslmm_amd.dist import rank_jobs, shard_units
+    m = _config4_blocks()
+    world = 8
+    ud, _ = shard_units(m, 10000, world, 3)
+    seen = np.zeros(ud.shape, dtype=int)
+    for r in range(world):
+        for blocks, copies in rank_jobs(ud, r):
+            assert len(copies) in (1, 3)
+            for c in copies:
+                seen[blocks, c] += 1
+    assert np.all(seen[m > 0] == 1) and np.all(seen[m == 0] == 0)
 
 
 def test_sub_problem_roundtrip():
@@ -131,9 +195,35 @@ def test_compact_sub_problem_same_rows():
         np.testing.assert_array_equal(x, y)
 
 
-def _gather_worker(rank, world, port, out_path):
-    """The bench's per-step path: compact shard per rank, oracle solve, ShardGather (k = 2 solves
-    per step, called twice)."""
+def _split_problem():
+    """One dominant block (1600 SNPs) beside small ones: with 3 h2f copies on >= 3 ranks the shard
+    plan splits that block's copies over three ranks."""
+    from dbslmm_amd import BlockProblem, synth
+    sizes = [60, 1600, 80, 100, 0, 40, 70]
+    total = sum(sizes)
+    p = synth.simulate(total + 50, 96, pop="EUR", chroms=[22], seed=6, large_every=0)
+    rng = np.random.default_rng(6)
+    bid = np.repeat(np.arange(len(sizes)), sizes)
+    large = np.zeros(total, dtype=bool)
+    large[rng.choice(total, size=5, replace=False)] = True
+    z = rng.standard_normal(total)
+    z[large] *= 6.0
+
+    def csr(mask):
+        idx = np.flatnonzero(mask)
+        ptr = np.zeros(len(sizes) + 1, dtype=np.int64)
+        np.add.at(ptr, bid[idx] + 1, 1)
+        return np.cumsum(ptr), idx.astype(np.int32), z[idx]
+    s_ptr, s_pos, z_s = csr(~large)
+    l_ptr, l_pos, z_l = csr(large)
+    prob = BlockProblem(bed=p.bed, n_ref=96, n_obs=100000, sigma_s=0.5 / total, s_ptr=s_ptr, s_pos=s_pos,
+                        z_s=z_s, l_ptr=l_ptr, l_pos=l_pos, z_l=z_l)
+    return prob, np.array(sizes)
+
+
+def _gather_worker(rank, world, port, out_path, k):
+    """The bench's per-step path: this rank's units of the shard plan (k h2f copies), oracle solve
+    of each job, UnitGather called twice."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle"), here):
@@ -141,25 +231,37 @@ def _gather_worker(rank, world, port, out_path):
     import torch.distributed as dist
     from dbslmm_amd import dist as D
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    prob = _problem()
-    m = np.diff(prob.s_ptr) + np.diff(prob.l_ptr)
-    sub, s_idx, l_idx = D.sub_problem(prob, D.shard_blocks(m, prob.n_ref, world)[rank], compact=True)
-    g = D.ShardGather(prob.n_s, prob.n_l, s_idx, l_idx, k=2)
-    bs, bl, _ = _oracle_solve(sub)
+    prob, m = _split_problem()
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)[:k]]
+    ud, _ = D.shard_units(m, prob.n_ref, world, k)
+    bs = np.zeros((k, prob.n_s))
+    bl = np.zeros((k, prob.n_l))
+    for blocks, copies in D.rank_jobs(ud, rank):
+        sub, s_idx, l_idx = D.sub_problem(prob, blocks, compact=True)
+        for c, (s, l) in zip(copies, _oracle_solve(sub, [sig[c] for c in copies])):
+            bs[c, s_idx] = s
+            bl[c, l_idx] = l
+    g = D.UnitGather(prob, ud)
     for _ in range(2):
-        res = g([(bs, bl), (2 * bs, 2 * bl)])
+        res = g(bs, bl)
     if rank == 0:
         np.save(out_path, np.stack([np.concatenate(r) for r in res]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_shard_gather_per_step(tmp_path, world):
+@pytest.mark.parametrize("world,k", [(2, 1), (3, 3)])
+def test_unit_gather_per_step(tmp_path, world, k):
+    """world 3, k 3: the dominant block's copies are split over the three ranks (asserted); the
+    gathered betas equal the single-process oracle solve of every copy bit for bit."""
+    from dbslmm_amd.dist import shard_units
+    prob, m = _split_problem()
+    ud, _ = shard_units(m, prob.n_ref, world, k)
+    split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
+    assert (split.size > 0) == (k == 3), split
     out = str(tmp_path / "beta.npy")
-    mp.spawn(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_gather_worker, args=(world, _free_port(), out, k), nprocs=world, join=True)
     got = np.load(out)
-    bs, bl, _ = _oracle_solve(_problem())
-    ref = np.concatenate([bs, bl])
-    np.testing.assert_array_equal(got[0], ref)
-    np.testing.assert_array_equal(got[1], 2 * ref)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)[:k]]
+    for c, (bs, bl) in enumerate(_oracle_solve(prob, sig)):
+        np.testing.assert_array_equal(got[c], np.concatenate([bs, bl]))

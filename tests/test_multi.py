@@ -50,10 +50,10 @@ def test_sharded_plan_run_multi_and_shards():
     m = np.diff(prob.s_ptr) + np.diff(prob.l_ptr)
     assert np.all((info == -1) == (m == 0))
     assert set(info[m > 0].tolist()) == set(range(len(DEVS)))      # every device got blocks
-    # LPT balance: no device holds more than the largest block plus its fair share of the cost
-    cost = prob.n_ref * m * (m + 1.0) + m ** 3 / 3.0
-    loads = [cost[info == d].sum() for d in range(len(DEVS))]
-    assert max(loads) <= cost.sum() / len(DEVS) + cost.max()
+    # the library's shard plan (time model, dbslmm_shard_plan) is what the context used
+    from dbslmm_amd.dist import shard_units
+    ud, _ = shard_units(m, prob.n_ref, len(DEVS), 1)
+    np.testing.assert_array_equal(info, ud[:, 0])
     for _ in range(2):                                             # repeated runs stay identical
         got = plan.run_multi(sig)
         for (a, b, c), (x, y, z) in zip(got, ref):
@@ -129,3 +129,61 @@ def test_sharded_more_devices_than_blocks():
     for x, y in zip(one, many):
         np.testing.assert_array_equal(x, y)
     assert normwise(np.concatenate(one[:2]), np.concatenate(many[:2])) == 0.0
+
+
+def test_split_h2f_units_match_single_device():
+    """shard_copies = 3 on three devices (all device 0 here): the dominant block's three h2f
+    copies become (block, copy) units on distinct devices, each factored directly on a context of
+    its own beside that device's whole blocks.  Every other block equals the one-device run bit for
+    bit, and so does the split block's base copy (the same factorisation and backward solve); its
+    other copies are exact solves where the one-device run iterated (Chebyshev to cheb_tol), so
+    they agree with it to cheb_tol and with the oracle's direct solve to 1e-10.  One units plan
+    per device index (dbslmm_plan_create_units, the torchrun ranks' path) fills the same arrays bit
+    for bit; a run_multi with another number of sigmas solves the split block whole."""
+    import oracle as O
+    from test_dist import _split_problem
+    from dbslmm_amd import Context, Plan
+    from dbslmm_amd.dist import shard_units
+    prob, m = _split_problem()
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    ud, _ = shard_units(m, prob.n_ref, 3, 3)
+    split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
+    assert split.tolist() == [1] and sorted(ud[1].tolist()) == [0, 1, 2]
+    single = Plan(Context(0), prob).run_multi(sig)
+    prob.opts["shard_copies"] = 3
+    many = Plan(Context(DEVS), prob)
+    got = many.run_multi(sig)
+    sl = np.r_[prob.s_ptr[1]:prob.s_ptr[2]]
+    ll = np.r_[prob.l_ptr[1]:prob.l_ptr[2]]
+    keep_s = np.setdiff1d(np.arange(prob.n_s), sl)
+    keep_l = np.setdiff1d(np.arange(prob.n_l), ll)
+    for c in range(3):
+        np.testing.assert_array_equal(got[c][0][keep_s], single[c][0][keep_s])
+        np.testing.assert_array_equal(got[c][1][keep_l], single[c][1][keep_l])
+        np.testing.assert_array_equal(got[c][2], single[c][2])
+        g = np.concatenate([got[c][0][sl], got[c][1][ll]])
+        o = np.concatenate([single[c][0][sl], single[c][1][ll]])
+        if c == 1:                                       # the base copy (median sigma)
+            np.testing.assert_array_equal(g, o)
+        else:
+            assert normwise(g, o) < 1e-8, c
+        rs, rl, _, _ = O.est(prob.bed, prob.n_ref, prob.n_obs, sig[c], prob.s_ptr, prob.s_pos, prob.z_s,
+                             prob.l_ptr, prob.l_pos, prob.z_l, method="direct")
+        assert normwise(np.concatenate([got[c][0], got[c][1]]), np.concatenate([rs, rl])) < 1e-10, c
+    # the torchrun ranks' path: one units plan per device index, each writing its units only
+    bs, bl = np.full((3, prob.n_s), np.nan), np.full((3, prob.n_l), np.nan)
+    st = np.full((3, prob.num_block), -7, dtype=np.int32)
+    for d in range(3):
+        u = Plan.units(Context(0), prob, ud, d)
+        u.run_multi(sig, out=(bs, bl, st))
+        u.close()
+    for c in range(3):
+        np.testing.assert_array_equal(bs[c], got[c][0])
+        np.testing.assert_array_equal(bl[c], got[c][1])
+    # two sigmas (!= shard_copies): the split block is solved whole by its copy-0 device
+    two = many.run_multi(sig[:2])
+    ref2 = Plan(Context(0), prob).run_multi(sig[:2])
+    for (a, b, c_), (x, y, z) in zip(two, ref2):
+        np.testing.assert_array_equal(a, x)
+        np.testing.assert_array_equal(b, y)
+        np.testing.assert_array_equal(c_, z)

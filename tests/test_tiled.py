@@ -311,6 +311,49 @@ def test_phase_diagnosis_of_a_good_block():
         O.blas_threads(1)
 
 
+def test_outputs_refused_after_debug_stop():
+    """A debug_stop = 1 run stops after the Gram: its betas are never computed, so download and
+    run_multi's outputs must be refused (E_STATE), not served from an earlier run or uninitialised
+    memory; a following full run serves them again."""
+    from dbslmm_amd import Context, DbslmmError, Plan
+    prob = _problem(seed=41, n_ref=256, sizes=[700, 300, 40])
+    plan = Plan(Context(0), prob)
+    plan.run()
+    good = plan.download()
+    plan.close()
+    prob.opts["debug_stop"] = 1
+    plan = Plan(Context(0), prob)
+    plan.run()
+    plan.sync()
+    assert plan.block_matrix(0).shape[0] >= 700     # the diagnostic read still works
+    with pytest.raises(DbslmmError):
+        plan.download()
+    plan.close()
+    prob.opts["debug_stop"] = 0
+    plan = Plan(Context(0), prob)
+    plan.run()
+    for x, y in zip(plan.download(), good):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_fused_cheb_with_lead_group_matches_unfused():
+    """cheb_fused = 1 on a plan with a lead group: the fused launch covers all tiled items, so the
+    plan turns the split substitutions off (before round 5 the option was silently ignored there);
+    the h2f copies equal the per-pass launches bit for bit."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=43, n_ref=512, sizes=LEAD_MIX, miss_rate=0.0)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    res = {}
+    for fused in (0, 1):
+        prob.opts = dict(cheb_fused=fused, sub_split=-1 if fused == 0 else 0)
+        plan = Plan(Context(0), prob)
+        res[fused] = plan.run_multi(sig)
+        plan.close()
+    for c in range(3):
+        for x, y in zip(res[1][c], res[0][c]):
+            np.testing.assert_array_equal(x, y)
+
+
 @pytest.mark.parametrize("delay_us", [0, 300, -300])
 def test_split_substitutions_bit_identical(delay_us):
     """dbslmm_options.sub_split = 1: the rest group's backward solve and h2f Chebyshev passes run
