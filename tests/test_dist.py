@@ -153,7 +153,7 @@ def _gpu_worker(rank, world, port, out_path):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     prob = _problem()
-    bs, bl = D.est_distributed(prob, device=0)       # HIP solver on each rank
+    bs, bl = D.est_distributed(prob, device=0) or (None, None)   # HIP solver on each rank
     if rank == 0:
         np.save(out_path, np.concatenate([bs, bl]))
     dist.barrier()
