@@ -26,8 +26,11 @@
 // ---------------------------------------------------------------- time model of one device
 // Calibrated on config 4 (1M SNPs x 10k): chip-time of each kernel class from a
 // serialised SQ_WAVE_CYCLES pass (round 4: trailing 13.2, substitutions 12.0, panels 3.2, Gram 2.9,
-// regions 1.75, unpack 1.4, chol_large 1.0 chip-ms) over its algorithmic work, and the block chains
-// from the 9.6k-SNP block alone (tools/micro/tchol_alone.py) and the substitution stamps.
+// regions 1.75, unpack 1.4, chol_large 1.0 chip-ms) over its algorithmic work; the block chains
+// from the 9.6k-SNP block alone (tools/micro/tchol_alone.py: 14.7 ms) and the substitution
+// stamps; the chain slow-down under the device's other work and the serialisation of split units
+// that share a device from the round-5 one-GPU rehearsal (bench.py --predict 2,4,8: per-device
+// steps of 31.8 / 15.4 / 24.8 ms against a first model's 21.9 / 11.2 / 10.8).
 namespace shard {
 constexpr double kUnpackBps = 3.6e12;       // unpack: packed + operand bytes per second
 constexpr double kGramOps = 3.1e15;         // Gram: ops (2 per MAC) per second
@@ -36,9 +39,10 @@ constexpr double kPanelFlops = 68e12;       // panels: 2 x 128 x m^2 flops per b
 constexpr double kRegionChipUs = 0.17;      // regions: chip-us per 128 columns (86 us on half a CU)
 constexpr double kCholLargeFlops = 2e12;    // single-workgroup blocks (latency-bound)
 constexpr double kSubBps = 4.3e12;          // substitution passes: factor bytes per second
-constexpr double kChainRegionUs = 135.0;    // factorisation chain per 128 columns, block alone
+constexpr double kChainRegionUs = 182.0;    // factorisation chain per 128 columns, block alone
 constexpr double kChainSubUs = 4.5;         // substitution chain per 64-row tile, per pass
 constexpr double kBusy = 0.85;              // fraction of the chip the overlapped phases keep busy
+constexpr double kDrag = 0.67;              // a chain's slow-down per chip-ms of other work beside it
 constexpr int kChebIters = 7;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 (plan.hip cheb_plan)
 constexpr int kTiledMin = 384;              // plan.hip kTiledMinDefault
 
@@ -72,6 +76,30 @@ static Cost block_cost(double m, double n_ref, int copies, bool direct) {
     return c;
 }
 
+// One device's load: total work, the longest whole-block chain of its main job, and its split
+// units (contexts of their own: on the shared hardware queues their chains run one after the
+// other).  Predicted step = max(work / busy, critical chain + drag x the other work).
+struct Dev {
+    double work = 0.0, whole_chain = 0.0, whole_chain_work = 0.0, split_chain = 0.0, split_work = 0.0;
+    int n_split = 0;
+    double time() const {
+        const bool sp = split_chain >= whole_chain;
+        const double c = sp ? split_chain : whole_chain, cw = sp ? split_work : whole_chain_work;
+        return std::max(work / kBusy, c + kDrag * std::max(0.0, work - cw));
+    }
+    void add(const Cost& k, bool split) {
+        work += k.work;
+        if (split) {
+            split_chain += k.chain;
+            split_work += k.work;
+            ++n_split;
+        } else if (k.chain > whole_chain) {
+            whole_chain = k.chain;
+            whole_chain_work = k.work;
+        }
+    }
+};
+
 // Units -> devices.  unit_device[b * K + c] (K = copies per run) = device of copy c of block b, -1
 // for an empty block; dev_ms[d] = predicted step of device d.  Deterministic.
 static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, int32_t K,
@@ -81,61 +109,72 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
     dev_ms.assign(G, 0.0);
     std::vector<char> split(nb, 0);
     std::vector<Cost> whole(nb), unit(nb);
-    double total = 0.0, chain_floor = 0.0;
+    double total = 0.0;
     for (int b = 0; b < nb; ++b) {
         whole[b] = block_cost(m[b], n_ref, K, false);
         unit[b] = block_cost(m[b], n_ref, 1, true);
         total += whole[b].work;
     }
-    // split the h2f copies of the blocks whose whole chain exceeds the fair share of the step (one
-    // copy per device, so at least K devices), longest chain first; every split adds the extra
-    // factorisations to the total, so the share is re-evaluated after each
-    if (K > 1 && G >= K) {
-        std::vector<int32_t> byc;
-        for (int b = 0; b < nb; ++b)
-            if (m[b] > 0) byc.push_back(b);
-        std::stable_sort(byc.begin(), byc.end(), [&](int32_t x, int32_t y) { return whole[x].chain > whole[y].chain; });
-        for (int32_t b : byc) {
-            const double share = total / (kBusy * G);
-            if (whole[b].chain <= share || unit[b].chain >= whole[b].chain) break;
+    // Split the h2f copies of a block (one copy per device) when its whole chain exceeds both the
+    // fair share of the step and the chains already decided, and K devices without a split unit
+    // remain (two split units on one device run their chains one after the other); longest
+    // chain first.  Every split adds its extra factorisations to the total.
+    std::vector<int32_t> byc;
+    for (int b = 0; b < nb; ++b)
+        if (m[b] > 0) byc.push_back(b);
+    std::stable_sort(byc.begin(), byc.end(), [&](int32_t x, int32_t y) { return whole[x].chain > whole[y].chain; });
+    int free_dev = G;
+    double bound = 0.0;
+    for (int32_t b : byc) {
+        const double share = total / (kBusy * G);
+        if (whole[b].chain <= std::max(share, bound)) break;
+        if (K > 1 && free_dev >= K && unit[b].chain < whole[b].chain) {
             split[b] = 1;
+            free_dev -= K;
             total += K * unit[b].work - whole[b].work;
+            bound = std::max(bound, unit[b].chain);
+        } else {
+            bound = std::max(bound, whole[b].chain);
         }
     }
-    for (int b = 0; b < nb; ++b) chain_floor = std::max(chain_floor, split[b] ? unit[b].chain : whole[b].chain);
-    // LPT on the predicted device time max(work / busy, longest chain): units by that cost, each to
-    // the device where it ends earliest; a split block's copies on distinct devices
-    struct U { int32_t b, c; Cost k; double key; };
-    std::vector<U> us;
-    for (int b = 0; b < nb; ++b) {
-        if (m[b] <= 0) continue;
-        if (split[b])
-            for (int c = 0; c < K; ++c) us.push_back({b, c, unit[b], std::max(unit[b].work / kBusy, unit[b].chain)});
-        else
-            us.push_back({b, -1, whole[b], std::max(whole[b].work / kBusy, whole[b].chain)});
+    std::vector<Dev> dev(G);
+    // split units first, each copy on a device without a split unit (least loaded first)
+    for (int32_t b : byc) {
+        if (!split[b]) continue;
+        for (int c = 0; c < K; ++c) {
+            int best = -1;
+            for (int d = 0; d < G; ++d) {
+                bool taken = false;
+                for (int e = 0; e < c; ++e) taken |= unit_device[static_cast<size_t>(b) * K + e] == d;
+                if (taken) continue;
+                if (best < 0 || dev[d].n_split < dev[best].n_split ||
+                    (dev[d].n_split == dev[best].n_split && dev[d].time() < dev[best].time() - 1e-12))
+                    best = d;
+            }
+            dev[best].add(unit[b], true);
+            unit_device[static_cast<size_t>(b) * K + c] = best;
+        }
     }
-    std::stable_sort(us.begin(), us.end(), [](const U& x, const U& y) { return x.key > y.key; });
-    std::vector<double> work(G, 0.0), chain(G, 0.0);
-    for (const U& u : us) {
+    // whole blocks: LPT by the predicted device step, longest first
+    std::vector<int32_t> rest;
+    for (int32_t b : byc)
+        if (!split[b]) rest.push_back(b);
+    std::stable_sort(rest.begin(), rest.end(), [&](int32_t x, int32_t y) {
+        return std::max(whole[x].work / kBusy, whole[x].chain) > std::max(whole[y].work / kBusy, whole[y].chain);
+    });
+    for (int32_t b : rest) {
         int best = -1;
         double bt = 0.0;
         for (int d = 0; d < G; ++d) {
-            if (u.c >= 0) {   // a copy of this block already on d?
-                bool taken = false;
-                for (int c = 0; c < K; ++c) taken |= unit_device[static_cast<size_t>(u.b) * K + c] == d;
-                if (taken) continue;
-            }
-            const double t = std::max((work[d] + u.k.work) / kBusy, std::max(chain[d], u.k.chain));
-            if (best < 0 || t < bt - 1e-12) { best = d; bt = t; }
+            Dev t = dev[d];
+            t.add(whole[b], false);
+            const double v = t.time();
+            if (best < 0 || v < bt - 1e-12) { best = d; bt = v; }
         }
-        work[best] += u.k.work;
-        chain[best] = std::max(chain[best], u.k.chain);
-        if (u.c >= 0) unit_device[static_cast<size_t>(u.b) * K + u.c] = best;
-        else
-            for (int c = 0; c < K; ++c) unit_device[static_cast<size_t>(u.b) * K + c] = best;
+        dev[best].add(whole[b], false);
+        for (int c = 0; c < K; ++c) unit_device[static_cast<size_t>(b) * K + c] = best;
     }
-    for (int d = 0; d < G; ++d) dev_ms[d] = std::max(work[d] / kBusy, chain[d]);
-    (void)chain_floor;
+    for (int d = 0; d < G; ++d) dev_ms[d] = dev[d].time();
 }
 }  // namespace shard
 
