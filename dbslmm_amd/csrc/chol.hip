@@ -70,10 +70,10 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 
 #ifdef DBSLMM_STAMPS
 // diagnostic build only: accumulated 100 MHz ticks per phase of the large path
-__device__ unsigned long long g_stamp[8];
-#define STAMP_DECL unsigned long long st_t0 = 0;
+__device__ unsigned long long g_stamp[16];
+#define STAMP_DECL unsigned long long st_t0 = 0; int st_base = 0;
 #define STAMP_BEGIN() do { if (threadIdx.x == 0) st_t0 = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define STAMP_END(k) do { if (threadIdx.x == 0) atomicAdd(&g_stamp[k], __builtin_amdgcn_s_memrealtime() - st_t0); } while (0)
+#define STAMP_END(k) do { if (threadIdx.x == 0) atomicAdd(&g_stamp[(k) + st_base], __builtin_amdgcn_s_memrealtime() - st_t0); } while (0)
 #define FSTAMP(k) do { if (lane == 0) { unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); atomicAdd(&g_stamp[k], t_ - fst); fst = t_; } } while (0)
 #define FSTAMP_DECL unsigned long long fst = __builtin_amdgcn_s_memrealtime();
 #else

@@ -352,6 +352,9 @@ extern "C" __global__ __launch_bounds__(chol::kLargeThreads, 2) void dbslmm_tcho
     const double dshift = *a.dshift;
     const int c0 = 2 * kBT * reg;
     STAMP_DECL
+#ifdef DBSLMM_STAMPS
+    st_base = (update == 0 && reg > 0) ? 8 : 0;   // the first region of a super step: its own counters
+#endif
     STAMP_BEGIN();
     double* R = lds;
     double* colb = lds + 10 * kSub;

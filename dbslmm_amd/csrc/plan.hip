@@ -2628,11 +2628,12 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
 
 #ifdef DBSLMM_STAMPS
 // diagnostic build only (libdbslmm_hip_stamps.so): read + clear the per-phase tick counters
+// (16 counters: the region kernel's first-of-super-step regions count at 8..15)
 int dbslmm_debug_stamps(double* out8) {
-    unsigned long long h[8];
+    unsigned long long h[16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(chol::g_stamp), sizeof(h)) != hipSuccess) return -2;
-    for (int i = 0; i < 8; ++i) out8[i] = static_cast<double>(h[i]) * 10.0;  // ns (100 MHz clock)
-    unsigned long long z[8] = {0};
+    for (int i = 0; i < 16; ++i) out8[i] = static_cast<double>(h[i]) * 10.0;  // ns (100 MHz clock)
+    unsigned long long z[16] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(chol::g_stamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
 }
 #endif

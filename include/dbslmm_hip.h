@@ -179,12 +179,12 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out);
 
 /* Create a context over n_dev HIP devices (ordinals; a device may repeat: several shards on one
  * GPU).  Replaces the reference's only parallelism, OpenMP over LD blocks
- * (scr/dbslmmfit.cpp:191-220), with one GPU per shard: plan_create assigns the non-empty LD
- * blocks to the devices (longest processing time first on n_ref m (m+1) + m^3/3), uploads to each
- * device only the .bed rows of its blocks, and every plan / est call then drives all devices
- * concurrently (one host thread per device) and returns beta, status and variance columns in the
- * caller's original order.  dbslmm_bed_maf splits its rows over the devices; read_snp_std and
- * valid_blocks run on the first device.  n_dev == 1 is dbslmm_ctx_create(device_ids[0]). */
+ * (scr/dbslmmfit.cpp:191-220), with one GPU per shard: plan_create assigns the work units --
+ * (LD block, h2f copy) pairs, dbslmm_shard_plan with dbslmm_options.shard_copies -- to the devices,
+ * uploads to each device only the .bed rows of its blocks, and every plan / est call then drives
+ * all devices concurrently (one host thread per job) and returns beta, status and variance columns
+ * in the caller's original order.  dbslmm_bed_maf splits its rows over the devices; read_snp_std
+ * and valid_blocks run on the first device.  n_dev == 1 is dbslmm_ctx_create(device_ids[0]). */
 int dbslmm_ctx_create_multi(int32_t n_dev, const int32_t* device_ids, dbslmm_ctx** out);
 /* Shard plan (ABI 10): assign the work units of a problem -- (LD block, h2f copy) pairs -- to n_dev
  * devices.  m[b] = SNPs of block b (small + large), n_copies = h2f solves per run (1: single solves).
@@ -211,7 +211,8 @@ int dbslmm_plan_create_units(dbslmm_ctx* ctx, const dbslmm_problem* p, int32_t n
 /* Devices a context drives (1 for dbslmm_ctx_create). */
 int dbslmm_ctx_num_devices(const dbslmm_ctx* ctx);
 /* block_device[b] (num_block entries) = the device index (0 .. n_dev-1, in device_ids order) that
- * solves block b, -1 for an empty block; all 0 on a single-device context. */
+ * solves block b (its h2f copy 0 when the shard plan split its copies), -1 for an empty block (or,
+ * on a units plan, a block none of whose units it solves); all 0 on a single-device context. */
 int dbslmm_plan_shard_info(const dbslmm_plan* plan, int32_t* block_device);
 void dbslmm_ctx_destroy(dbslmm_ctx* ctx);
 const char* dbslmm_last_error(const dbslmm_ctx* ctx);

@@ -27,7 +27,7 @@ prob = BlockProblem(bed=bed, n_ref=n_ref, n_obs=50000, sigma_s=0.5 / 1e6,
 ctx = Context(0)
 plan = Plan(ctx, prob)
 L = _lib.load()
-out = np.zeros(8)
+out = np.zeros(16)
 if STAMPS:
     L.dbslmm_debug_stamps.argtypes = [C.c_void_p]
 plan.run()
@@ -44,6 +44,9 @@ nreg = (m + 127) // 128
 print("m", m, "regions", nreg, "per run (ms):", {k: round(v / max(nrun, 1), 3) for k, v in zip(_lib.KERNEL_NAMES, ms)})
 if STAMPS:
     L.dbslmm_debug_stamps(out.ctypes.data_as(C.c_void_p))
-    ph = out[:8] / reps / nreg / 1e3
-    print("region per launch us: load+update %.1f  4 steps %.1f  X10 %.1f  writeback %.1f"
-          " | in the steps: factor (t>0) %.1f  panel %.1f  trailing %.1f  factor t=0 %.1f" % tuple(ph))
+    R = 4 if m >= 4096 else 2                      # regions per super step (plan.hip kWideMin)
+    n_first = max(0, (nreg - 1) // R)               # first regions of super steps 1.. (no pending update)
+    for lab, ph, n in (("other regions", out[:8], nreg - n_first), ("first of super step", out[8:16], n_first)):
+        ph = ph / reps / max(n, 1) / 1e3
+        print(("%s (%d) per launch us: load+update %.1f  4 steps %.1f  X10 %.1f  writeback %.1f"
+               " | in the steps: factor (t>0) %.1f  panel %.1f  trailing %.1f  factor t=0 %.1f") % ((lab, n) + tuple(ph)))
