@@ -26,69 +26,92 @@
 // ---------------------------------------------------------------- time model of one device
 // Calibrated on config 4 (1M SNPs x 10k): chip-time of each kernel class from a
 // serialised SQ_WAVE_CYCLES pass (round 4: trailing 13.2, substitutions 12.0, panels 3.2, Gram 2.9,
-// regions 1.75, unpack 1.4, chol_large 1.0 chip-ms) over its algorithmic work; the block chains
-// from the 9.6k-SNP block alone (tools/micro/tchol_alone.py: 14.7 ms) and the substitution
-// stamps; the chain slow-down under the device's other work and the serialisation of split units
-// that share a device from the round-5 one-GPU rehearsal (bench.py --predict 2,4,8: per-device
-// steps of 31.8 / 15.4 / 24.8 ms against a first model's 21.9 / 11.2 / 10.8).
+// regions 1.75, unpack 1.4, chol_large 1.0 chip-ms) over its algorithmic work, the Gram's rate by
+// block size from the uniform-block probes (profiles/r05/gram), the block chains from the 9.6k-SNP
+// block alone (tools/micro/tchol_alone.py: 14.7 ms); the remaining constants (busy fraction, chain
+// drags, pipeline rates, download) fitted to the round-5 one-GPU rehearsal (bench.py --predict
+// 2,4,8: 14 per-device steps, profiles/r05/shard/README).
 namespace shard {
-constexpr double kUnpackBps = 3.6e12;       // unpack: packed + operand bytes per second
-constexpr double kGramOps = 3.1e15;         // Gram: ops (2 per MAC) per second
+constexpr double kUnpackBps = 3.1e12;       // unpack: packed + operand bytes per second (alone)
+constexpr double kGramOpsSmall = 1.7e15;    // Gram ops (2 per MAC) per second, m <= 600 ...
+constexpr double kGramOpsBig = 3.4e15;      // ... m >= 4096 (log-linear between)
 constexpr double kTrailFlops = 62e12;       // tiled factorisation bulk (trailing update)
 constexpr double kPanelFlops = 68e12;       // panels: 2 x 128 x m^2 flops per block
 constexpr double kRegionChipUs = 0.17;      // regions: chip-us per 128 columns (86 us on half a CU)
 constexpr double kCholLargeFlops = 2e12;    // single-workgroup blocks (latency-bound)
 constexpr double kSubBps = 4.3e12;          // substitution passes: factor bytes per second
 constexpr double kChainRegionUs = 182.0;    // factorisation chain per 128 columns, block alone
-constexpr double kChainSubUs = 4.5;         // substitution chain per 64-row tile, per pass
-constexpr double kBusy = 0.85;              // fraction of the chip the overlapped phases keep busy
-constexpr double kDrag = 0.67;              // a chain's slow-down per chip-ms of other work beside it
+constexpr double kChainSubUs = 3.8;         // substitution chain per 64-row tile, per pass
+constexpr double kBusy = 0.9;               // fraction of the chip the overlapped phases keep busy
+constexpr double kDragWhole = 0.63;         // a whole block's chain: slow-down per chip-ms beside it
+constexpr double kDragSplit = 1.06;         // a split unit's chain (its own context, no priority)
+// the device's phases in sequence: unpack + Gram of everything, then the factorisations, then the
+// substitution passes (each group's passes wait for its factorisation), then the result download
+constexpr double kFrontRate = 0.79, kFacRate = 1.39, kSubRate = 0.73;
+constexpr double kDownloadMsPerM = 0.95;    // per million (SNP, h2f copy) results
 constexpr int kChebIters = 7;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 (plan.hip cheb_plan)
 constexpr int kTiledMin = 384;              // plan.hip kTiledMinDefault
 
 struct Cost {
-    double work;    // chip-ms
-    double chain;   // ms: the block's dependency chain when it runs alone
+    double work = 0.0;    // chip-ms
+    double chain = 0.0;   // ms: the block's dependency chain when it runs alone
+    double front = 0.0, fac = 0.0, sub = 0.0;   // chip-ms of the unpack + Gram / factorisation / passes
+    double results = 0.0;                       // (SNP, copy) results downloaded
 };
+
+static double gram_ops(double m) {
+    if (m <= 600.0) return kGramOpsSmall;
+    if (m >= 4096.0) return kGramOpsBig;
+    return kGramOpsSmall + std::log(m / 600.0) / std::log(4096.0 / 600.0) * (kGramOpsBig - kGramOpsSmall);
+}
 
 // Block of m SNPs, `copies` h2f solves; direct = every copy factored (a split unit is one direct
 // copy), else one factorisation + Chebyshev iterations for the other copies
 static Cost block_cost(double m, double n_ref, int copies, bool direct) {
-    Cost c{0.0, 0.0};
+    Cost c;
     if (m <= 0) return c;
     const double kp = std::ceil(n_ref / 128.0) * 128.0;
     const double unpack = m * (std::ceil(n_ref / 4.0) + kp / 4.0) / kUnpackBps * 1e3;
-    const double gram = n_ref * m * (m + 1.0) / kGramOps * 1e3;
+    const double gram = n_ref * m * (m + 1.0) / gram_ops(m) * 1e3;
     const int nfac = direct ? copies : 1;
     const double T = std::ceil(m / 64.0);
     const double pass_bytes = T * (T + 1.0) / 2.0 * 64.0 * 64.0 * 8.0;
     const int passes = direct ? copies : 1 + (copies > 1 ? 2 * kChebIters : 0);
-    c.work = unpack + gram;
+    c.front = unpack + gram;
+    c.results = m * copies;
     if (m >= kTiledMin) {
-        const double fac = m * m * m / 3.0 / kTrailFlops * 1e3 + 256.0 * m * m / kPanelFlops * 1e3 +
-                           m / 128.0 * kRegionChipUs * 1e-3;
-        c.work += nfac * fac + passes * pass_bytes / kSubBps * 1e3;
+        c.fac = nfac * (m * m * m / 3.0 / kTrailFlops * 1e3 + 256.0 * m * m / kPanelFlops * 1e3 +
+                        m / 128.0 * kRegionChipUs * 1e-3);
+        c.sub = passes * pass_bytes / kSubBps * 1e3;
         c.chain = gram + m / 128.0 * kChainRegionUs * 1e-3 + (direct ? 1 : passes) * T * kChainSubUs * 1e-3;
     } else {
-        c.work += (direct ? copies : 1) * m * m * m / 3.0 / kCholLargeFlops * 1e3;
+        c.fac = (direct ? copies : 1) * m * m * m / 3.0 / kCholLargeFlops * 1e3;
         c.chain = gram + m * 0.2e-3;   // ~0.2 us per column of the single-workgroup factorisation
     }
+    c.work = c.front + c.fac + c.sub;
     return c;
 }
 
-// One device's load: total work, the longest whole-block chain of its main job, and its split
-// units (contexts of their own: on the shared hardware queues their chains run one after the
-// other).  Predicted step = max(work / busy, critical chain + drag x the other work).
+// One device's load: total work, the longest whole-block chain of its main job, its split units
+// (contexts of their own: on the shared hardware queues their chains run one after the other) and
+// its phase totals.  Predicted step = the largest of work / busy, each kind of chain + drag x the
+// other work, and the phases in sequence.
 struct Dev {
     double work = 0.0, whole_chain = 0.0, whole_chain_work = 0.0, split_chain = 0.0, split_work = 0.0;
+    double front = 0.0, fac = 0.0, sub = 0.0, results = 0.0;
     int n_split = 0;
     double time() const {
-        const bool sp = split_chain >= whole_chain;
-        const double c = sp ? split_chain : whole_chain, cw = sp ? split_work : whole_chain_work;
-        return std::max(work / kBusy, c + kDrag * std::max(0.0, work - cw));
+        double t = work / kBusy;
+        if (whole_chain > 0) t = std::max(t, whole_chain + kDragWhole * std::max(0.0, work - whole_chain_work));
+        if (split_chain > 0) t = std::max(t, split_chain + kDragSplit * std::max(0.0, work - split_work));
+        return std::max(t, front / kFrontRate + fac / kFacRate + sub / kSubRate + kDownloadMsPerM * results * 1e-6);
     }
     void add(const Cost& k, bool split) {
         work += k.work;
+        front += k.front;
+        fac += k.fac;
+        sub += k.sub;
+        results += k.results;
         if (split) {
             split_chain += k.chain;
             split_work += k.work;
@@ -391,6 +414,47 @@ static int mp_download(dbslmm_plan* p, int copy, double* beta_s, double* beta_l,
         if (beta_s) for (size_t i = 0; i < bs.size(); ++i) beta_s[sh.s_idx[i]] = bs[i];
         if (beta_l) for (size_t i = 0; i < bl.size(); ++i) beta_l[sh.l_idx[i]] = bl[i];
         if (block_status) for (size_t i = 0; i < st.size(); ++i) block_status[sh.blocks[i]] = st[i];
+        return DBSLMM_OK;
+    });
+}
+
+// every solve of the last run (n = its sigmas), from every job in ONE pass: each job's copies come
+// down in one pipelined download (download_copies) into its reused staging, then each copy is
+// scattered into the caller's arrays at the caller's copy index (beta_s / beta_l / block_status:
+// n consecutive arrays of n_s / n_l / num_block, as dbslmm_plan_run_multi's outputs)
+static int mp_download_all(dbslmm_plan* p, int n, double* beta_s, double* beta_l, int32_t* block_status) {
+    auto& S = p->mp->shards;
+    if (block_status && !p->mp->partial)
+        for (int64_t i = 0; i < static_cast<int64_t>(n) * p->num_block; ++i) block_status[i] = DBSLMM_BLOCK_EMPTY;
+    return fan_out(p, [&](int d) -> int {
+        DeviceShard& sh = S[d];
+        const int nr = static_cast<int>(sh.run_copies.size());
+        if (nr == 0) return DBSLMM_OK;
+        const size_t ns = sh.s_idx.size(), nl = sh.l_idx.size(), nb = sh.blocks.size();
+        if (sh.dl_s.size() < nr * ns) sh.dl_s.resize(nr * ns);
+        if (sh.dl_l.size() < nr * nl) sh.dl_l.resize(nr * nl);
+        if (sh.dl_st.size() < nr * nb) sh.dl_st.resize(nr * nb);
+        const int rc = download_copies(sh.plan, 0, nr, sh.dl_s.data(), sh.dl_l.data(), sh.dl_st.data());
+        if (rc != DBSLMM_OK) return rc;
+        for (int k = 0; k < nr; ++k) {
+            const int64_t c = sh.run_copies[k];
+            if (c >= n) continue;
+            const double* bs = sh.dl_s.data() + k * ns;
+            const double* bl = sh.dl_l.data() + k * nl;
+            const int32_t* st = sh.dl_st.data() + k * nb;
+            if (beta_s) {
+                double* o = beta_s + c * p->n_s;
+                for (size_t i = 0; i < ns; ++i) o[sh.s_idx[i]] = bs[i];
+            }
+            if (beta_l) {
+                double* o = beta_l + c * p->n_l;
+                for (size_t i = 0; i < nl; ++i) o[sh.l_idx[i]] = bl[i];
+            }
+            if (block_status) {
+                int32_t* o = block_status + c * p->num_block;
+                for (size_t i = 0; i < nb; ++i) o[sh.blocks[i]] = st[i];
+            }
+        }
         return DBSLMM_OK;
     });
 }

@@ -132,6 +132,8 @@ struct DeviceShard {
     std::vector<int32_t> blocks;        // original block ids, in sub-problem order
     std::vector<int64_t> s_idx, l_idx;  // sub small / large SNP -> original beta position
     std::vector<int> run_copies;        // the caller's h2f copy of each of the plan's copies (last run)
+    std::vector<double> dl_s, dl_l;     // download staging of every run copy, reused across runs
+    std::vector<int32_t> dl_st;         //   (fresh vectors page-faulted ~1 ms per step on a big shard)
 };
 struct dbslmm_mplan {
     std::vector<DeviceShard> shards;
@@ -272,6 +274,7 @@ struct dbslmm_plan {
 static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out);
 static void mp_destroy(dbslmm_plan* p);
 static int mp_download(dbslmm_plan* p, int copy, double* beta_s, double* beta_l, int32_t* block_status);
+static int mp_download_all(dbslmm_plan* p, int n, double* beta_s, double* beta_l, int32_t* block_status);
 static int mp_run(dbslmm_plan* p, const double* sigmas, int n, bool wait);
 static int mp_sync(dbslmm_plan* p);
 static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diags, int32_t* n_test_out);
@@ -1127,7 +1130,23 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         // persistent workgroups then hold the CUs the lead factorisation's tail still needs)
         // (cheb_fused = 1 runs every Chebyshev pass of ALL tiled items in one launch: no groups)
         p->sub_split = op.sub_split >= 0 && !p->tl_rest.empty() && !p->cheb_fused;
-        p->sub_grid_lead = op.sub_grid_lead > 0 ? op.sub_grid_lead : std::max(1, ctx->n_cu * 5 / 16);
+        // lead workgroups by the lead group's share f of the factor bytes a pass streams:
+        // 2.05 f^1.5 of the CUs, within [1/16, 1/2]: config 4's f = 0.285 gives the 80 of 256 tuned
+        // there in round 4; a shard whose lead group is small (the bulk device of the 8-GPU plan,
+        // f = 0.135: 26) gives its rest group the CUs instead of leaving 5/16 of the chip to a few
+        // short chains (that device 19.4 ms at 80 lead workgroups, 17.1 at 24 / 32, 18.3 at 16)
+        {
+            double lb = 0.0, ab = 0.0;
+            for (int32_t b : p->h_tb) {
+                const double T = (mv[b] + trsv::kT - 1) / trsv::kT, by = T * (T + 1) / 2;
+                ab += by;
+                if (mv[b] >= lead_min) lb += by;
+            }
+            const double share = ab > 0 ? lb / ab : 0.0;
+            const int g = static_cast<int>(std::lround(ctx->n_cu * 2.05 * share * std::sqrt(share)));
+            p->sub_grid_lead = op.sub_grid_lead > 0 ? op.sub_grid_lead
+                                                    : std::clamp(g, std::max(1, ctx->n_cu / 16), std::max(1, ctx->n_cu / 2));
+        }
         p->sub_grid_rest = op.sub_grid_rest > 0 ? op.sub_grid_rest : std::max(1, ctx->n_cu - p->sub_grid_lead);
         auto grp_of = [&](int32_t b) { return p->sub_split && mv[b] < lead_min ? 1 : 0; };
         struct It { int grp; double key; int T; int32_t b, I; };
@@ -2224,10 +2243,7 @@ int dbslmm_plan_run_multi(dbslmm_plan* p, const double* sigmas, int32_t n_sigma,
             ARG_CHECK(ctx, static_cast<int64_t>(sh.plan->n_nonempty) * n_sigma < 32768,
                       "blocks x sigmas per device must stay below 32768 (packed work items)");
         int rc = mp_run(p, sigmas, n_sigma, true);
-        for (int i = 0; i < n_sigma && !rc; ++i)
-            rc = mp_download(p, i, beta_s ? beta_s + static_cast<int64_t>(i) * p->n_s : nullptr,
-                             beta_l ? beta_l + static_cast<int64_t>(i) * p->n_l : nullptr,
-                             block_status ? block_status + static_cast<int64_t>(i) * p->num_block : nullptr);
+        if (rc == DBSLMM_OK) rc = mp_download_all(p, n_sigma, beta_s, beta_l, block_status);
         return rc;
     }
     ARG_CHECK(ctx, static_cast<int64_t>(p->n_nonempty) * n_sigma < 32768,

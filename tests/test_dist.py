@@ -271,3 +271,29 @@ def test_unit_gather_per_step(tmp_path, world, k):
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)[:k]]
     for c, (bs, bl) in enumerate(_oracle_solve(prob, sig)):
         np.testing.assert_array_equal(got[c], np.concatenate([bs, bl]))
+
+
+@pytest.mark.gpu
+def test_unit_gather_device_scatter_rccl():
+    """The nccl (RCCL) path of UnitGather -- received segments scattered on the device, one copy
+    into pinned memory -- on a world-1 process group: every unit of every copy lands at its
+    original position, twice in a row (the reused buffers)."""
+    import torch
+    import torch.distributed as dist
+    from dbslmm_amd import dist as D
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        prob, m = _split_problem()
+        ud, _ = D.shard_units(m, prob.n_ref, 1, 3)
+        g = D.UnitGather(prob, ud, device="cuda")
+        rng = np.random.default_rng(5)
+        for _ in range(2):
+            bs, bl = rng.standard_normal((3, prob.n_s)), rng.standard_normal((3, prob.n_l))
+            res = g(bs, bl)
+            for c in range(3):
+                np.testing.assert_array_equal(res[c][0], bs[c])
+                np.testing.assert_array_equal(res[c][1], bl[c])
+    finally:
+        dist.destroy_process_group()
