@@ -95,10 +95,11 @@ def parse():
                     help="process group backend (nccl = RCCL over xGMI; gloo only for rehearsals)")
     ap.add_argument("--rank-device", type=int, default=None,
                     help="rehearsal on a 1-GPU box: every rank on this device instead of LOCAL_RANK")
-    ap.add_argument("--predict", default=None, metavar="N[,N..]",
+    ap.add_argument("--predict", default="auto", metavar="N[,N..]",
                     help="N = 1 only: one-GPU rehearsal of an N-GPU strong-scaling step -- each device's "
                          "units of the N-device shard plan timed alone on this GPU; predicted step = the "
-                         "slowest device (reported beside the line, never as value)")
+                         "slowest device (reported beside the line, never as value).  auto (default) = "
+                         "2,4,8 for the metric's workload (config 4), none elsewhere; none = off")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: independent replicas of the workload per rank (weak scaling) instead "
                          "of one problem sharded over the ranks (strong scaling)")
@@ -107,6 +108,10 @@ def parse():
         if getattr(a, k) is None:
             setattr(a, k, v)
     a.h2f = [float(x) for x in a.h2f.split(",")] if a.h2f else None
+    if a.predict == "auto":
+        a.predict = "2,4,8" if a.config == 4 and a.snps == CONFIGS[4]["snps"] else None
+    elif a.predict == "none":
+        a.predict = None
     return a
 
 

@@ -4,7 +4,7 @@
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/${GOUT:-ab}; mkdir -p $O
-B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e"
+B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --predict none --no-e2e"
 for i in 1 2; do
   for L in base ""; do
     N=${L:-new}

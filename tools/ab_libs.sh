@@ -8,7 +8,7 @@ mkdir -p gpurun_out/abl
 for r in $(seq 1 $rounds); do
   for lib in "$@"; do
     log=gpurun_out/abl/c${cfg}_$(basename $lib .so)_$r.log
-    DBSLMM_LIB_PATH=$PWD/$lib timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-isolated > $log 2>&1
+    DBSLMM_LIB_PATH=$PWD/$lib timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --predict none --no-e2e --no-isolated > $log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "FAILED rc=$rc ($lib)"; tail -5 $log; exit $rc; }
     python - "$lib" $log << 'PY'
 import json, sys

@@ -8,7 +8,7 @@ i=0
 for o in "$@"; do
   args=""
   for kv in $o; do args="$args --opt $kv"; done
-  timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-isolated $args > gpurun_out/ab/c${cfg}_$i.log 2>&1
+  timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --predict none --no-e2e --no-isolated $args > gpurun_out/ab/c${cfg}_$i.log 2>&1
   rc=$?
   [ $rc -eq 0 ] || { echo "FAILED rc=$rc ($o)"; tail -5 gpurun_out/ab/c${cfg}_$i.log; exit $rc; }
   python - "$o" gpurun_out/ab/c${cfg}_$i.log << 'PY'

@@ -19,7 +19,7 @@ step() {  # step <name> <timeout-s> <cmd...>
     esac
 }
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
-step bench 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
+step bench 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --predict none
 step rehearse_c3 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --config 3 --steps 5 --warmup 2 --dist-backend gloo --rank-device 0
 step rehearse_c4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --rank-device 0
 echo done

@@ -18,7 +18,7 @@ step() {  # step <name> <timeout-s> <cmd...>
     esac
 }
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
-step bench_c4 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline
-step bench_c5 600 python bench.py --config 5 --steps 10 --warmup 3 --no-cpu-baseline
-step bench_c3 600 python bench.py --config 3 --steps 10 --warmup 3 --no-cpu-baseline
+step bench_c4 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --predict none
+step bench_c5 600 python bench.py --config 5 --steps 10 --warmup 3 --no-cpu-baseline --predict none
+step bench_c3 600 python bench.py --config 3 --steps 10 --warmup 3 --no-cpu-baseline --predict none
 echo done

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc_c$N
 i=0
 for grp in "$@"; do
-  timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_c$N -o p$i -- python3 bench.py --config $N --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_c$N/p$i.log 2>&1
+  timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_c$N -o p$i -- python3 bench.py --config $N --steps 1 --warmup 0 --no-cpu-baseline --predict none > gpurun_out/pmc_c$N/p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc_c$N/p$i.log; exit $rc; }
   i=$((i+1))
 done

@@ -6,7 +6,7 @@ set -u
 O=${1:-gpurun_out/pmc_round}
 export TMPDIR=/tmp
 mkdir -p $O
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated --no-e2e"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --predict none --no-isolated --no-e2e"
 pass() {
   local name=$1; shift
   timeout -k 10 600 rocprofv3 --pmc "$@" --output-format csv -d $O -o $name -- $B > $O/$name.log 2>&1

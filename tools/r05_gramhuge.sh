@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${GOUT:-r05gh}; mkdir -p $O
 for r in 1 2; do
 for g in 384 256 192 128; do
-  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-e2e --opt gram_huge_min=$g > $O/c4_${g}_${r}.log 2>&1 || { echo FAILED; exit 1; }
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --predict none --no-e2e --opt gram_huge_min=$g > $O/c4_${g}_${r}.log 2>&1 || { echo FAILED; exit 1; }
   python - $g $O/c4_${g}_${r}.log << 'PY'
 import json, sys
 p = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -10,7 +10,7 @@ run 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method th
 run 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 run 400 python bench.py > $O/bench_c4.log 2>&1
 tail -1 $O/bench_c4.log > $O/bench_c4.json
-B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-isolated --no-e2e"
+B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --predict none --no-isolated --no-e2e"
 run 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o run -- $B > $O/c4_prof.log 2>&1
 run 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc4 -o fetch -- $B > $O/pmc4_fetch.log 2>&1
 run 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc4 -o write -- $B > $O/pmc4_write.log 2>&1

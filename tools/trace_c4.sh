@@ -4,4 +4,4 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
 rm -rf gpurun_out/c4t
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c4t -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-} > gpurun_out/c4t.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c4t -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --predict none --no-e2e ${BENCH_ARGS:-} > gpurun_out/c4t.log 2>&1

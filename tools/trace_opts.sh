@@ -8,7 +8,7 @@ for o in "$@"; do
   args=""
   for kv in $o; do args="$args --opt $kv"; done
   rm -rf gpurun_out/tr$i
-  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-isolated $args > gpurun_out/tr$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --predict none --no-e2e --no-isolated $args > gpurun_out/tr$i.log 2>&1
   rc=$?; echo "trace $i ($o) rc=$rc"; [ $rc -eq 0 ] || exit $rc
   i=$((i+1))
 done
