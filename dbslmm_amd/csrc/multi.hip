@@ -113,8 +113,12 @@ struct Dev {
         sub += k.sub;
         results += k.results;
         if (split) {
-            split_chain += k.chain;
-            split_work += k.work;
+            // a device's split units share one h2f copy (plan_units) and so one job: their chains
+            // advance together in the same launches, each slowed by the others' work (the drag)
+            if (k.chain > split_chain) {
+                split_chain = k.chain;
+                split_work = k.work;
+            }
             ++n_split;
         } else if (k.chain > whole_chain) {
             whole_chain = k.chain;
@@ -138,44 +142,57 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
         unit[b] = block_cost(m[b], n_ref, 1, true);
         total += whole[b].work;
     }
-    // Split the h2f copies of a block (one copy per device) when its whole chain exceeds both the
-    // fair share of the step and the chains already decided, and K devices without a split unit
-    // remain (two split units on one device run their chains one after the other); longest
-    // chain first.  Every split adds its extra factorisations to the total.
+    // Split the h2f copies of a block (copy c on device t K + c of a K-device group t) when its whole
+    // chain exceeds both the fair share of the step and the chains already decided; longest chain
+    // first.  A new group while K devices remain; after that a split block joins the group whose
+    // devices' predicted step grows least, if that beats its whole chain: the units of one copy on
+    // one device form ONE job (one plan, one launch sequence), so their chains run together --
+    // split units of different copies on one device would be separate jobs sharing the hardware
+    // queues, their chains one after the other, which the groups rule out.  Every split adds its
+    // extra factorisations to the total.
     std::vector<int32_t> byc;
     for (int b = 0; b < nb; ++b)
         if (m[b] > 0) byc.push_back(b);
     std::stable_sort(byc.begin(), byc.end(), [&](int32_t x, int32_t y) { return whole[x].chain > whole[y].chain; });
-    int free_dev = G;
+    std::vector<Dev> dev(G);
+    int n_grp = 0;
     double bound = 0.0;
+    auto place = [&](int32_t b, int t) {
+        for (int c = 0; c < K; ++c) {
+            dev[t * K + c].add(unit[b], true);
+            unit_device[static_cast<size_t>(b) * K + c] = t * K + c;
+        }
+        split[b] = 1;
+        total += K * unit[b].work - whole[b].work;
+    };
     for (int32_t b : byc) {
         const double share = total / (kBusy * G);
         if (whole[b].chain <= std::max(share, bound)) break;
-        if (K > 1 && free_dev >= K && unit[b].chain < whole[b].chain) {
-            split[b] = 1;
-            free_dev -= K;
-            total += K * unit[b].work - whole[b].work;
+        if (K == 1 || unit[b].chain >= whole[b].chain) {
+            bound = std::max(bound, whole[b].chain);
+            continue;
+        }
+        if ((n_grp + 1) * K <= G) {
+            place(b, n_grp++);
             bound = std::max(bound, unit[b].chain);
+            continue;
+        }
+        int best = -1;
+        double bt = 0.0;
+        for (int t = 0; t < n_grp; ++t) {
+            double v = 0.0;
+            for (int c = 0; c < K; ++c) {
+                Dev x = dev[t * K + c];
+                x.add(unit[b], true);
+                v = std::max(v, x.time());
+            }
+            if (best < 0 || v < bt - 1e-12) { best = t; bt = v; }
+        }
+        if (best >= 0 && bt < whole[b].chain) {
+            place(b, best);
+            bound = std::max(bound, bt);
         } else {
             bound = std::max(bound, whole[b].chain);
-        }
-    }
-    std::vector<Dev> dev(G);
-    // split units first, each copy on a device without a split unit (least loaded first)
-    for (int32_t b : byc) {
-        if (!split[b]) continue;
-        for (int c = 0; c < K; ++c) {
-            int best = -1;
-            for (int d = 0; d < G; ++d) {
-                bool taken = false;
-                for (int e = 0; e < c; ++e) taken |= unit_device[static_cast<size_t>(b) * K + e] == d;
-                if (taken) continue;
-                if (best < 0 || dev[d].n_split < dev[best].n_split ||
-                    (dev[d].n_split == dev[best].n_split && dev[d].time() < dev[best].time() - 1e-12))
-                    best = d;
-            }
-            dev[best].add(unit[b], true);
-            unit_device[static_cast<size_t>(b) * K + c] = best;
         }
     }
     // whole blocks: LPT by the predicted device step, longest first
@@ -248,7 +265,8 @@ static int mp_build(dbslmm_ctx* ctx, const dbslmm_problem* pr, int32_t K, const 
     p->mp->n_copies = K;
     p->mp->partial = partial;
     p->mp->unit_device = unit_device;
-    // jobs: per device its whole blocks (copy -1), then one job per split unit (copy c)
+    // jobs: per device its whole blocks (copy -1), then one job per h2f copy c holding the device's
+    // split units of that copy (shard::plan_units gives a device split units of one copy only)
     auto& J = p->mp->shards;
     for (int d : devs) {
         DeviceShard main_job;
@@ -261,19 +279,17 @@ static int mp_build(dbslmm_ctx* ctx, const dbslmm_problem* pr, int32_t K, const 
             if (whole) main_job.blocks.push_back(b);
         }
         J.push_back(std::move(main_job));
-        for (int b = 0; b < pr->num_block; ++b) {
-            const int32_t* ud = unit_device.data() + static_cast<size_t>(b) * K;
-            bool whole = true;
-            for (int c = 1; c < K; ++c) whole &= ud[c] == ud[0];
-            if (whole) continue;
-            for (int c = 0; c < K; ++c)
-                if (ud[c] == d) {
-                    DeviceShard u;
-                    u.device_index = d;
-                    u.copy = c;
-                    u.blocks.push_back(b);
-                    J.push_back(std::move(u));
-                }
+        for (int c = 0; c < K; ++c) {
+            DeviceShard u;
+            u.device_index = d;
+            u.copy = c;
+            for (int b = 0; b < pr->num_block; ++b) {
+                const int32_t* ud = unit_device.data() + static_cast<size_t>(b) * K;
+                bool whole = true;
+                for (int e = 1; e < K; ++e) whole &= ud[e] == ud[0];
+                if (!whole && ud[c] == d) u.blocks.push_back(b);
+            }
+            if (!u.blocks.empty()) J.push_back(std::move(u));
         }
     }
     // sub-problems with compact .bed images (rows renumbered in first-use order)

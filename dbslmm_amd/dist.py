@@ -54,16 +54,14 @@ def shard_blocks(m_per_block: np.ndarray, n_ref: int, world: int) -> list[np.nda
 
 def rank_jobs(unit_device: np.ndarray, rank: int):
     """The jobs of `rank` (the decomposition dbslmm_plan_create_units builds, multi.hip mp_build):
-    [(blocks, copies)] -- first its whole blocks with every copy, then one job per split unit
-    (one block, one copy)."""
+    [(blocks, copies)] -- first its whole blocks with every copy, then one job per h2f copy c
+    holding the rank's split units of that copy."""
     ud = np.asarray(unit_device)
     K = ud.shape[1]
     whole = np.all(ud == ud[:, :1], axis=1)
     jobs = [(np.flatnonzero(whole & (ud[:, 0] == rank)), list(range(K)))]
-    for b in np.flatnonzero(~whole):
-        for c in range(K):
-            if ud[b, c] == rank:
-                jobs.append((np.array([b]), [c]))
+    for c in range(K):
+        jobs.append((np.flatnonzero(~whole & (ud[:, c] == rank)), [c]))
     return [j for j in jobs if j[0].size]
 
 

@@ -79,10 +79,12 @@ def _config4_blocks():
 
 def test_shard_units_split_largest_blocks_copies():
     """h2f (3 copies): the blocks whose chain exceeds the fair share get one copy per device (three
-    distinct devices); every other block keeps its copies together; every unit has a device."""
+    distinct devices of a 3-device group); every other block keeps its copies together; every unit
+    has a device.  A device's split units all share one h2f copy (one job, chains run together):
+    at 4 GPUs both large blocks join the one group, at 8 each has a group of its own."""
     from dbslmm_amd.dist import shard_units
     m = _config4_blocks()
-    for world, want_split in ((1, 0), (2, 0), (4, 1), (8, 2)):
+    for world, want_split, groups in ((1, 0, 0), (2, 0, 0), (4, 2, 1), (8, 2, 2)):
         ud, ms = shard_units(m, 10000, world, 3)
         assert np.all((ud >= 0) == (m > 0)[:, None])
         split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
@@ -90,9 +92,12 @@ def test_shard_units_split_largest_blocks_copies():
         for b in split:
             assert len(set(ud[b].tolist())) == 3          # distinct devices
             assert m[b] >= np.sort(m)[-2]                  # the largest blocks
-        # split units never share a device (their chains would run one after the other)
-        split_dev = ud[split].ravel()
-        assert split_dev.size == np.unique(split_dev).size
+        # on a device, every split unit has the same copy (two copies would be two jobs sharing
+        # the device's hardware queues, their chains one after the other)
+        for d in range(world):
+            copies = {c for b in split for c in range(3) if ud[b, c] == d}
+            assert len(copies) <= 1, (world, d, copies)
+        assert len({tuple(ud[b].tolist()) for b in split}) == groups
         assert ms.size == world and np.all(ms > 0)
 
 
@@ -201,11 +206,11 @@ def test_compact_sub_problem_same_rows():
         np.testing.assert_array_equal(x, y)
 
 
-def _split_problem():
+def _split_problem(sizes=(60, 1600, 80, 100, 0, 40, 70)):
     """One dominant block (1600 SNPs) beside small ones: with 3 h2f copies on >= 3 ranks the shard
     plan splits that block's copies over three ranks."""
     from dbslmm_amd import BlockProblem, synth
-    sizes = [60, 1600, 80, 100, 0, 40, 70]
+    sizes = list(sizes)
     total = sum(sizes)
     p = synth.simulate(total + 50, 96, pop="EUR", chroms=[22], seed=6, large_every=0)
     rng = np.random.default_rng(6)

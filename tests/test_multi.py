@@ -187,3 +187,52 @@ def test_split_h2f_units_match_single_device():
         np.testing.assert_array_equal(a, x)
         np.testing.assert_array_equal(b, y)
         np.testing.assert_array_equal(c_, z)
+
+
+def test_two_split_blocks_share_one_job_per_device():
+    """Two dominant blocks and three devices (all device 0 here): both blocks' h2f copies are split
+    over the same 3-device group, so each device runs ONE job holding copy c of both blocks (their
+    chains in the same launches).  The base copy of both equals the one-device run bit for bit,
+    the other copies agree with it to cheb_tol and with the oracle's direct solve to 1e-10, every
+    other block bit for bit; the units plans of the torchrun ranks fill the same arrays."""
+    import oracle as O
+    from test_dist import _split_problem
+    from dbslmm_amd import Context, Plan
+    from dbslmm_amd.dist import rank_jobs, shard_units
+    prob, m = _split_problem((60, 1600, 80, 1400, 0, 40, 70))
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    ud, _ = shard_units(m, prob.n_ref, 3, 3)
+    split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
+    assert split.tolist() == [1, 3] and ud[1].tolist() == ud[3].tolist()
+    for d in range(3):   # one job per device for the split units
+        assert [j for j in rank_jobs(ud, d) if len(j[1]) == 1][0][0].tolist() == [1, 3]
+    single = Plan(Context(0), prob).run_multi(sig)
+    prob.opts["shard_copies"] = 3
+    many = Plan(Context(DEVS), prob)
+    got = many.run_multi(sig)
+    sl = np.concatenate([np.r_[prob.s_ptr[b]:prob.s_ptr[b + 1]] for b in split])
+    ll = np.concatenate([np.r_[prob.l_ptr[b]:prob.l_ptr[b + 1]] for b in split])
+    keep_s = np.setdiff1d(np.arange(prob.n_s), sl)
+    keep_l = np.setdiff1d(np.arange(prob.n_l), ll)
+    for c in range(3):
+        np.testing.assert_array_equal(got[c][0][keep_s], single[c][0][keep_s])
+        np.testing.assert_array_equal(got[c][1][keep_l], single[c][1][keep_l])
+        np.testing.assert_array_equal(got[c][2], single[c][2])
+        g = np.concatenate([got[c][0][sl], got[c][1][ll]])
+        o = np.concatenate([single[c][0][sl], single[c][1][ll]])
+        if c == 1:
+            np.testing.assert_array_equal(g, o)
+        else:
+            assert normwise(g, o) < 1e-8, c
+        rs, rl, _, _ = O.est(prob.bed, prob.n_ref, prob.n_obs, sig[c], prob.s_ptr, prob.s_pos, prob.z_s,
+                             prob.l_ptr, prob.l_pos, prob.z_l, method="direct")
+        assert normwise(np.concatenate([got[c][0], got[c][1]]), np.concatenate([rs, rl])) < 1e-10, c
+    bs, bl = np.full((3, prob.n_s), np.nan), np.full((3, prob.n_l), np.nan)
+    st = np.full((3, prob.num_block), -7, dtype=np.int32)
+    for d in range(3):
+        u = Plan.units(Context(0), prob, ud, d)
+        u.run_multi(sig, out=(bs, bl, st))
+        u.close()
+    for c in range(3):
+        np.testing.assert_array_equal(bs[c], got[c][0])
+        np.testing.assert_array_equal(bl[c], got[c][1])
