@@ -10,8 +10,8 @@ compute.  One process per GPU (torch.distributed, backend "nccl" = RCCL over xGM
    model of one MI355X -- per-block chip time of each kernel class plus the block's dependency
    chain alone; a block's h2f copies are split over devices only when its chain exceeds the fair
    share of the step);
-2. each rank solves its units on its own GPU (`Plan.units`: its whole blocks in one plan, each split
-   copy in a single-copy plan on its own streams beside it);
+2. each rank solves its units on its own GPU (`Plan.units`: its whole blocks in one plan, its split
+   units -- all of one h2f copy -- in a single-copy plan on its own streams beside it);
 3. the betas (fp64, <= 8 MB per h2f solve at 1M SNPs) are gathered to rank 0 in the original order
    -- the only collective, one `gather` of this rank's unit values per step.
 """

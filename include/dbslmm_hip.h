@@ -190,7 +190,9 @@ int dbslmm_ctx_create_multi(int32_t n_dev, const int32_t* device_ids, dbslmm_ctx
  * devices.  m[b] = SNPs of block b (small + large), n_copies = h2f solves per run (1: single solves).
  * A block's copies stay on one device (one Gram, one factorisation, the other copies iterated on
  * it) unless the block's dependency chain exceeds the fair share of the step and n_dev >= n_copies:
- * then each copy is a unit of its own, factored directly, on distinct devices.  Units go to devices
+ * then each copy is a unit of its own, factored directly, copy c on device c of a group of n_copies
+ * devices (several split blocks may share a group: a device's split units are all of one copy and
+ * are solved as one job, their chains together).  Whole blocks go to devices
  * longest-first by a time model of one MI355X (per-block chip time of each kernel class and the
  * block's chain alone).  Out: unit_device[b * n_copies + c] = the device index
  * of copy c of block b (-1: empty block); dev_ms (optional, n_dev entries) = the model's predicted
@@ -200,8 +202,8 @@ int dbslmm_shard_plan(int32_t num_block, const int32_t* m, int32_t n_ref, int32_
                       int32_t* unit_device, double* dev_ms);
 /* A plan over ONE device's units of a shard plan (ABI 10), on a single-device context: the same
  * problem as dbslmm_plan_create (the whole .bed image and CSR arrays), solving only the units with
- * unit_device[b * n_copies + c] == device_index (split units on contexts of their own on the same
- * GPU, so they run beside the device's whole blocks).  run_multi / download / variance write only
+ * unit_device[b * n_copies + c] == device_index (its split units -- all of one h2f copy -- as one
+ * job on a context of its own on the same GPU, so they run beside the device's whole blocks).  run_multi / download / variance write only
  * those units' entries of the caller's full-size arrays; everything else is left untouched, so
  * one process per GPU (bench.py under torch.distributed) solves its part and gathers the rest.
  * Run it with n_sigma == n_copies (otherwise a split block is solved whole by the device of its
