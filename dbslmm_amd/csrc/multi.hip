@@ -40,8 +40,12 @@ constexpr double kPanelFlops = 68e12;       // panels: 2 x 128 x m^2 flops per b
 constexpr double kRegionChipUs = 0.17;      // regions: chip-us per 128 columns (86 us on half a CU)
 constexpr double kCholLargeFlops = 2e12;    // single-workgroup blocks (latency-bound)
 constexpr double kSubBps = 4.3e12;          // substitution passes: factor bytes per second
-constexpr double kChainRegionUs = 182.0;    // factorisation chain per 128 columns, block alone
-constexpr double kChainSubUs = 3.8;         // substitution chain per 64-row tile, per pass
+// factorisation chain per 128 columns of a block alone: 128 us up to 4000 SNPs, then growing with
+// the far updates the chain's launches wait beside (+0.0107 us per SNP above 4000): one block alone,
+// unpack to beta, 1.71 / 2.74 / 4.21 / 6.75 / 10.05 / 14.60 ms at 1.6k / 2.6k / 4k / 5.5k / 7.5k /
+// 9.6k SNPs (profiles/r05/chain/alone_by_size.txt)
+constexpr double kChainRegionUs = 128.0, kChainRegionGrow = 0.0107, kChainRegionKnee = 4000.0;
+constexpr double kChainSubUs = 4.5;         // substitution chain per 64-row tile, per pass (in situ)
 constexpr double kBusy = 0.9;               // fraction of the chip the overlapped phases keep busy
 constexpr double kDragWhole = 0.63;         // a whole block's chain: slow-down per chip-ms beside it
 constexpr double kDragSplit = 1.06;         // a split unit's chain (its own context, no priority)
@@ -83,7 +87,8 @@ static Cost block_cost(double m, double n_ref, int copies, bool direct) {
         c.fac = nfac * (m * m * m / 3.0 / kTrailFlops * 1e3 + 256.0 * m * m / kPanelFlops * 1e3 +
                         m / 128.0 * kRegionChipUs * 1e-3);
         c.sub = passes * pass_bytes / kSubBps * 1e3;
-        c.chain = gram + m / 128.0 * kChainRegionUs * 1e-3 + (direct ? 1 : passes) * T * kChainSubUs * 1e-3;
+        const double region_us = kChainRegionUs + kChainRegionGrow * std::max(0.0, m - kChainRegionKnee);
+        c.chain = gram + m / 128.0 * region_us * 1e-3 + (direct ? 1 : passes) * T * kChainSubUs * 1e-3;
     } else {
         c.fac = (direct ? copies : 1) * m * m * m / 3.0 / kCholLargeFlops * 1e3;
         c.chain = gram + m * 0.2e-3;   // ~0.2 us per column of the single-workgroup factorisation
