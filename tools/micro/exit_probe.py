@@ -31,12 +31,20 @@ variants = [("pipe", d, subprocess.PIPE), ("pipe", d, subprocess.PIPE), ("shm", 
             ("devnull", d, subprocess.DEVNULL), ("pipe", d, subprocess.PIPE)]
 if os.environ.get("EXIT_PROBE_H2F"):   # 3 h2f copies (22 GB of block matrices) vs 1 (7.5 GB), alternating
     variants = [("h2f", d, subprocess.PIPE), ("single", d, subprocess.PIPE)] * 3
+if os.environ.get("EXIT_PROBE_QUEUES"):   # hardware queues of the CLI process: default (4) vs 2 / 3
+    variants = [("pipe", d, subprocess.PIPE), ("q2", d, subprocess.PIPE), ("q3", d, subprocess.PIPE)] * 3
+settle = float(os.environ.get("EXIT_PROBE_SETTLE", "0"))   # seconds between runs
 for label, outdir, sink in variants:
+    if settle:
+        time.sleep(settle)
     cmd = base + ["-eff", os.path.join(outdir, "eff")]
     if label == "single":
         cmd = [x for x in cmd if x not in ("-h2f", "0.8,1,1.2")]
     t0 = time.time()
-    p = subprocess.Popen(cmd, stdout=sink, stderr=subprocess.PIPE, text=True)
+    env = None
+    if label in ("q2", "q3"):
+        env = dict(os.environ, GPU_MAX_HW_QUEUES=label[1])
+    p = subprocess.Popen(cmd, stdout=sink, stderr=subprocess.PIPE, text=True, env=env)
     _, err = p.communicate(timeout=600)
     t1 = time.time()
     ph = {}
