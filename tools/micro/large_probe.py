@@ -45,5 +45,5 @@ ms, nrun = plan.kernel_ms()
 print("m", m, "blocks", nblk, "per run (ms):", {k: round(v / max(nrun, 1), 3) for k, v in zip(_lib.KERNEL_NAMES, ms)})
 if STAMPS:
     L.dbslmm_debug_stamps(out.ctypes.data_as(C.c_void_p))
-    ph = out[:4] / reps / nblk / 1e2    # 100 MHz ticks -> us per block
+    ph = out[:4] / reps / nblk / 1e3    # counter ticks -> us per block (the scale region_probe.py uses; it matches the kernel traces)
     print("per block us: diag0 %.1f  panels %.1f  trailing (+ lookahead factor) %.1f  backward %.1f" % tuple(ph))
