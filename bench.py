@@ -740,7 +740,8 @@ def main():
             par = f"{world} independent replicas (no exchange)"
         elif world > 1:
             par = (f"LD blocks of one problem sharded over {world} GPU(s) (LPT, one process per GPU), "
-                   f"betas gathered to rank 0 by one RCCL gather per step")
+                   f"betas gathered to rank 0 by one {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
+                   f"gather per step")
         else:
             par = "1 GPU"
         line = {
