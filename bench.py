@@ -733,13 +733,14 @@ def main():
 
     if rank == 0:
         if in_proc:
-            par = (f"LD blocks of one problem sharded over {n_gpus} GPU(s) {devices} by the product's "
-                   f"multi-device context (dbslmm_ctx_create_multi: LPT shards, one host thread per "
-                   f"device, betas copied from each device to the caller's arrays)")
+            par = (f"(LD block, h2f copy) units of one problem sharded over {n_gpus} GPU(s) {devices} by the "
+                   f"product's multi-device context (dbslmm_ctx_create_multi: time-model shard plan, one host "
+                   f"thread per job, betas copied from each device to the caller's arrays)")
         elif args.replicas:
             par = f"{world} independent replicas (no exchange)"
         elif world > 1:
-            par = (f"LD blocks of one problem sharded over {world} GPU(s) (LPT, one process per GPU), "
+            par = (f"(LD block, h2f copy) units of one problem sharded over {world} GPU(s) by the time-model "
+                   f"shard plan (dbslmm_shard_plan, one process per GPU), "
                    f"betas gathered to rank 0 by one {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} "
                    f"gather per step")
         else:
