@@ -23,7 +23,7 @@ EXPORTS = (
     "dbslmm_shard_plan", "dbslmm_plan_create_units",
 )
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv")
@@ -38,7 +38,7 @@ class Options(C.Structure):
         ("h2f_mode", C.c_int32), ("cheb_tol", C.c_double), ("lead_min", C.c_int32),
         ("large_cheb", C.c_int32), ("cheb_fused", C.c_int32), ("debug_delay_us", C.c_int32),
         ("debug_stop", C.c_int32), ("sub_split", C.c_int32), ("sub_grid_lead", C.c_int32),
-        ("sub_grid_rest", C.c_int32), ("shard_copies", C.c_int32),
+        ("sub_grid_rest", C.c_int32), ("shard_copies", C.c_int32), ("h2f_iter", C.c_int32),
     ]
 
 

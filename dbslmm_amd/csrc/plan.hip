@@ -223,6 +223,9 @@ struct dbslmm_plan {
     bool large_cheb_ok = true;               // dbslmm_options.large_cheb and every chol_large block
                                              // fits dbslmm_chol_cheb (ld <= chol::kChebMaxM)
     bool cheb_fused = false;                 // dbslmm_options.cheb_fused
+    bool h2f_cg = false;                     // dbslmm_options.h2f_iter: the tiled blocks' copies by CG
+    double* d_cgrec = nullptr;               // CG: per non-empty block and copy {gamma, alpha}
+    int32_t* d_cgconv = nullptr;             // CG: per non-empty block, its copies have converged
     int32_t debug_delay_us = 0;              // dbslmm_options.debug_delay_us (tests)
     int32_t debug_stop = 0;                  // dbslmm_options.debug_stop (tests)
     int64_t n_runs = 0;                      // completed run enqueues (graphs are captured from the second)
@@ -817,7 +820,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
                     p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items,
-                    p->d_tcheb_blocks};
+                    p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -867,9 +870,10 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    op.debug_delay_us >= -100000 && op.debug_delay_us <= 100000 &&
                    (op.debug_stop == 0 || op.debug_stop == 1) && op.sub_split >= -1 && op.sub_split <= 2 &&
                    op.sub_grid_lead >= 0 && op.sub_grid_rest >= 0 && op.shard_copies >= 0 &&
-                   op.shard_copies <= 64, "bad dbslmm_options");
+                   op.shard_copies <= 64 && op.h2f_iter >= 0 && op.h2f_iter <= 2, "bad dbslmm_options");
     p->h2f_mode = op.h2f_mode;
     p->cheb_fused = op.cheb_fused == 1;
+    p->h2f_cg = op.h2f_iter == 2;
     p->debug_delay_us = op.debug_delay_us;
     p->debug_stop = op.debug_stop;
     if (op.cheb_tol > 0.0) p->cheb_tol = std::max(1e-16, op.cheb_tol);
@@ -1546,6 +1550,7 @@ static int run_rest_copy(dbslmm_plan* p, double isn, int copy) {
 // ---- h2f tuning by Chebyshev on one factor (trsv.hip)
 struct ChebPlan {
     int base = -1;
+    double db = 0.0;                  // the base copy's shift d_b = 1 / (sigma_b n)
     std::vector<int> others;          // copies solved by iteration, in launch groups of kMaxR
     std::vector<int> iters;           // per group
     std::vector<double> coef;         // per group: [iters][nr][3] {alpha, beta, delta}
@@ -1564,6 +1569,7 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
     cp.base = idx[n / 2];
     const double nobs = static_cast<double>(p->n_obs);
     const double db = 1.0 / (sigmas[cp.base] * nobs);
+    cp.db = db;
     const double floor_ = db + 1.0 - p->tau;
     const double tol = p->cheb_tol;
     for (int c = 0; c < n; ++c)
@@ -1628,6 +1634,12 @@ static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
     if (!p->d_cheb) {
         std::lock_guard<std::mutex> lk(g_capture_mu);
         HIP_TRY(ctx, hipMalloc(&p->d_cheb, 6 * trsv::kMaxR * vs * sizeof(double)));
+    }
+    if (p->h2f_cg && !p->d_cgconv) {
+        std::lock_guard<std::mutex> lk(g_capture_mu);
+        const size_t nb = std::max(1, p->n_nonempty);
+        HIP_TRY(ctx, hipMalloc(&p->d_cgrec, nb * trsv::kMaxR * 2 * sizeof(double)));
+        HIP_TRY(ctx, hipMalloc(&p->d_cgconv, nb * sizeof(int32_t)));
     }
     // the coefficients depend only on the sigmas: uploaded when they change, synchronously (the
     // host vector is a temporary of the run; an asynchronous copy from pageable memory may still
@@ -1696,6 +1708,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
     hipStream_t st = grp.st;
     if (grp.n_items == 0) return DBSLMM_OK;
     const bool fused = p->cheb_fused && grp.item_off == 0 && grp.n_items == p->n_titems;
+    const bool cg = p->h2f_cg && !fused;   // (the fused launch iterates by Chebyshev)
     const int64_t vs = std::max<int64_t>(1, p->n_slots);
     const int64_t blk = trsv::kMaxR * vs;
     double *Y = p->d_cheb, *Z = Y + blk, *X = Z + blk, *R = X + blk, *D = R + blk, *S = D + blk;
@@ -1720,7 +1733,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
         hipLaunchKernelGGL(dbslmm_cheb_init, dim3(grp.n_tb), dim3(256), 0, st, p->d_tb + grp.tb_off, p->d_row0, p->d_m,
                            p->d_ms, p->d_blk_id, p->d_y + static_cast<int64_t>(cp.base) * p->n_slots, coef,
                            nr, vs, X, R, D, S, p->d_status + cp.base * p->nbk, p->d_status, p->nbk,
-                           cix[0], cix[1]);
+                           cix[0], cix[1], cg ? p->d_cgconv : nullptr);
         HIP_TRY(ctx, hipGetLastError());
         trsv::Args a{};
         a.M = p->d_M + static_cast<int64_t>(cp.base) * p->M_elems;
@@ -1764,7 +1777,40 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
 #endif
         if (!fused) {   // one launch per pass (the launch boundary orders the passes)
             a.n_items = grp.n_items;
-            for (int k = 0; k < K; ++k)
+            trsv::CGArgs ca{};
+            if (cg) {   // K (the a priori Chebyshev count) caps the iterations
+                a.mode = 2;
+                a.conv = p->d_cgconv;
+                ca.tb = p->d_tb + grp.tb_off;
+                ca.row0 = p->d_row0;
+                ca.m = p->d_m;
+                ca.ms = p->d_ms;
+                ca.blk_id = p->d_blk_id;
+                ca.slot_out = p->d_slot_out;
+                ca.st_base = a.status;
+                ca.nr = nr;
+                ca.vs = vs;
+                ca.Z = Z;
+                ca.X = X;
+                ca.R = R;
+                ca.D = D;
+                ca.S = S;
+                for (int j = 0; j < nr; ++j) {
+                    ca.delta[j] = cp.coef[cp.coef_off[g] + 3 * j + 2];
+                    ca.floor_s[j] = cp.db + ca.delta[j] + 1.0 - p->tau;
+                    ca.cix[j] = cix[j];
+                }
+                ca.floor_l = 1.0 - p->tau;
+                ca.tol = p->cheb_tol;
+                ca.rec = p->d_cgrec;
+                ca.conv = p->d_cgconv;
+                ca.inv_sqrt_n = isn;
+                ca.beta_s = p->d_beta_s;
+                ca.beta_l = p->d_beta_l;
+                ca.ns_stride = p->n_s;
+                ca.nl_stride = p->n_l;
+            }
+            for (int k = 0; k < K; ++k) {
                 for (int pass = 0; pass < 2; ++pass) {
                     const bool fwd = pass == 0;
                     if (const int rc = next_epoch(p, 1)) return rc;
@@ -1779,6 +1825,13 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
                     HIP_TRY(ctx, hipGetLastError());
                     p->trsv_pending = true;
                 }
+                if (cg) {
+                    ca.k = k;
+                    ca.last = k == K - 1;
+                    hipLaunchKernelGGL(dbslmm_cg_update, dim3(grp.n_tb), dim3(trsv::kCGThreads), 0, st, ca);
+                    HIP_TRY(ctx, hipGetLastError());
+                }
+            }
             continue;
         }
         a.fused = 1;

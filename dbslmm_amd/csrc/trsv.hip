@@ -87,7 +87,10 @@ struct Args {
     int32_t cix[kMaxR];
     const int32_t* status;       // the base copy's block status
     int32_t mode;                // backward: 0 Chebyshev epilogue; 1 plain solve of the factored
-                                 // system (y = the matrix's z row, x -> X, beta of copy cix[0])
+                                 // system (y = the matrix's z row, x -> X, beta of copy cix[0]);
+                                 // 2 CG: z only (dbslmm_cg_update does the block's update)
+    const int32_t* conv;         // CG: per plan block, nonzero once every copy has converged (its
+                                 // items are skipped); nullptr otherwise
     unsigned long long* stamps;  // diagnostic build (DBSLMM_DIAG, env DBSLMM_TRSV_STAMPS): per tile of block stamp_b,
     int32_t stamp_b;             // 100 MHz times [claim, last hand-off staged, stream done, publish]
     // all passes of a Chebyshev group in one launch (dbslmm_trsv_cheb): pass p = 2 k (+1 for the
@@ -295,7 +298,7 @@ __device__ __forceinline__ void tile_item(const trsv::Args& a, const trsv::Pass&
         const int vv = lane / kG, vk = vv / NR, vc = vv - vk * NR, vr = 8 * wave + vk;
         const double* sp = ps.src + vc * a.vs + g0 + r0 + vr;
         const double src = vr >= jmax ? 0.0
-                           : (bwd && a.mode) ? A[static_cast<int64_t>(m) * ld + r0 + vr]   // bordered row m: y = L^-1 z
+                           : (bwd && a.mode == 1) ? A[static_cast<int64_t>(m) * ld + r0 + vr]   // bordered row m: y = L^-1 z
                                              : a.fused ? ld_sc1(sp) : *sp;
         const double* Lw = A + static_cast<int64_t>(r0 + 8 * wave) * ld + lane;   // rows of tile I
         double acc[8][NR];
@@ -374,7 +377,7 @@ __device__ __forceinline__ void tile_item(const trsv::Args& a, const trsv::Pass&
     if (tid == 0) stamp(a, b, I, 6);
     publish(a.flags + a.foff[b] + I, ps.epoch, tid);   // (its barrier also frees ws and orders zt)
     if (tid == 0) stamp(a, b, I, 3);
-    if (!bwd) return;
+    if (!bwd || a.mode == 2) return;
     // Chebyshev epilogue: d = alpha d + beta z; s = alpha s + beta r; x += d;
     // r -= s + delta P_s d  (this tile's rows; read and written only here in this pass)
     if (tid < kT * NR) {
@@ -430,6 +433,7 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_fwd(trsv::Args 
         if (it >= a.n_items) break;
         const int b = __builtin_amdgcn_readfirstlane(a.items[2 * it]);
         const int I = __builtin_amdgcn_readfirstlane(a.items[2 * it + 1]);
+        if (a.conv && __builtin_amdgcn_readfirstlane(a.conv[b]) != 0) continue;   // CG: converged block
         tile_item<NR>(a, pass_of(a), rg, lds, b, I, false, nullptr, 0, tid);
     }
 }
@@ -445,6 +449,7 @@ __global__ __launch_bounds__(trsv::kThreads, 1) void dbslmm_trsv_bwd(trsv::Args 
         if (it >= a.n_items) break;
         const int b = __builtin_amdgcn_readfirstlane(a.items[2 * it]);
         const int I = __builtin_amdgcn_readfirstlane(a.items[2 * it + 1]);
+        if (a.conv && __builtin_amdgcn_readfirstlane(a.conv[b]) != 0) continue;   // CG: converged block
         tile_item<NR>(a, pass_of(a), rg, lds, b, I, true, nullptr, 0, tid);
     }
 }
@@ -484,9 +489,10 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_cheb_init(
     const int32_t* __restrict__ tb, const int32_t* __restrict__ row0, const int32_t* __restrict__ mv,
     const int32_t* __restrict__ msv, const int32_t* __restrict__ blk_id, const double* __restrict__ xbase,
     const double* __restrict__ coef0, int nr, int64_t vs, double* X, double* R, double* D, double* S,
-    const int32_t* __restrict__ st_base, int32_t* st, int64_t st_stride, int c0, int c1) {
+    const int32_t* __restrict__ st_base, int32_t* st, int64_t st_stride, int c0, int c1, int32_t* conv) {
     const int b = tb[blockIdx.x];
     const int g0 = row0[b], m = mv[b], ms = msv[b];
+    if (conv && threadIdx.x == 0) conv[b] = 0;   // CG (dbslmm_cg_update): the block iterates
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         const double xb = xbase[g0 + i];
         for (int c = 0; c < nr; ++c) {
@@ -498,6 +504,152 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_cheb_init(
         }
     }
     if (threadIdx.x < nr) st[(threadIdx.x == 0 ? c0 : c1) * st_stride + blk_id[b]] = st_base[blk_id[b]];
+}
+
+// ---------------------------------------------------------------- h2f by conjugate gradients
+// The copies' iteration as preconditioned CG (dbslmm_options.h2f_iter = 1) instead of Chebyshev:
+// same operator M_c = M_b + delta P_s, same preconditioner (the base factor: one forward and one
+// backward pass per iteration), same state vectors (D = p, S = q = M_c p), and no product with
+// M_b either -- the Chronopoulos-Gear form takes both inner products from r and z = M_b^{-1} r:
+//     gamma = r.z,  eta = z.M_c z = gamma + delta |P_s z|^2   (M_b z = r)
+//     beta = gamma / gamma_prev,  alpha = gamma / (eta - beta gamma / alpha_prev)
+//     p = z + beta p,  q = r + delta P_s z + beta q,  x += alpha p,  r -= alpha q.
+// CG adapts to the block's actual spectrum (M_b^{-1} M_c within [1 + delta / lambda_max(M_b),
+// 1 + delta / (d_b + 1 - tau)], not the a priori [1, ...] the Chebyshev coefficients must cover),
+// so it stops early: after each update a copy has converged when |r| <= cheb_tol lambda_min(M_c)
+// |x| (a bound on the relative error, lambda_min(M_c) >= d_c + 1 - tau, or 1 - tau for a block
+// with large SNPs).  A block whose copies have all converged writes its betas and sets conv[b]:
+// the later passes skip its items (tools/cheb_vs_cg.py: 5 iterations on config 4's blocks of
+// 544 - 9667 SNPs where Chebyshev needs 7; the a priori Chebyshev count stays the cap).
+// One workgroup per tiled block of the group, after each backward pass; reductions in a fixed
+// order (deterministic).
+namespace trsv {
+constexpr int kCGThreads = 512;
+struct CGArgs {
+    const int32_t* tb;           // the group's tiled blocks (plan block ids)
+    const int32_t* row0;
+    const int32_t* m;
+    const int32_t* ms;
+    const int32_t* blk_id;
+    const int32_t* slot_out;
+    const int32_t* st_base;      // the base copy's block status
+    int32_t nr, k, last;
+    int64_t vs;
+    const double* Z;             // z = M_b^{-1} r (the backward pass's result)
+    double* X;
+    double* R;
+    double* D;                   // p
+    double* S;                   // q = M_c p
+    double delta[kMaxR];
+    double floor_s[kMaxR];       // lambda_min(M_c) bound of a block without large SNPs: d_c + 1 - tau
+    double floor_l;              // ... with large SNPs: 1 - tau
+    double tol;
+    double* rec;                 // per plan block and copy: {gamma, alpha} of the previous iteration
+    int32_t* conv;
+    double inv_sqrt_n;
+    double* beta_s;
+    double* beta_l;
+    int64_t ns_stride, nl_stride;
+    int32_t cix[kMaxR];
+};
+// sums of v[0..4) over the workgroup, in a fixed order; every thread gets the totals
+__device__ __forceinline__ void cg_sum4(double (&v)[4], double (*red)[4], int tid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int sft = 32; sft >= 1; sft >>= 1) v[j] += __shfl_xor(v[j], sft);
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[tid >> 6][j] = v[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double t = 0.0;
+        for (int w = 0; w < kCGThreads / 64; ++w) t += red[w][j];
+        v[j] = t;
+    }
+    __syncthreads();
+}
+}  // namespace trsv
+
+extern "C" __global__ __launch_bounds__(trsv::kCGThreads) void dbslmm_cg_update(trsv::CGArgs a) {
+    using namespace trsv;
+    __shared__ double red[kCGThreads / 64][4];
+    __shared__ double sc[2 * kMaxR];
+    const int b = a.tb[blockIdx.x];
+    if (a.conv[b]) return;
+    const int tid = threadIdx.x;
+    const int g0 = a.row0[b], m = a.m[b], ms = a.ms[b];
+    const bool fail = a.st_base[a.blk_id[b]] >= DBSLMM_BLOCK_NOT_PD;
+    // gamma_c = r.z, zeta_c = |P_s z|^2
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = tid; i < m; i += kCGThreads)
+#pragma unroll
+        for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
+            const int64_t o = c * a.vs + g0 + i;
+            const double z = a.Z[o];
+            v[2 * c] += a.R[o] * z;
+            if (i < ms) v[2 * c + 1] += z * z;
+        }
+    cg_sum4(v, red, tid);
+    if (tid == 0)
+#pragma unroll
+        for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
+            double* rc = a.rec + (static_cast<int64_t>(b) * kMaxR + c) * 2;
+            const double gam = v[2 * c], eta = gam + a.delta[c] * v[2 * c + 1];
+            double be = 0.0, den = eta;
+            if (a.k > 0) {
+                be = rc[0] > 0.0 ? gam / rc[0] : 0.0;
+                den = eta - (rc[1] != 0.0 ? be * gam / rc[1] : 0.0);
+            }
+            const double al = den > 0.0 && gam > 0.0 ? gam / den : 0.0;
+            sc[2 * c] = al;
+            sc[2 * c + 1] = be;
+            rc[0] = gam;
+            rc[1] = al;
+        }
+    __syncthreads();
+    // the update; |r|^2 and |x|^2 of the new iterate
+    double w[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = tid; i < m; i += kCGThreads)
+#pragma unroll
+        for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
+            const int64_t o = c * a.vs + g0 + i;
+            const double al = sc[2 * c], be = sc[2 * c + 1];
+            const double z = a.Z[o], r = a.R[o];
+            const double p = z + be * a.D[o];
+            const double q = r + (i < ms ? a.delta[c] * z : 0.0) + be * a.S[o];
+            const double x = a.X[o] + al * p;
+            const double rn = r - al * q;
+            a.D[o] = p;
+            a.S[o] = q;
+            a.X[o] = x;
+            a.R[o] = rn;
+            w[2 * c] += rn * rn;
+            w[2 * c + 1] += x * x;
+        }
+    cg_sum4(w, red, tid);
+    bool done = a.last || fail;
+    if (!done) {
+        done = true;
+#pragma unroll
+        for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
+            const double t = a.tol * (ms == m ? a.floor_s[c] : a.floor_l);
+            done = done && w[2 * c] <= t * t * w[2 * c + 1];   // NaN: not converged
+        }
+    }
+    if (!done) return;
+    for (int i = tid; i < m; i += kCGThreads) {   // this thread's own x entries
+        const int so = a.slot_out[g0 + i];
+#pragma unroll
+        for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
+            const double x = a.X[c * a.vs + g0 + i];
+            const double bv = fail ? __builtin_nan("") : x * a.inv_sqrt_n;
+            if (so >= 0) a.beta_s[a.cix[c] * a.ns_stride + so] = bv;
+            else a.beta_l[a.cix[c] * a.nl_stride - 1 - so] = bv;
+        }
+    }
+    if (tid == 0) a.conv[b] = 1;
 }
 
 // ---------------------------------------------------------------- whole-block Chebyshev passes

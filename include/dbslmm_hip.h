@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 10
+#define DBSLMM_ABI_VERSION 11
 
 enum {
     DBSLMM_OK = 0,
@@ -104,6 +104,11 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                exceeds the fair share of the step into K (block, copy) units on distinct devices
  *                (dbslmm_shard_plan).  Any n_sigma still works: with n_sigma != K a split block is
  *                solved whole on the device of its copy 0.  Ignored by single-device plans.
+ * h2f_iter       h2f_mode 0, the tiled blocks' other copies: 1 = Chebyshev (a priori coefficients
+ *                and iteration count), 2 = preconditioned CG on the same factor (Chronopoulos-Gear
+ *                form, dbslmm_cg_update): stops per block once |r| <= cheb_tol lambda_min(M_c) |x|,
+ *                capped at the Chebyshev count; 0 = the default (1).  Both within cheb_tol; the
+ *                base copy is bit-identical either way.
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -120,6 +125,7 @@ typedef struct dbslmm_options {
     int32_t sub_grid_lead;
     int32_t sub_grid_rest;
     int32_t shard_copies;
+    int32_t h2f_iter;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.

@@ -207,3 +207,68 @@ def test_whole_block_cheb_for_rest_group(factors):
             assert _finite_normwise(_cat(got), _cat(ref)) < CHEB_TOL, c
             # the lead group's small-effect betas (its blocks come first) are unchanged
             np.testing.assert_array_equal(got[0][:n_lead - 8], old[0][:n_lead - 8])
+
+
+@pytest.mark.parametrize("tiled_min", ["64", "512"])
+@pytest.mark.parametrize("factors", [(0.8, 1.0, 1.2), (1.2, 0.8), (0.5, 0.7, 1.0, 1.3, 1.6, 2.0)])
+def test_cg_copies_match_fresh_solves(tiled_min, factors):
+    """dbslmm_options.h2f_iter = 2: the tiled blocks' copies by preconditioned CG on the base factor
+    (dbslmm_cg_update after each backward pass, converged blocks skipped by the later passes).
+    Every copy against a fresh single-sigma solve at CHEB_TOL, the base copy bit for bit, statuses
+    and the monomorphic block's NaN identical; two runs bit-identical (fixed reduction order)."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=5, mono_block=3)
+    prob.opts.update(tiled_min=int(tiled_min), h2f_iter=2)
+    sig = [prob.sigma_s * f for f in factors]
+    plan = Plan(Context(0), prob)
+    multi = plan.run_multi(sig)
+    again = plan.run_multi(sig)
+    prob.opts.pop("h2f_iter")
+    fresh = _fresh(prob, sig)
+    base = int(np.argsort(sig, kind="stable")[len(sig) // 2])
+    for c, (got, ref, rep) in enumerate(zip(multi, fresh, again)):
+        np.testing.assert_array_equal(got[2], ref[2])
+        np.testing.assert_array_equal(_cat(got), _cat(rep))
+        assert got[2][3] == 3
+        if c == base:
+            np.testing.assert_array_equal(_cat(got), _cat(ref))
+        else:
+            assert _finite_normwise(_cat(got), _cat(ref)) < CHEB_TOL, c
+
+
+@pytest.mark.parametrize("cheb_tol", [1e-7, 1e-11])
+def test_cg_error_within_target(cheb_tol):
+    """CG's stopping bound |r| <= cheb_tol lambda_min(M_c) |x| bounds each block's relative error:
+    every iterated copy within cheb_tol of a fresh solve, normwise (with a 2 x margin for the fresh
+    solve's own rounding at the tight target)."""
+    from dbslmm_amd import Context, Plan
+    prob = _problem(seed=9)
+    prob.opts.update(tiled_min=64, cheb_tol=cheb_tol, h2f_iter=2)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    multi = Plan(Context(0), prob).run_multi(sig)
+    prob.opts.pop("h2f_iter")
+    for c, (got, ref) in enumerate(zip(multi, _fresh(prob, sig))):
+        assert _finite_normwise(_cat(got), _cat(ref)) <= 2 * cheb_tol, c
+
+
+@pytest.mark.parametrize("split", [-1, 1])
+def test_cg_with_lead_group(split):
+    """CG on a plan with a lead group (4500, 2600) and a rest group (800, 900, 1200, one block with a
+    monomorphic SNP), per-group substitutions (sub_split 1) or one sequence (-1): every copy
+    within CHEB_TOL of the Chebyshev run, the base copy and the statuses identical."""
+    from dbslmm_amd import Context, Plan
+    from test_tiled import LEAD_MIX
+    prob = _problem(seed=41, n_ref=512, sizes=LEAD_MIX, miss_rate=0.0, mono_block=3)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    res = {}
+    for it in (1, 2):
+        prob.opts = dict(tiled_min=256, sub_split=split, h2f_iter=it)
+        plan = Plan(Context(0), prob)
+        res[it] = plan.run_multi(sig)
+        plan.close()
+    for c, (got, ref) in enumerate(zip(res[2], res[1])):
+        np.testing.assert_array_equal(got[2], ref[2])
+        if c == 1:
+            np.testing.assert_array_equal(_cat(got), _cat(ref))
+        else:
+            assert _finite_normwise(_cat(got), _cat(ref)) < CHEB_TOL, c
