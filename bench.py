@@ -133,15 +133,17 @@ def kernel_roofline(name, ms, wl, n_solve=1):
                          "the dense FP4 peak of the instruction it issues (v_mfma_scale_f32_32x32x64_f8f6f4, "
                          "dosages as e2m1); executed = padded tiles x padded individuals")
     if name == "dbslmm_trsv":
-        # h2f Chebyshev iterations: per iteration one forward + one backward substitution, each
-        # streaming the base copy's factor once (HBM-bound; chained over 64-row tiles)
-        b = 2.0 * wl["trsv_bytes"] * wl["cheb_iters"]
+        # h2f iterations (CG by default): per iteration one forward + one backward substitution,
+        # each streaming the base copy's factor once (HBM-bound; chained over 64-row tiles); the
+        # plan counts each tiled block's own passes (a converged block's later items are skipped)
+        b = wl.get("h2f_pass_bytes") or 2.0 * wl["trsv_bytes"] * wl["cheb_iters"]
         a = b / s / 1e9 if s > 0 else 0.0
+        it = b / (2.0 * wl["trsv_bytes"]) if wl["trsv_bytes"] > 0 else 0.0
         return dict(kernel=name, bound="hbm", achieved=a, peak=PEAK_HBM_GBS, unit="GB/s",
                     frac=a / PEAK_HBM_GBS, algorithmic=b, ms=ms,
-                    note="factor bytes read by the %d forward + backward substitutions of h2f tuning "
-                         "(iterations on the base copy's factor; chain- and streaming-bound, ~5.7 us per 64-row step of the largest block)"
-                         % wl["cheb_iters"])
+                    note="factor bytes read by the h2f iterations' forward + backward substitutions on the "
+                         "base copy's factor: %.2f iterations per tiled block on average (byte-weighted; cap %d); "
+                         "chain- and streaming-bound, ~5.7 us per 64-row step of the largest block" % (it, wl["cheb_iters"]))
     if name in ("dbslmm_tchol", "dbslmm_chol_large") and wl["cheb_iters"] > 0:
         n_solve = 1     # h2f: only the base copy of the tiled and single-workgroup blocks is factored
     fl = n_solve * {"dbslmm_chol_large": wl["chol_flops_large"], "dbslmm_chol_small": wl["chol_flops_small"],
@@ -762,7 +764,10 @@ def main():
                                "fp64 epilogue",
                        "solve": "fp64 Cholesky of the joint per-block matrix" + (
                            "; h2f: tiled blocks factored once (base h2f), the other h2f solves by "
-                           "%d Chebyshev iterations on that factor" % wl["cheb_iters"]
+                           + ("%d Chebyshev iterations on that factor" % wl["cheb_iters"]
+                              if "h2f_iter=1" in [o.replace(" ", "") for o in args.opt] else
+                              "CG preconditioned by that factor, each block until |r| <= cheb_tol "
+                              "lambda_min |x| (at most %d iterations)" % wl["cheb_iters"])
                            if wl["cheb_iters"] > 0 else ""),
                        "parallelism": par},
             "roofline": roof,

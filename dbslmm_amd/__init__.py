@@ -210,7 +210,7 @@ class Plan:
         keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
                 "gram_ops_exec", "chol_flops_large", "blocks", "gram_tiles", "chol_flops_small",
                 "blocks_large", "chol_flops_tiled", "blocks_tiled", "tiled_launches", "trsv_bytes",
-                "cheb_iters", "cheb_base")
+                "cheb_iters", "cheb_base", "h2f_pass_bytes")
         return dict(zip(keys, w.tolist()))
 
     def shard_info(self) -> np.ndarray:

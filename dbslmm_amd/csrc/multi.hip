@@ -53,7 +53,8 @@ constexpr double kDragSplit = 1.06;         // a split unit's chain (its own con
 // substitution passes (each group's passes wait for its factorisation), then the result download
 constexpr double kFrontRate = 0.79, kFacRate = 1.39, kSubRate = 0.73;
 constexpr double kDownloadMsPerM = 0.95;    // per million (SNP, h2f copy) results
-constexpr int kChebIters = 7;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 (plan.hip cheb_plan)
+constexpr int kChebIters = 5;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9: CG's count on config 4's
+                                            // blocks (dbslmm_cg_update; Chebyshev's a priori count is 7)
 constexpr int kTiledMin = 384;              // plan.hip kTiledMinDefault
 
 struct Cost {
@@ -70,7 +71,7 @@ static double gram_ops(double m) {
 }
 
 // Block of m SNPs, `copies` h2f solves; direct = every copy factored (a split unit is one direct
-// copy), else one factorisation + Chebyshev iterations for the other copies
+// copy), else one factorisation + CG iterations for the other copies
 static Cost block_cost(double m, double n_ref, int copies, bool direct) {
     Cost c;
     if (m <= 0) return c;

@@ -226,6 +226,8 @@ struct dbslmm_plan {
     bool h2f_cg = false;                     // dbslmm_options.h2f_iter: the tiled blocks' copies by CG
     double* d_cgrec = nullptr;               // CG: per non-empty block and copy {gamma, alpha}
     int32_t* d_cgconv = nullptr;             // CG: per non-empty block, its copies have converged
+    int32_t* d_cgit = nullptr;               // CG: per non-empty block, iterations of the latest run
+    bool cg_ran = false;                     // the latest run_multi iterated by CG
     int32_t debug_delay_us = 0;              // dbslmm_options.debug_delay_us (tests)
     int32_t debug_stop = 0;                  // dbslmm_options.debug_stop (tests)
     int64_t n_runs = 0;                      // completed run enqueues (graphs are captured from the second)
@@ -820,7 +822,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
                     p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items,
-                    p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv};
+                    p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv, p->d_cgit};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -873,7 +875,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    op.shard_copies <= 64 && op.h2f_iter >= 0 && op.h2f_iter <= 2, "bad dbslmm_options");
     p->h2f_mode = op.h2f_mode;
     p->cheb_fused = op.cheb_fused == 1;
-    p->h2f_cg = op.h2f_iter == 2;
+    p->h2f_cg = op.h2f_iter != 1;
     p->debug_delay_us = op.debug_delay_us;
     p->debug_stop = op.debug_stop;
     if (op.cheb_tol > 0.0) p->cheb_tol = std::max(1e-16, op.cheb_tol);
@@ -1640,6 +1642,7 @@ static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
         const size_t nb = std::max(1, p->n_nonempty);
         HIP_TRY(ctx, hipMalloc(&p->d_cgrec, nb * trsv::kMaxR * 2 * sizeof(double)));
         HIP_TRY(ctx, hipMalloc(&p->d_cgconv, nb * sizeof(int32_t)));
+        HIP_TRY(ctx, hipMalloc(&p->d_cgit, nb * sizeof(int32_t)));
     }
     // the coefficients depend only on the sigmas: uploaded when they change, synchronously (the
     // host vector is a temporary of the run; an asynchronous copy from pageable memory may still
@@ -1733,7 +1736,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
         hipLaunchKernelGGL(dbslmm_cheb_init, dim3(grp.n_tb), dim3(256), 0, st, p->d_tb + grp.tb_off, p->d_row0, p->d_m,
                            p->d_ms, p->d_blk_id, p->d_y + static_cast<int64_t>(cp.base) * p->n_slots, coef,
                            nr, vs, X, R, D, S, p->d_status + cp.base * p->nbk, p->d_status, p->nbk,
-                           cix[0], cix[1], cg ? p->d_cgconv : nullptr);
+                           cix[0], cix[1], cg ? p->d_cgconv : nullptr, cg && g == 0 ? p->d_cgit : nullptr);
         HIP_TRY(ctx, hipGetLastError());
         trsv::Args a{};
         a.M = p->d_M + static_cast<int64_t>(cp.base) * p->M_elems;
@@ -1804,6 +1807,7 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
                 ca.tol = p->cheb_tol;
                 ca.rec = p->d_cgrec;
                 ca.conv = p->d_cgconv;
+                ca.iters = p->d_cgit;
                 ca.inv_sqrt_n = isn;
                 ca.beta_s = p->d_beta_s;
                 ca.beta_l = p->d_beta_l;
@@ -2189,6 +2193,8 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         for (int k : cp.iters) iters += k;
         p->wl[14] = cheb ? iters : 0;
         p->wl[15] = p->cheb_base;
+        p->cg_ran = cheb && p->h2f_cg && !p->cheb_fused;
+        p->wl[16] = cheb ? 2.0 * iters * p->wl[13] : 0.0;   // (CG: counted from d_cgit on query)
         p->cheb_pending_var = cheb && cp.base != n - 1;   // no factor of the last copy's tiled blocks
     }
     return DBSLMM_OK;
@@ -2366,6 +2372,18 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
         return DBSLMM_OK;
     }
     for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = p->wl[i];
+    if (p->cg_ran && p->d_cgit) {   // the passes each tiled block ran before it converged (run_multi is synchronous)
+        std::vector<int32_t> it(std::max(1, p->n_nonempty));
+        if (hipSetDevice(p->ctx->device) != hipSuccess ||
+            hipMemcpy(it.data(), p->d_cgit, it.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return DBSLMM_E_HIP;
+        double bytes = 0.0;
+        for (int32_t b : p->h_tb) {
+            const double T = (p->h_m[b] + trsv::kT - 1) / trsv::kT;
+            bytes += 2.0 * it[b] * T * (T + 1) / 2 * trsv::kT * trsv::kT * sizeof(double);
+        }
+        out[16] = bytes;
+    }
     return DBSLMM_OK;
 }
 

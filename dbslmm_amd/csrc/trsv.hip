@@ -489,10 +489,11 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_cheb_init(
     const int32_t* __restrict__ tb, const int32_t* __restrict__ row0, const int32_t* __restrict__ mv,
     const int32_t* __restrict__ msv, const int32_t* __restrict__ blk_id, const double* __restrict__ xbase,
     const double* __restrict__ coef0, int nr, int64_t vs, double* X, double* R, double* D, double* S,
-    const int32_t* __restrict__ st_base, int32_t* st, int64_t st_stride, int c0, int c1, int32_t* conv) {
+    const int32_t* __restrict__ st_base, int32_t* st, int64_t st_stride, int c0, int c1, int32_t* conv, int32_t* iters) {
     const int b = tb[blockIdx.x];
     const int g0 = row0[b], m = mv[b], ms = msv[b];
     if (conv && threadIdx.x == 0) conv[b] = 0;   // CG (dbslmm_cg_update): the block iterates
+    if (iters && threadIdx.x == 0) iters[b] = 0;  // CG: the run's first copy group
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         const double xb = xbase[g0 + i];
         for (int c = 0; c < nr; ++c) {
@@ -546,6 +547,7 @@ struct CGArgs {
     double tol;
     double* rec;                 // per plan block and copy: {gamma, alpha} of the previous iteration
     int32_t* conv;
+    int32_t* iters;              // per plan block: iterations run, summed over the copy groups
     double inv_sqrt_n;
     double* beta_s;
     double* beta_l;
@@ -649,7 +651,10 @@ extern "C" __global__ __launch_bounds__(trsv::kCGThreads) void dbslmm_cg_update(
             else a.beta_l[a.cix[c] * a.nl_stride - 1 - so] = bv;
         }
     }
-    if (tid == 0) a.conv[b] = 1;
+    if (tid == 0) {
+        a.conv[b] = 1;
+        a.iters[b] += a.k + 1;
+    }
 }
 
 // ---------------------------------------------------------------- whole-block Chebyshev passes

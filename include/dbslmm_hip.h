@@ -107,8 +107,9 @@ typedef struct dbslmm_plan dbslmm_plan;
  * h2f_iter       h2f_mode 0, the tiled blocks' other copies: 1 = Chebyshev (a priori coefficients
  *                and iteration count), 2 = preconditioned CG on the same factor (Chronopoulos-Gear
  *                form, dbslmm_cg_update): stops per block once |r| <= cheb_tol lambda_min(M_c) |x|,
- *                capped at the Chebyshev count; 0 = the default (1).  Both within cheb_tol; the
- *                base copy is bit-identical either way.
+ *                capped at the Chebyshev count; 0 = the default (2).  Both within cheb_tol; the
+ *                base copy is bit-identical either way.  (cheb_fused = 1 and the whole-block rest
+ *                group of sub_split = 2 iterate by Chebyshev.)
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -280,8 +281,9 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * [8] the same fp64 flops for the small blocks, [9] large blocks, [10] the same fp64 flops for
  * the tiled blocks, [11] tiled blocks, [12] launches of the tiled sequence per run, [13] bytes of
  * the factor read by one substitution launch over the tiled blocks (64-row tiles), [14] Chebyshev
- * iterations of the latest run_multi (0: none), [15] its base copy (-1: none). */
-#define DBSLMM_WORKLOAD_LEN 16
+ * iterations of the latest run_multi (0: none; with CG their cap), [15] its base copy (-1: none),
+ * [16] factor bytes its h2f passes read (CG: each tiled block's own iteration count). */
+#define DBSLMM_WORKLOAD_LEN 17
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
 
 /* Diagnostics (parity tests): after plan_sync, the working matrix of block `block` (original

@@ -39,7 +39,7 @@ def _finite_normwise(a, b):
 def test_cheb_copies_match_fresh_solves(monkeypatch, tiled_min, factors):
     from dbslmm_amd import Context, Plan
     prob = _problem(seed=5, mono_block=3)
-    prob.opts["tiled_min"] = int(tiled_min)
+    prob.opts.update(tiled_min=int(tiled_min), h2f_iter=1)   # Chebyshev (CG: test_cg_*)
     s0 = prob.sigma_s
     sig = [s0 * f for f in factors]
     plan = Plan(Context(0), prob)
@@ -117,7 +117,7 @@ def test_cheb_error_within_target(cheb_tol):
     take fewer iterations."""
     from dbslmm_amd import Context, Plan
     prob = _problem(seed=9)
-    prob.opts.update(tiled_min=64, cheb_tol=cheb_tol)
+    prob.opts.update(tiled_min=64, cheb_tol=cheb_tol, h2f_iter=1)
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     plan = Plan(Context(0), prob)
     multi = plan.run_multi(sig)
@@ -140,7 +140,7 @@ def test_fused_cheb_launch_bit_identical(monkeypatch, factors):
     the per-pass kernels' own, so the betas are bit-identical (groups of 2 and of 1 copy)."""
     from dbslmm_amd import Context, Plan
     prob = _problem(seed=5, mono_block=3)
-    prob.opts["tiled_min"] = 64
+    prob.opts.update(tiled_min=64, h2f_iter=1)   # the fused launch iterates by Chebyshev
     sig = [prob.sigma_s * f for f in factors]
     ref = Plan(Context(0), prob).run_multi(sig)
     prob.opts["cheb_fused"] = 1
@@ -223,6 +223,8 @@ def test_cg_copies_match_fresh_solves(tiled_min, factors):
     plan = Plan(Context(0), prob)
     multi = plan.run_multi(sig)
     again = plan.run_multi(sig)
+    wl = plan.workload()   # the passes the blocks ran before converging, capped by Chebyshev's count
+    assert 0 < wl["h2f_pass_bytes"] <= 2 * wl["trsv_bytes"] * wl["cheb_iters"]
     prob.opts.pop("h2f_iter")
     fresh = _fresh(prob, sig)
     base = int(np.argsort(sig, kind="stable")[len(sig) // 2])

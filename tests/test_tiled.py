@@ -345,7 +345,7 @@ def test_fused_cheb_with_lead_group_matches_unfused():
     sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
     res = {}
     for fused in (0, 1):
-        prob.opts = dict(cheb_fused=fused, sub_split=-1 if fused == 0 else 0)
+        prob.opts = dict(cheb_fused=fused, sub_split=-1 if fused == 0 else 0, h2f_iter=1)   # (fused: Chebyshev)
         plan = Plan(Context(0), prob)
         res[fused] = plan.run_multi(sig)
         plan.close()
