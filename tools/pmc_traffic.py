@@ -6,7 +6,7 @@ coalesced streaming read (MI355X_MICROARCH.md, HBM section): the read side is do
 
 Also records launches per kernel and, for the composite phases the bench times as one slot --
 the tiled Cholesky (dbslmm_tchol_* launches plus the persistent backward substitution
-dbslmm_trsv_bwd<1>) and the h2f Chebyshev substitutions (dbslmm_trsv_fwd/bwd<2>) -- the summed
+dbslmm_trsv_bwd<1>) and the h2f substitutions (dbslmm_trsv_fwd/bwd<2>) -- the summed
 HBM bytes per run (= per bench step; runs = launches of dbslmm_gram_i8, one per run -- the unpack
 is two launches per run with a lead group) under
 "dbslmm_tchol" and "dbslmm_trsv" (key "hbm_bytes_per_step").
@@ -51,7 +51,7 @@ def main(src, dst, bench_args=""):
                                               note="dbslmm_tchol_* + persistent backward, per run")
     if runs and trsv:
         out["kernels"]["dbslmm_trsv"] = dict(hbm_bytes_per_step=trsv / runs, runs=runs,
-                                             note="h2f Chebyshev substitutions, per run")
+                                             note="h2f substitutions (CG by default), per run")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
