@@ -564,8 +564,37 @@ constexpr int kChebMaxM = 512;                      // ld > 64 blocks are below 
 constexpr int kChebThreads = 512;                   // one strip row / column per thread (m <= 512)
 constexpr int kChebLdsDoubles = 5 * kChebR * kChebMaxM + kTileD + kChebR * (kChebThreads / kT) * kT;
 
+// CG instead (dbslmm_options.h2f_iter, the default; trsv.hip dbslmm_cg_update): the same passes,
+// then gamma = r.z, zeta = |P_s z|^2, the Chronopoulos-Gear scalars and the update of p (Dv),
+// q = M_c p (Sv), x, r; the block stops once every copy has |r| <= tol lambda_min(M_c) |x|
+// (lambda_min >= fs[q] = d_c + 1 - tau without large SNPs, fl = 1 - tau with), `iters` the cap.
+struct CgStop {
+    int32_t on;
+    double fs[kChebR];
+    double fl;
+    double tol;
+};
+// totals of v[0..4) over the workgroup (8 waves), fixed order: every thread gets the same values
+__device__ __forceinline__ void cg_sum4(double (&v)[4], double* red, int tid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int sft = 32; sft >= 1; sft >>= 1) v[j] += __shfl_xor(v[j], sft);
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(tid >> 6) * 4 + j] = v[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double t = 0.0;
+        for (int w = 0; w < kChebThreads / 64; ++w) t += red[w * 4 + j];
+        v[j] = t;
+    }
+    __syncthreads();
+}
+
 __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, int nr, int iters,
-                           const double* __restrict__ coef, double* lds) {
+                           const double* __restrict__ coef, double* lds, const CgStop& cgs) {
     constexpr int NT = kChebThreads, NG = NT / kT;
     const int tid = threadIdx.x;
     double* X = lds;                                 // [kChebR][kChebMaxM] each
@@ -576,6 +605,7 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
     double* Dt = V + kChebR * kChebMaxM;             // diagonal tile, stride kTS
     double* red = Dt + kTileD;                       // [kChebR][NG][32] partial sums
     const int T = (m + kT - 1) / kT;
+    double gp[kChebR] = {0.0, 0.0}, ap[kChebR] = {0.0, 0.0};   // CG: gamma, alpha of the previous iteration
     for (int k = 0; k < iters; ++k) {
         for (int e = tid; e < nr * kChebMaxM; e += NT) V[e] = R[e];
         __syncthreads();
@@ -672,6 +702,60 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
             }
             __syncthreads();
         }
+        if (cgs.on) {   // CG update (V = z = M_b^{-1} r)
+            static_assert(kChebMaxM == NT, "one element per thread and copy");
+            const int i = tid;
+            double v[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < kChebR; ++q)
+                if (q < nr && i < m) {
+                    const int e = q * kChebMaxM + i;
+                    const double z = V[e];
+                    v[2 * q] += R[e] * z;
+                    if (i < ms) v[2 * q + 1] += z * z;
+                }
+            cg_sum4(v, red, tid);
+            double al[kChebR], be[kChebR];
+#pragma unroll
+            for (int q = 0; q < kChebR; ++q) {
+                const double gam = v[2 * q], eta = gam + coef[3 * q + 2] * v[2 * q + 1];
+                be[q] = 0.0;
+                double den = eta;
+                if (k > 0) {
+                    be[q] = gp[q] > 0.0 ? gam / gp[q] : 0.0;
+                    den = eta - (ap[q] != 0.0 ? be[q] * gam / ap[q] : 0.0);
+                }
+                al[q] = den > 0.0 && gam > 0.0 ? gam / den : 0.0;
+                gp[q] = gam;
+                ap[q] = al[q];
+            }
+            double w[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < kChebR; ++q) {
+                if (q >= nr || i >= m) continue;
+                const int e = q * kChebMaxM + i;
+                const double z = V[e], r = R[e];
+                const double pv = z + be[q] * Dv[e];
+                const double qv = r + (i < ms ? coef[3 * q + 2] * z : 0.0) + be[q] * Sv[e];
+                const double x = X[e] + al[q] * pv;
+                const double rn = r - al[q] * qv;
+                Dv[e] = pv;
+                Sv[e] = qv;
+                X[e] = x;
+                R[e] = rn;
+                w[2 * q] += rn * rn;
+                w[2 * q + 1] += x * x;
+            }
+            cg_sum4(w, red, tid);
+            bool done = true;
+#pragma unroll
+            for (int q = 0; q < kChebR; ++q) {
+                const double t = cgs.tol * (ms == m ? cgs.fs[q] : cgs.fl);
+                if (q < nr) done = done && w[2 * q] <= t * t * w[2 * q + 1];   // NaN: not converged
+            }
+            if (done) break;   // uniform: every thread holds the same totals
+            continue;
+        }
         // Chebyshev update (V = M_b^{-1} r)
         const double* cf = coef + static_cast<int64_t>(k) * nr * 3;
         for (int e = tid; e < nr * kChebMaxM; e += NT) {
@@ -705,7 +789,7 @@ extern "C" __global__ __launch_bounds__(chol::kChebThreads) void dbslmm_chol_che
     const double* __restrict__ coef, int32_t nr, int32_t iters, double inv_sqrt_n,
     double* __restrict__ beta_s, double* __restrict__ beta_l, int64_t bs_stride, int64_t bl_stride,
     const int32_t* __restrict__ st_base, int32_t* __restrict__ status, int64_t st_stride,
-    int32_t c0, int32_t c1) {
+    int32_t c0, int32_t c1, chol::CgStop cgs) {
     using namespace chol;
     const int g = static_cast<int>(blockIdx.x);
     if (g >= n_blocks) return;
@@ -730,7 +814,7 @@ extern "C" __global__ __launch_bounds__(chol::kChebThreads) void dbslmm_chol_che
             Sv[e] = 0.0;
         }
         __syncthreads();
-        cheb_block(M_base + blk_matoff[b], ld, m, ms, nr, iters, coef, lds);
+        cheb_block(M_base + blk_matoff[b], ld, m, ms, nr, iters, coef, lds, cgs);
     }
     for (int e = tid; e < nr * m; e += kChebThreads) {
         const int q = e / m, i = e - q * m;

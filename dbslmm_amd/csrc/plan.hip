@@ -2086,12 +2086,17 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
             for (size_t g = 0; g < cp.iters.size(); ++g) {
                 const size_t g0 = g * chol::kChebR;
                 const int nr = static_cast<int>(std::min<size_t>(chol::kChebR, cp.others.size() - g0));
+                chol::CgStop cgs{};   // h2f by CG (the default): stopping bounds per copy
+                cgs.on = p->h2f_cg ? 1 : 0;
+                for (int j = 0; j < nr; ++j) cgs.fs[j] = cp.db + cp.coef[cp.coef_off[g] + 3 * j + 2] + 1.0 - p->tau;
+                cgs.fl = 1.0 - p->tau;
+                cgs.tol = p->cheb_tol;
                 hipLaunchKernelGGL(dbslmm_chol_cheb, dim3(p->n_large), dim3(chol::kChebThreads), kCholChebLds, s,
                                    p->d_M + bc * p->M_elems, p->d_order, p->n_large, p->d_row0, p->d_m, p->d_ms,
                                    p->d_ld, p->d_matoff, p->d_blk_id, p->d_slot_out, p->d_y + bc * p->n_slots,
                                    p->d_coef + cp.coef_off[g], nr, cp.iters[g], isn, p->d_beta_s, p->d_beta_l,
                                    p->n_s, p->n_l, p->d_status + bc * p->nbk, p->d_status,
-                                   static_cast<int64_t>(p->nbk), cp.others[g0], nr > 1 ? cp.others[g0 + 1] : 0);
+                                   static_cast<int64_t>(p->nbk), cp.others[g0], nr > 1 ? cp.others[g0 + 1] : 0, cgs);
                 HIP_TRY(ctx, hipGetLastError());
             }
         }
