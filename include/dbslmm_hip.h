@@ -104,9 +104,10 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                exceeds the fair share of the step into K (block, copy) units on distinct devices
  *                (dbslmm_shard_plan).  Any n_sigma still works: with n_sigma != K a split block is
  *                solved whole on the device of its copy 0.  Ignored by single-device plans.
- * h2f_iter       h2f_mode 0, the tiled blocks' other copies: 1 = Chebyshev (a priori coefficients
- *                and iteration count), 2 = preconditioned CG on the same factor (Chronopoulos-Gear
- *                form, dbslmm_cg_update): stops per block once |r| <= cheb_tol lambda_min(M_c) |x|,
+ * h2f_iter       h2f_mode 0, the iterated copies (tiled and single-workgroup blocks): 1 = Chebyshev
+ *                (a priori coefficients and iteration count), 2 = preconditioned CG on the same
+ *                factor (Chronopoulos-Gear form, dbslmm_cg_update / dbslmm_chol_cheb): stops per
+ *                block once |r| <= cheb_tol lambda_min(M_c) |x|,
  *                capped at the Chebyshev count; 0 = the default (2).  Both within cheb_tol; the
  *                base copy is bit-identical either way.  (cheb_fused = 1 and the whole-block rest
  *                group of sub_split = 2 iterate by Chebyshev.)
