@@ -53,8 +53,12 @@ constexpr double kDragSplit = 1.06;         // a split unit's chain (its own con
 // substitution passes (each group's passes wait for its factorisation), then the result download
 constexpr double kFrontRate = 0.79, kFacRate = 1.39, kSubRate = 0.73;
 constexpr double kDownloadMsPerM = 0.95;    // per million (SNP, h2f copy) results
-constexpr int kChebIters = 5;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9: CG's count on config 4's
-                                            // blocks (dbslmm_cg_update; Chebyshev's a priori count is 7)
+constexpr int kChebIters = 6;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 by CG (dbslmm_cg_update:
+                                            // 5.03 iterations per block byte-weighted, 6-7 for blocks with
+                                            // large SNPs; Chebyshev's a priori count is 7).  6 against the
+                                            // rates fitted before CG: the rehearsal's devices within
+                                            // 21.5-22.1 (N = 4) / 15.0-15.8 ms (N = 8) where 5 left the
+                                            // whole-block devices 1.1-1.3 ms behind (profiles/r05/cg)
 constexpr int kTiledMin = 384;              // plan.hip kTiledMinDefault
 
 struct Cost {
