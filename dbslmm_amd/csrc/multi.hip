@@ -53,7 +53,7 @@ constexpr double kDragSplit = 1.06;         // a split unit's chain (its own con
 // substitution passes (each group's passes wait for its factorisation), then the result download
 constexpr double kFrontRate = 0.79, kFacRate = 1.39, kSubRate = 0.73;
 constexpr double kDownloadMsPerM = 0.95;    // per million (SNP, h2f copy) results
-constexpr int kChebIters = 6;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 by CG (dbslmm_cg_update:
+constexpr int kH2fIters = 6;               // h2f {0.8, 1, 1.2} at cheb_tol 1e-9 by CG (dbslmm_cg_update:
                                             // 5.03 iterations per block byte-weighted, 6-7 for blocks with
                                             // large SNPs; Chebyshev's a priori count is 7).  6 against the
                                             // rates fitted before CG: the rehearsal's devices within
@@ -85,7 +85,7 @@ static Cost block_cost(double m, double n_ref, int copies, bool direct) {
     const int nfac = direct ? copies : 1;
     const double T = std::ceil(m / 64.0);
     const double pass_bytes = T * (T + 1.0) / 2.0 * 64.0 * 64.0 * 8.0;
-    const int passes = direct ? copies : 1 + (copies > 1 ? 2 * kChebIters : 0);
+    const int passes = direct ? copies : 1 + (copies > 1 ? 2 * kH2fIters : 0);
     c.front = unpack + gram;
     c.results = m * copies;
     if (m >= kTiledMin) {
