@@ -123,7 +123,22 @@ def kernel_roofline(name, ms, wl, n_solve=1):
         a = b / s / 1e9
         return dict(kernel=name, bound="hbm", achieved=a, peak=PEAK_HBM_GBS, unit="GB/s",
                     frac=a / PEAK_HBM_GBS, algorithmic=b, ms=ms)
-    if name == "dbslmm_gram_i8":
+    if name == "dbslmm_pcg":
+        # the PCG route (pcg.hip): per iteration one pass over every block's lower-triangle LD
+        # matrix (uint16 integer Gram) plus the product's partial sums (written + read once)
+        it = wl.get("pcg_iters", 0.0)
+        b = (wl.get("pcg_matrix_bytes", 0.0) + wl.get("pcg_partial_bytes", 0.0)) * it
+        a = b / s / 1e9 if s > 0 else 0.0
+        return dict(kernel=name, bound="hbm", achieved=a, peak=PEAK_HBM_GBS, unit="GB/s",
+                    frac=a / PEAK_HBM_GBS, algorithmic=b, ms=ms, iterations=it,
+                    matrix_bytes_per_iter=wl.get("pcg_matrix_bytes", 0.0),
+                    partial_bytes_per_iter=wl.get("pcg_partial_bytes", 0.0),
+                    flops_per_iter=wl.get("pcg_flops", 0.0),
+                    note="Jacobi-PCG (the reference's PCGv) on every block's joint matrix, all h2f copies "
+                         "together: per iteration the blocks' lower-triangle integer Gram (uint16) streamed "
+                         "once + the product's partial sums; ms = init to final (the rows / update "
+                         "launches included)")
+    if name == "dbslmm_gram":
         a = wl["gram_ops_alg"] / s / 1e12
         return dict(kernel=name, bound="mfma", achieved=a, peak=PEAK_FP4_TOPS, unit="TFLOP/s",
                     frac=a / PEAK_FP4_TOPS, frac_vs_i8_peak=a / PEAK_I8_TOPS,
@@ -609,7 +624,7 @@ def main():
     full = synth.make_problem(panel, lmm_only=args.lmm_only)
     for kv in args.opt:
         k, v = kv.split("=", 1)
-        full.opts[k] = float(v) if k == "cheb_tol" else int(v)
+        full.opts[k] = float(v) if k in ("cheb_tol", "pcg_tol") else int(v)
     del panel   # (the end-to-end leg generated its own copy in its child process)
     sigmas = [full.sigma_s * f for f in args.h2f] if args.h2f else None
     n_copies = len(sigmas) if sigmas else 1
@@ -762,7 +777,11 @@ def main():
                        "gram": "exact integer dosages as FP4 (e2m1, unit block scales) on "
                                "v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation exact below 2^24, "
                                "fp64 epilogue",
-                       "solve": "fp64 Cholesky of the joint per-block matrix" + (
+                       "solve": ("Jacobi-PCG (the reference's PCGv, scr/dbslmmfit.cpp:629-678) on the joint "
+                                 "per-block matrix streamed from the exact integer Gram, every h2f copy a "
+                                 "right-hand side, each block and copy until |r| <= %g lambda_min |x| "
+                                 "(%d iterations for the slowest block)" % (1e-12, wl["pcg_iters"]))
+                       if wl.get("pcg_route") else "fp64 Cholesky of the joint per-block matrix" + (
                            "; h2f: tiled blocks factored once (base h2f), the other h2f solves by "
                            + ("%d Chebyshev iterations on that factor" % wl["cheb_iters"]
                               if "h2f_iter=1" in [o.replace(" ", "") for o in args.opt] else

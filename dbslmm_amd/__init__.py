@@ -19,12 +19,12 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import (WORKLOAD_LEN, BLOCK_EMPTY, BLOCK_MONOMORPHIC, BLOCK_NOT_PD, BLOCK_OK, KERNEL_NAMES,
-                   DbslmmError)
+from ._lib import (WORKLOAD_LEN, BLOCK_EMPTY, BLOCK_MONOMORPHIC, BLOCK_NOT_CONVERGED, BLOCK_NOT_PD,
+                   BLOCK_OK, KERNEL_NAMES, SOLVER_AUTO, SOLVER_FACTOR, SOLVER_PCG, DbslmmError)
 
 __all__ = ["Context", "Plan", "DBSLMMFIT", "BlockProblem", "bed_maf", "read_snp_std", "valid_blocks",
            "DbslmmError", "BLOCK_OK", "BLOCK_EMPTY", "BLOCK_NOT_PD", "BLOCK_MONOMORPHIC",
-           "KERNEL_NAMES"]
+           "BLOCK_NOT_CONVERGED", "KERNEL_NAMES", "SOLVER_AUTO", "SOLVER_FACTOR", "SOLVER_PCG"]
 
 
 def _ptr(a):
@@ -97,7 +97,8 @@ class BlockProblem:
     z_l: np.ndarray | None = None
     tau: float = 0.8
     # dbslmm_options (path-selection thresholds; missing keys = the library defaults):
-    # tiled_min, gram_big_min, gram_huge_min, h2f_mode (0 auto / 1 merged), cheb_tol, lead_min
+    # tiled_min, gram_big_min, gram_huge_min, h2f_mode (0 auto / 1 merged), cheb_tol, lead_min,
+    # ..., solver (0 auto / 1 factorisation / 2 PCG), pcg_tol, pcg_maxit
     opts: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -210,7 +211,8 @@ class Plan:
         keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
                 "gram_ops_exec", "chol_flops_large", "blocks", "gram_tiles", "chol_flops_small",
                 "blocks_large", "chol_flops_tiled", "blocks_tiled", "tiled_launches", "trsv_bytes",
-                "cheb_iters", "cheb_base", "h2f_pass_bytes")
+                "cheb_iters", "cheb_base", "h2f_pass_bytes", "pcg_route", "pcg_iters", "pcg_matrix_bytes",
+                "pcg_partial_bytes", "pcg_flops")
         return dict(zip(keys, w.tolist()))
 
     def shard_info(self) -> np.ndarray:

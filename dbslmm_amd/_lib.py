@@ -23,12 +23,13 @@ EXPORTS = (
     "dbslmm_shard_plan", "dbslmm_plan_create_units",
 )
 
-ABI_VERSION = 11
-K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED = 0, 1, 2, 3, 4
-KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram_i8", "dbslmm_chol_large", "dbslmm_chol_small",
-                "dbslmm_tchol", "dbslmm_trsv")
-WORKLOAD_LEN = 17
-BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC = 0, 1, 2, 3
+ABI_VERSION = 12
+K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED, K_TRSV, K_PCG = 0, 1, 2, 3, 4, 5, 6
+KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram", "dbslmm_chol_large", "dbslmm_chol_small",
+                "dbslmm_tchol", "dbslmm_trsv", "dbslmm_pcg")
+WORKLOAD_LEN = 22
+BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC, BLOCK_NOT_CONVERGED = 0, 1, 2, 3, 4
+SOLVER_AUTO, SOLVER_FACTOR, SOLVER_PCG = 0, 1, 2
 
 
 class Options(C.Structure):
@@ -39,6 +40,7 @@ class Options(C.Structure):
         ("large_cheb", C.c_int32), ("cheb_fused", C.c_int32), ("debug_delay_us", C.c_int32),
         ("debug_stop", C.c_int32), ("sub_split", C.c_int32), ("sub_grid_lead", C.c_int32),
         ("sub_grid_rest", C.c_int32), ("shard_copies", C.c_int32), ("h2f_iter", C.c_int32),
+        ("solver", C.c_int32), ("pcg_tol", C.c_double), ("pcg_maxit", C.c_int32),
     ]
 
 

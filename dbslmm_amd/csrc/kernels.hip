@@ -254,7 +254,8 @@ __device__ __forceinline__ void gram_tile32(
     const uint32_t* __restrict__ Gp, int64_t kpad, int row0, int m, int ld, int64_t moff, bool missing,
     int r0, int c0, int lane, const double* __restrict__ S, const double* __restrict__ mu,
     const double* __restrict__ rsd, double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy, uint16_t* __restrict__ G16,
+    int64_t g16off, int64_t g16ld) {
     const int64_t kw = kpad / 16;                 // Gp dwords per slot (kpad: a multiple of 256)
     const uint32_t* pa = Gp + static_cast<int64_t>(row0 + r0 + (lane & 31)) * kw + 4 * (lane >> 5);
     const uint32_t* pb = Gp + static_cast<int64_t>(row0 + c0 + (lane & 31)) * kw + 4 * (lane >> 5);
@@ -294,6 +295,14 @@ __device__ __forceinline__ void gram_tile32(
     // fp64 epilogue.  C/D map of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
     const int j = lane & 31;
     const int lj = c0 + j;
+    if (G16 && !missing) {   // PCG route: the exact integer Gram (pcg.hip forms Sigma around it)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int li = r0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (li < m && lj < m) G16[g16off + li * g16ld + lj] = static_cast<uint16_t>(acc[r]);
+        }
+        return;
+    }
     const int sj = row0 + lj;
     const double Sj = lj < m ? S[sj] : 0.0;
     const double muj = lj < m ? mu[sj] : 0.0;
@@ -329,7 +338,8 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
     double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy, uint16_t* __restrict__ G16,
+    const int64_t* __restrict__ g16off, const int32_t* __restrict__ g16ld) {
     const int lane = threadIdx.x & (kWave - 1);
     const int t = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (t >= n_tiles) return;
@@ -337,7 +347,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_i8(
     const int b = tile.block;
     gram_tile32(Gp, kpad, blk_row0[b], blk_m[b], blk_ld[b], blk_matoff[b], (block_flags[b] & 1) != 0,
                 kTile * tile.ti, kTile * tile.tj, lane, S, mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride,
-                tmin, tcopy);
+                tmin, tcopy, G16, G16 ? g16off[b] : 0, G16 ? g16ld[b] : 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -367,7 +377,8 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
     const int32_t* __restrict__ block_flags,
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,
     double n_ref_d, double pad_k, double tau, double* __restrict__ M,
-    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy) {
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy, uint16_t* __restrict__ G16,
+    const int64_t* __restrict__ g16off, const int32_t* __restrict__ g16ld) {
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t glds[];
     if (static_cast<int>(blockIdx.x) >= n_tiles) return;
@@ -385,7 +396,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
             const int r0 = kGT * tile.ti + 32 * si, c0 = kGT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
             gram_tile32(Gp, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
-                        tau, M, ncopy, cstride, tmin, tcopy);
+                        tau, M, ncopy, cstride, tmin, tcopy, nullptr, 0, 0);
         }
         return;
     }
@@ -464,6 +475,22 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_gram_big(
         __syncthreads();
     }
     if (idle) return;
+    if (G16) {   // PCG route: the exact integer Gram
+        const int64_t go = g16off[b], gl = g16ld[b];
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj) {
+            const int lj = kGT * tile.tj + 64 * wc + 32 * sj + (lane & 31);
+#pragma unroll
+            for (int si = 0; si < 2; ++si)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int li = kGT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (li < m && lj < m)
+                        G16[go + li * gl + lj] = static_cast<uint16_t>(acc[si][sj][r]);
+                }
+        }
+        return;
+    }
     // fp64 epilogue (as dbslmm_gram_i8, no-missing form): C/D col = lane & 31,
     // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     const double scale = tau / n_ref_d, rn = 1.0 / n_ref_d;
@@ -623,9 +650,10 @@ __device__ __forceinline__ void gram_huge_dma_loop(const uint32_t* __restrict__ 
     const int32_t* __restrict__ block_flags,                                                       \
     const double* __restrict__ S, const double* __restrict__ mu, const double* __restrict__ rsd,   \
     double n_ref_d, double pad_k, double tau, double* __restrict__ M,                              \
-    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy
+    int32_t ncopy, int64_t cstride, int32_t tmin, int32_t tcopy, uint16_t* __restrict__ G16,          \
+    const int64_t* __restrict__ g16off, const int32_t* __restrict__ g16ld
 #define GRAM_HUGE_ARGS Gp, kpad, tiles, n_tiles, blk_row0, blk_m, blk_ld, blk_matoff, block_flags, S, \
-    mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride, tmin, tcopy
+    mu, rsd, n_ref_d, pad_k, tau, M, ncopy, cstride, tmin, tcopy, G16, g16off, g16ld
 __device__ __forceinline__ void gram_huge_body(GRAM_HUGE_PARAMS) {
     using namespace gram;
     extern __shared__ __attribute__((aligned(16))) int8_t hlds[];
@@ -645,7 +673,7 @@ __device__ __forceinline__ void gram_huge_body(GRAM_HUGE_PARAMS) {
             const int r0 = kHT * tile.ti + 32 * si, c0 = kHT * tile.tj + 32 * sj;
             if (r0 >= m || c0 >= m) continue;
             gram_tile32(Gp, kpad, row0, m, ld, moff, true, r0, c0, lane, S, mu, rsd, n_ref_d, pad_k,
-                        tau, M, ncopy, cstride, tmin, tcopy);
+                        tau, M, ncopy, cstride, tmin, tcopy, nullptr, 0, 0);
         }
         return;
     }
@@ -706,6 +734,24 @@ __device__ __forceinline__ void gram_huge_body(GRAM_HUGE_PARAMS) {
             if (act == 0xFFu) gram_huge_dma_loop<2, true>(Gp, kw, rbase, svl, nst, hlds, wave, lane, wr, wc, act, acc);
             else gram_huge_dma_loop<2, false>(Gp, kw, rbase, svl, nst, hlds, wave, lane, wr, wc, act, acc);
         }
+    }
+    if (G16) {   // PCG route: the exact integer Gram
+        if (idle) return;
+        const int64_t go = g16off[b], gl = g16ld[b];
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int li = kHT * tile.ti + 64 * wr + 32 * si + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (li >= m) continue;
+#pragma unroll
+                for (int sj = 0; sj < 4; ++sj) {
+                    const int lj = kHT * tile.tj + 128 * wc + 32 * sj + (lane & 31);
+                    if (!(act & (1u << (4 * si + sj))) || lj >= m) continue;
+                    G16[go + li * gl + lj] = static_cast<uint16_t>(acc[si][sj][r]);
+                }
+            }
+        return;
     }
     // fp64 epilogue.  The per-row (S, rsd) and per-column values of the tile go through LDS (the
     // K loop's last barrier has passed: no wave reads the stages any more), so the element loop

@@ -1,0 +1,598 @@
+// pcg.hip -- the iterative route of the per-block solve (round 6): DBSLMMFIT's own algorithm,
+// Jacobi-preconditioned CG (PCGv / PCGm, reference scr/dbslmmfit.cpp:629-678), run on the LD
+// matrix the FP4 Gram kernels (kernels.hip) build, for every block of a plan and every h2f copy at
+// once.
+//
+// What it solves.  estBlock (scr/dbslmmfit.cpp:680-770) is one solve of the joint matrix
+//     M_c = [[Sigma_ss + d_c I, Sigma_sl], [Sigma_ls, Sigma_ll]],   d_c = 1 / (sigma_c n)
+// with beta = M_c^{-1} [z_s; z_l] / sqrt(n) (the reference's PCGm /
+// Schur-complement steps are block elimination of exactly this system; LMM-only is m_l = 0).  The
+// reference iterates on A = Sigma_ss + d I with Jacobi-PCG; here one Jacobi-PCG runs on the whole
+// joint M_c (diagonal c0 + d_c on small SNPs, c0 on large ones, c0 = tau (n_ref - 1) / n_ref +
+// 1 - tau for every standardised column), which needs no Schur step and no per-large-SNP
+// right-hand side: the few large SNPs are a handful of outlying eigenvalues of the scaled matrix
+// (tools/cg_gate.py: 13 -> 17 iterations from 0 to 10 large SNPs in a block at config 4).
+//
+// Why it is cheap.  Sigma_ss >= (1 - tau) I, so lambda_min(M_c) >= 1 - tau, and >= d_c + 1 - tau
+// for a block without large SNPs; at the BASELINE configs d_c = nsnp / (h n) = 10 .. 25 and
+// lambda_max(tau X^T X / n_ref) ~ 10, so kappa ~ 1.4 - 2 and PCG reaches a relative error of 1e-12
+// in ~13 - 19 iterations (tools/cg_gate.py) -- where the factorisation costs m^3 / 3 flops on a
+// dependency chain of m columns.  Stopping rule per block and copy: |r| <= tol lambda |x| with
+// lambda the bound above, a bound on the relative 2-norm error of x that holds for any data; a
+// copy that reaches the iteration cap without it reports DBSLMM_BLOCK_NOT_CONVERGED (the
+// reference prints "Matrix is Singular!" at maxiter and returns the iterate, :664-666).
+//
+// The operator.  The Gram kernels store, for blocks without missing calls and n_ref <= 16383, the
+// INTEGER Gram G_ij = sum_k g_ik g_jk of the dosages as uint16 (lower triangle, the block's ld x ld
+// row-major layout: a quarter of the bytes of the fp64 Sigma), and the product is formed around it:
+//     Sigma u = tau / n_ref * rsd o (G (rsd o u) - S (S . (rsd o u)) / n_ref) + (1 - tau) u
+// (S = per-SNP dosage sums, rsd = 1/sd with the N-1 divisor: the Gram epilogue's centring and
+// standardisation, scr/dtpr.cpp:375-380).  Blocks with missing calls (mean imputation) or larger
+// panels read the fp64 Sigma the Gram wrote instead.  Each iteration streams the lower triangle
+// ONCE: a 128 x 128 tile (I, J) adds G_IJ v_J to rows I and G_IJ^T v_I to rows J.
+//
+// Kernels (one launch each per iteration, every block of the plan in each):
+//   dbslmm_pcg_symv    one wave per item = a run of up to kRun tiles along a tile row; per lane an
+//                      8 x 8 sub-block of each 64 x 64 quadrant, row and column sums reduce-
+//                      scattered over the lanes (fixed order); writes the row partial of the run
+//                      and each tile's column partial into per-block slots (no atomics: the sums
+//                      are deterministic, run to run and device to device).
+//   dbslmm_pcg_rows    per 128-row tile row: w = M_c u from the partial slots (fixed order),
+//                      partial dots r.u, w.u, r.r, x.x.
+//   dbslmm_pcg_update  per tile row: block sums of the dots (fixed order, the same in every
+//                      workgroup of the block), the stopping test, alpha / beta (Chronopoulos-Gear
+//                      form: one reduction phase per iteration), p, s, x, r.
+//   dbslmm_pcg_init / dbslmm_pcg_final   right-hand sides and state; beta = x / sqrt(n) in the
+//                      caller's order, status per copy.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pcg {
+constexpr int kT = 128;           // tile edge of the operator's lower triangle (slots of a block)
+constexpr int kRun = 8;           // tiles per symv item (along a tile row)
+constexpr int kMaxNC = 4;         // h2f copies per run (right-hand sides) on this route
+constexpr int kWaves = 4;         // symv items per 256-thread workgroup
+constexpr int kVS = kT + 8;       // LDS stride of a staged vector column (doubles)
+constexpr int kNDot = 5;          // per tile row and copy: r.u, w.u, r.r, x.x, S.(rsd o u)
+constexpr int kThreads = 256;
+// symv LDS per wave: the staged rsd o u of the item's tile row and of the current tile column, and
+// the reduce-scattered row / column sums ([2][copy][64] each)
+constexpr int wave_lds_doubles(int nc) { return 2 * nc * kVS + 4 * nc * 64; }
+constexpr size_t lds_bytes(int nc) { return sizeof(double) * kWaves * wave_lds_doubles(nc); }
+}  // namespace pcg
+
+// One block of the route (plan block `blk`).  Slots row0 .. row0 + m: [small | large]; the block's
+// matrix at element matoff, row stride ld (as the factor route lays it out).
+struct PcgBlk {
+    int32_t blk, row0, m, ms;
+    int32_t ld, Tb, Ns, sco;        // Tb = ceil(m / kT) tile rows, Ns partial slots per tile row
+    int64_t matoff, vo, po, dof;    // vectors (per copy Tb * kT), partials, dots
+    int64_t off16;                  // the integer Gram: Tb kT x Tb kT uint16 at off16 (rows and
+                                    // columns past m stay zero: no masks in the product)
+};
+
+struct PcgArgs {
+    const PcgBlk* blk;
+    const uint16_t* G16;            // integer Gram (u16), or null (every block on the fp64 Sigma)
+    const double* M;                // fp64 Sigma (copy 0): blocks with missing calls
+    const int32_t* flags;           // per plan block, bit 0: missing calls
+    const double* S;                // per slot: dosage sum
+    const double* rsd;              // per slot: 1 / sd (N-1)
+    const double* z;                // per slot: z-score
+    const int32_t* slot_out;        // per slot: >= 0 small beta index, -1-l large
+    const int32_t* blk_id;          // plan block -> original block id
+    const double* dshift;           // per copy: 1 / (sigma_c n)
+    double *X, *R, *P, *Sv, *W;     // state vectors, [copy][Tb * kT] per block
+    double* part;                   // symv partial slots
+    double* dot;                    // per tile row [kNDot][copy]
+    double* qs;                     // per block copy: {gamma, alpha} x 2 parities
+    int32_t* cnv;                   // per block copy: iteration + 1 at convergence (0: running)
+    int32_t* itb;                   // per block: rows launches since init
+    int32_t* done;                  // per block: 0 iterating, 1 converged, 2 monomorphic
+    int32_t* active;                // blocks still iterating
+    double* beta_s;
+    double* beta_l;
+    int32_t* status;
+    int64_t vstride;                // elements per copy-major vector array
+    int64_t ns, nl, nbk;            // beta / status strides per copy
+    double tau, rn, c0, tol, inv_sqrt_n;
+    int32_t ncopy;
+};
+
+namespace pcg {
+
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Reduce-scatter of v[0..8) over the 8 lanes that differ in lane bits (x2, x1, x0): the lane
+// whose bits read s = 4 b2 + 2 b1 + b0 returns the sum of v[s] over those lanes (fixed order).
+__device__ __forceinline__ double rscatter8(const double (&v)[8], int lane, int x2, int x1, int x0) {
+    const bool h2 = (lane & x2) != 0, h1 = (lane & x1) != 0, h0 = (lane & x0) != 0;
+    double u[4], w[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double send = h2 ? v[q] : v[q + 4], keep = h2 ? v[q + 4] : v[q];
+        u[q] = keep + __shfl_xor(send, x2);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const double send = h1 ? u[q] : u[q + 2], keep = h1 ? u[q + 2] : u[q];
+        w[q] = keep + __shfl_xor(send, x1);
+    }
+    const double send = h0 ? w[0] : w[1], keep = h0 ? w[1] : w[0];
+    return keep + __shfl_xor(send, x0);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// sum of p[s * st] over s in [s0, s1) in order, eight loads in flight (a serial chain of dependent
+// loads over a 76-slot tile row cost ~100 us per launch)
+__device__ __forceinline__ double ordered_sum(const double* __restrict__ p, int64_t st, int s0, int s1, double acc) {
+    for (int s = s0; s < s1; s += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = s + u < s1 ? p[static_cast<int64_t>(s + u) * st] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    return acc;
+}
+
+__device__ __forceinline__ bool on_u16(const PcgArgs& a, const PcgBlk& B) {
+    return a.G16 != nullptr && (a.flags[B.blk] & 1) == 0;
+}
+
+// Jacobi diagonal of M_c at block slot i (c0 + d_c on small SNPs)
+__device__ __forceinline__ double jdiag(const PcgArgs& a, const PcgBlk& B, int i, double dc) {
+    return i < B.ms ? a.c0 + dc : a.c0;
+}
+
+// uint16 -> fp64 of the low / high half of a dword.  Volatile asm: the conversions stay inside the
+// copy loop (hoisted out of it, the 64 values of a quadrant would take 128 registers and half the
+// occupancy the loads need; tools: 234 -> 119 VGPRs).
+__device__ __forceinline__ double cvt_lo(uint32_t w) {
+    double g;
+    uint32_t t;
+    asm volatile("v_and_b32 %1, 0xffff, %2\n\tv_cvt_f64_u32 %0, %1" : "=v"(g), "=&v"(t) : "v"(w));
+    return g;
+}
+__device__ __forceinline__ double cvt_hi(uint32_t w) {
+    double g;
+    uint32_t t;
+    asm volatile("v_lshrrev_b32 %1, 16, %2\n\tv_cvt_f64_u32 %0, %1" : "=v"(g), "=&v"(t) : "v"(w));
+    return g;
+}
+
+typedef uint32_t pcg_u4 __attribute__((ext_vector_type(4)));
+
+// One 64 x 64 quadrant of a tile: lane (rg = lane >> 3, cg = lane & 7) holds rows 8 rg .. + 7,
+// columns 8 cg .. + 7 as 8 x 8 uint16 (raw: four dwords per row; on a diagonal quadrant the row
+// sums take j <= i, the column sums j < i).  Per copy k: row sums (G v_J) reduce-scatter over cg
+// -> row 8 rg + cg, added to rsum[k * 64 + lane]; column sums (G^T v_I) over rg -> column
+// 8 cg + rg, added to csum[k * 64 + lane] (wave-private LDS: the copy loop stays a loop).
+__device__ __forceinline__ void quad_mul16(const pcg_u4 (&raw)[8], bool diagq, int lane, int nc,
+                                           const double* vI, const double* vJ, double* rsum, double* csum) {
+    const int rg = lane >> 3, cg = lane & 7;
+#pragma unroll 1
+    for (int k = 0; k < nc; ++k) {
+        double vi[8], vj[8], racc[8], cacc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            vi[q] = vI[k * kVS + 8 * rg + q];
+            vj[q] = vJ[k * kVS + 8 * cg + q];
+            racc[q] = cacc[q] = 0.0;
+        }
+        if (!diagq) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t w = raw[r][c >> 1];
+                    const double g = (c & 1) ? cvt_hi(w) : cvt_lo(w);
+                    racc[r] = __builtin_fma(g, vj[c], racc[r]);
+                    cacc[c] = __builtin_fma(g, vi[r], cacc[c]);
+                }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t w = raw[r][c >> 1];
+                    const double g = (c & 1) ? cvt_hi(w) : cvt_lo(w);
+                    const int dd = 8 * (cg - rg) + c - r;   // j - i
+                    racc[r] = __builtin_fma(dd <= 0 ? g : 0.0, vj[c], racc[r]);
+                    cacc[c] = __builtin_fma(dd < 0 ? g : 0.0, vi[r], cacc[c]);
+                }
+        }
+        rsum[k * 64 + lane] += rscatter8(racc, lane, 4, 2, 1);
+        csum[k * 64 + lane] += rscatter8(cacc, lane, 32, 16, 8);
+    }
+}
+
+// the same on the fp64 Sigma (blocks with missing calls, panels beyond uint16): elements read per
+// copy from global (cache hits after the first copy)
+__device__ __forceinline__ void quad_mul64(const double* __restrict__ base, int64_t ld, int rows_ok, int cols_ok,
+                                           bool diagq, int lane, int nc, const double* vI, const double* vJ,
+                                           double* rsum, double* csum) {
+    const int rg = lane >> 3, cg = lane & 7;
+#pragma unroll 1
+    for (int k = 0; k < nc; ++k) {
+        double vi[8], vj[8], racc[8], cacc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            vi[q] = vI[k * kVS + 8 * rg + q];
+            vj[q] = vJ[k * kVS + 8 * cg + q];
+            racc[q] = cacc[q] = 0.0;
+        }
+#pragma unroll 1
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const double g = (r < rows_ok && c < cols_ok) ? base[r * ld + c] : 0.0;
+                const int dd = 8 * (cg - rg) + c - r;
+                // (racc / cacc indexed by r at run time: the row loop is not unrolled here)
+                const double gr = !diagq || dd <= 0 ? g : 0.0, gc = !diagq || dd < 0 ? g : 0.0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (q == r) racc[q] = __builtin_fma(gr, vj[c], racc[q]);
+                cacc[c] = __builtin_fma(gc, vi[r], cacc[c]);
+            }
+        rsum[k * 64 + lane] += rscatter8(racc, lane, 4, 2, 1);
+        csum[k * 64 + lane] += rscatter8(cacc, lane, 32, 16, 8);
+    }
+}
+
+// the product's input of tile row T, copy k, block slot i: u = r / diag, times rsd on the u16 path
+__device__ __forceinline__ void stage_v(const PcgArgs& a, const PcgBlk& B, bool u16, int T, int nc, int lane,
+                                        double* v) {
+    for (int k = 0; k < nc; ++k) {
+        const double dc = a.dshift[k];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int rr = lane + 64 * h, i = T * kT + rr;
+            double x = 0.0;
+            if (i < B.m) {
+                x = a.R[k * a.vstride + B.vo + i] / jdiag(a, B, i, dc);
+                if (u16) x *= a.rsd[B.row0 + i];
+            }
+            v[k * kVS + rr] = x;
+        }
+    }
+}
+
+// One symv item on one wave.  LDS (wave-private): vI, vJ = rsd o u of the item's tile row and of
+// the current tile column ([copy][kVS]); rsum / csum = the reduce-scattered row results of the run
+// and column results of the current tile ([qi or qj][copy][lane]).
+template <bool U16>
+__device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, double* vJ, double* rsum,
+                          double* csum) {
+    const PcgBlk B = a.blk[item.x];
+    if (a.done[item.x] || on_u16(a, B) != U16) return;
+    const int I = item.y, J0 = item.z, J1 = item.w, nc = a.ncopy;
+    constexpr bool u16 = U16;
+    const int64_t ld16 = static_cast<int64_t>(B.Tb) * kT;
+    const int rg = lane >> 3, cg = lane & 7;
+    stage_v(a, B, u16, I, nc, lane, vI);
+    for (int q = 0; q < 2 * nc; ++q) rsum[q * 64 + lane] = 0.0;
+    for (int J = J0; J <= J1; ++J) {
+        const double* vj = vI;
+        if (J != I) {
+            wave_fence();                     // every lane is done with the previous tile's vJ
+            stage_v(a, B, u16, J, nc, lane, vJ);
+            vj = vJ;
+        }
+        for (int q = 0; q < 2 * nc; ++q) csum[q * 64 + lane] = 0.0;
+        wave_fence();
+        for (int qi = 0; qi < 2; ++qi)
+            for (int qj = 0; qj < 2; ++qj) {
+                if (J == I && qj > qi) continue;              // upper quadrant of a diagonal tile
+                const int i0 = I * kT + 64 * qi, j0 = J * kT + 64 * qj;
+                if (i0 >= B.m || j0 >= B.m) continue;         // quadrant wholly past the block
+                const bool dq = J == I && qi == qj;
+                double* rs = rsum + qi * nc * 64;
+                double* cs = csum + qj * nc * 64;
+                if constexpr (U16) {
+                    // the quadrant's 8 KB: one 16-B row segment per lane and row (zero past m)
+                    const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(i0 + 8 * rg) * ld16 + j0 + 8 * cg;
+                    pcg_u4 raw[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) raw[r] = *reinterpret_cast<const pcg_u4*>(q16 + r * ld16);
+                    quad_mul16(raw, dq, lane, nc, vI + 64 * qi, vj + 64 * qj, rs, cs);
+                } else {
+                    const int ib = i0 + 8 * rg, jb = j0 + 8 * cg;
+                    quad_mul64(a.M + B.matoff + static_cast<int64_t>(ib) * B.ld + jb, B.ld, B.m - ib, B.m - jb,
+                               dq, lane, nc, vI + 64 * qi, vj + 64 * qj, rs, cs);
+                }
+            }
+        // column partial of tile (I, J): slot I of tile row J (the diagonal tile: slot I of row I)
+        double* dst = a.part + B.po + (static_cast<int64_t>(J) * B.Ns + I) * nc * kT;
+        for (int qj = 0; qj < 2; ++qj)
+            for (int k = 0; k < nc; ++k) dst[k * kT + 64 * qj + 8 * cg + rg] = csum[(qj * nc + k) * 64 + lane];
+    }
+    // row partial of the run: slot Tb + run of tile row I
+    double* dst = a.part + B.po + (static_cast<int64_t>(I) * B.Ns + B.Tb + J0 / kRun) * nc * kT;
+    for (int qi = 0; qi < 2; ++qi)
+        for (int k = 0; k < nc; ++k) dst[k * kT + 64 * qi + 8 * rg + cg] = rsum[(qi * nc + k) * 64 + lane];
+}
+
+}  // namespace pcg
+
+// ------------------------------------------------------------------------------------------
+// Right-hand sides and state.  One workgroup per (block, 128-row tile row): x = p = s = w = 0,
+// r = z (every copy), the partial S.(rsd o u) of the first product.  Tile row 0 also resets the
+// block's counters and flags a monomorphic block (a zero-variance SNP: the reference's 0/0 column,
+// beta NaN for the whole block, status MONOMORPHIC) as done.
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_init(PcgArgs a, const int2* __restrict__ rows) {
+    using namespace pcg;
+    __shared__ double red[kThreads / 64][kMaxNC];
+    __shared__ int mono_s;
+    const int2 it = rows[blockIdx.x];
+    const int bi = it.x, I = it.y, tid = threadIdx.x;
+    const PcgBlk B = a.blk[bi];
+    const bool u16 = on_u16(a, B);
+    if (I == 0) {
+        if (tid == 0) mono_s = 0;
+        __syncthreads();
+        bool mono = false;
+        for (int i = tid; i < B.m; i += kThreads) mono |= !(a.rsd[B.row0 + i] < INFINITY);
+        if (mono) atomicOr(&mono_s, 1);
+        __syncthreads();
+        if (tid < a.ncopy) a.cnv[B.sco + tid] = 0;
+        if (tid == 0) {
+            a.itb[bi] = 0;
+            a.done[bi] = mono_s ? 2 : 0;
+            if (!mono_s) atomicAdd(a.active, 1);
+        }
+    }
+    // rows 0..127 of the tile row, two halves of the copies
+    const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
+    const bool in = i < B.m;
+    double sv[kMaxNC];
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) sv[k] = 0.0;
+    for (int k = h; k < a.ncopy; k += 2) {
+        const int64_t o = k * a.vstride + B.vo + i;
+        const double rhs = in ? a.z[B.row0 + i] : 0.0;
+        a.X[o] = 0.0;
+        a.P[o] = 0.0;
+        a.Sv[o] = 0.0;
+        a.W[o] = 0.0;
+        a.R[o] = rhs;
+        if (in && u16) sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rhs / jdiag(a, B, i, a.dshift[k]));
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) sv[k] = wave_sum(sv[k]);
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < kMaxNC; ++k) red[tid >> 6][k] = sv[k];
+    __syncthreads();
+    if (tid < a.ncopy) {
+        const int hk = tid & 1;   // the half that handled copy tid: waves 2 hk, 2 hk + 1
+        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * a.ncopy + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// The product's partial sums: one wave per item (block, tile row I, tiles J0 .. J1 <= I).
+// ------------------------------------------------------------------------------------------
+// Two kernels over the same item list, each taking the blocks of its storage (the other's items
+// return at once): the uint16 integer Gram (the common case, held to 128 registers: 4 waves per
+// SIMD keep enough row segments in flight) and the fp64 Sigma (blocks with missing calls, panels
+// with n_ref > 16383; launched only when the plan has such blocks).
+template <bool U16>
+__device__ __forceinline__ void symv_body(const PcgArgs& a, const int4* __restrict__ items, int32_t n_items) {
+    using namespace pcg;
+    extern __shared__ double vlds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int e = blockIdx.x * kWaves + wave;
+    if (e >= n_items) return;
+    const int nc = a.ncopy;
+    double* w = vlds + wave * wave_lds_doubles(nc);
+    symv_item<U16>(a, items[e], lane, w, w + nc * kVS, w + 2 * nc * kVS, w + 2 * nc * kVS + 2 * nc * 64);
+}
+#ifndef PCG_SYMV_WAVES
+#define PCG_SYMV_WAVES 3   // waves per SIMD the uint16 product is compiled for (4: 37 VGPRs spilled)
+#endif
+extern "C" __global__ __launch_bounds__(pcg::kThreads) __attribute__((amdgpu_waves_per_eu(PCG_SYMV_WAVES, 8)))
+void dbslmm_pcg_symv16(PcgArgs a, const int4* __restrict__ items, int32_t n_items) {
+    symv_body<true>(a, items, n_items);
+}
+extern "C" __global__ __launch_bounds__(pcg::kThreads)
+void dbslmm_pcg_symv64(PcgArgs a, const int4* __restrict__ items, int32_t n_items) {
+    symv_body<false>(a, items, n_items);
+}
+
+// ------------------------------------------------------------------------------------------
+// w = M_c u for one tile row from its partial slots (fixed order), and the partial dots.
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgArgs a, const int2* __restrict__ rows) {
+    using namespace pcg;
+    __shared__ double red[kThreads / 64][kMaxNC][4];
+    __shared__ double sig[kMaxNC];
+    const int2 it = rows[blockIdx.x];
+    const int bi = it.x, I = it.y, tid = threadIdx.x;
+    if (a.done[bi]) return;
+    const PcgBlk B = a.blk[bi];
+    const bool u16 = on_u16(a, B);
+    const int nc = a.ncopy;
+    if (tid < nc)                        // sigma_k = S . (rsd o u) over the block (fixed order)
+        sig[tid] = ordered_sum(a.dot + B.dof + 4 * nc + tid, kNDot * nc, 0, B.Tb, 0.0);
+    __syncthreads();
+    const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
+    const bool in = i < B.m;
+    const double Si = in ? a.S[B.row0 + i] : 0.0, ri = in ? a.rsd[B.row0 + i] : 0.0;
+    const int nrun = (I + kRun) / kRun;   // runs of tile row I: ceil((I + 1) / kRun)
+    double dv[kMaxNC][4];
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) dv[k][f] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) {
+        if (k >= nc || (k & 1) != h) continue;
+        const double* pp = a.part + B.po + static_cast<int64_t>(I) * B.Ns * nc * kT + k * kT + r;
+        double y = ordered_sum(pp, nc * kT, I, B.Tb, 0.0);
+        y = ordered_sum(pp, nc * kT, B.Tb, B.Tb + nrun, y);
+        const int64_t o = k * a.vstride + B.vo + i;
+        const double dc = a.dshift[k];
+        const double rv = a.R[o], xv = a.X[o];
+        const double u = in ? rv / jdiag(a, B, i, dc) : 0.0;
+        const double sh = i < B.ms ? dc : 0.0;
+        double w = 0.0;
+        if (in) {
+            if (u16) w = a.tau * a.rn * ri * __builtin_fma(-Si, sig[k] * a.rn, y) + (1.0 - a.tau + sh) * u;
+            else w = y + sh * u;
+        }
+        a.W[o] = w;
+        dv[k][0] = rv * u;
+        dv[k][1] = w * u;
+        dv[k][2] = rv * rv;
+        dv[k][3] = xv * xv;
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) dv[k][f] = wave_sum(dv[k][f]);
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < kMaxNC; ++k)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) red[tid >> 6][k][f] = dv[k][f];
+    __syncthreads();
+    if (tid < 4 * nc) {
+        const int k = tid >> 2, f = tid & 3, hk = k & 1;
+        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + f) * nc + k] = red[2 * hk][k][f] + red[2 * hk + 1][k][f];
+    }
+    if (I == 0 && tid == 0) a.itb[bi] += 1;
+}
+
+// ------------------------------------------------------------------------------------------
+// The iteration's coefficients and update for one tile row.  Every workgroup of a block sums the
+// block's dots in the same order, so every tile row takes the same decisions; tile row 0 alone
+// writes the recurrence state (the other parity than the one read), the convergence iteration
+// and the block's done flag.
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(PcgArgs a, const int2* __restrict__ rows) {
+    using namespace pcg;
+    __shared__ double tot[kMaxNC][4];
+    __shared__ double coef[kMaxNC][2];
+    __shared__ int run_s[kMaxNC];
+    __shared__ double red[kThreads / 64][kMaxNC];
+    const int2 it = rows[blockIdx.x];
+    const int bi = it.x, I = it.y, tid = threadIdx.x;
+    if (a.done[bi]) return;
+    const PcgBlk B = a.blk[bi];
+    const bool u16 = on_u16(a, B);
+    const int nc = a.ncopy;
+    const int itn = a.itb[bi] - 1;       // the iteration whose dots the rows launch wrote
+    if (tid < 4 * nc) {
+        const int k = tid >> 2, f = tid & 3;
+        tot[k][f] = ordered_sum(a.dot + B.dof + f * nc + k, kNDot * nc, 0, B.Tb, 0.0);
+    }
+    __syncthreads();
+    if (tid < nc) {
+        const int k = tid;
+        const double gam = tot[k][0], del = tot[k][1], rr = tot[k][2], xx = tot[k][3];
+        const double lam = B.ms == B.m ? a.dshift[k] + 1.0 - a.tau : 1.0 - a.tau;
+        const double t = a.tol * lam;
+        // converged: |r| <= tol lambda_min |x| (a bound on the relative error of x), or r = 0;
+        // NaN never converges (the cap then reports it)
+        const bool conv = a.cnv[B.sco + k] != 0 || rr == 0.0 || rr <= t * t * xx;
+        double al = 0.0, be = 0.0;
+        if (!conv) {
+            const int par = itn & 1;
+            double* q = a.qs + static_cast<int64_t>(B.sco + k) * 4;
+            if (itn == 0) {
+                al = gam / del;
+            } else {
+                be = gam / q[2 * par];
+                al = gam / (del - be * gam / q[2 * par + 1]);
+            }
+            if (I == 0) {
+                q[2 * (par ^ 1)] = gam;
+                q[2 * (par ^ 1) + 1] = al;
+            }
+        } else if (I == 0 && a.cnv[B.sco + k] == 0) {
+            a.cnv[B.sco + k] = itn + 1;
+        }
+        coef[k][0] = al;
+        coef[k][1] = be;
+        run_s[k] = conv ? 0 : 1;
+    }
+    __syncthreads();
+    int running = 0;
+    for (int k = 0; k < nc; ++k) running += run_s[k];
+    if (running == 0) {
+        if (I == 0 && tid == 0) {
+            a.done[bi] = 1;
+            atomicSub(a.active, 1);
+        }
+        return;
+    }
+    const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
+    const bool in = i < B.m;
+    double sv[kMaxNC];
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) sv[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) {
+        if (k >= nc || (k & 1) != h || !run_s[k] || !in) continue;
+        const int64_t o = k * a.vstride + B.vo + i;
+        const double al = coef[k][0], be = coef[k][1];
+        const double dg = jdiag(a, B, i, a.dshift[k]);
+        const double u = a.R[o] / dg;
+        const double p = __builtin_fma(be, a.P[o], u);
+        const double s = __builtin_fma(be, a.Sv[o], a.W[o]);
+        const double x = __builtin_fma(al, p, a.X[o]);
+        const double rn = __builtin_fma(-al, s, a.R[o]);
+        a.P[o] = p;
+        a.Sv[o] = s;
+        a.X[o] = x;
+        a.R[o] = rn;
+        if (u16) sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rn / dg);
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) sv[k] = wave_sum(sv[k]);
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < kMaxNC; ++k) red[tid >> 6][k] = sv[k];
+    __syncthreads();
+    if (tid < nc && run_s[tid]) {
+        const int hk = tid & 1;
+        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * nc + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// beta = x / sqrt(n) into the caller's order (every copy), status per copy: MONOMORPHIC (beta NaN),
+// NOT_CONVERGED (the iterate at the cap), OK.  One workgroup per tile row.
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_final(PcgArgs a, const int2* __restrict__ rows) {
+    using namespace pcg;
+    const int2 it = rows[blockIdx.x];
+    const int bi = it.x, I = it.y, tid = threadIdx.x;
+    const PcgBlk B = a.blk[bi];
+    const bool mono = a.done[bi] == 2;
+    const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
+    if (i < B.m) {
+        const int so = a.slot_out[B.row0 + i];
+        for (int k = h; k < a.ncopy; k += 2) {
+            const double bv = mono ? __builtin_nan("") : a.X[k * a.vstride + B.vo + i] * a.inv_sqrt_n;
+            if (so >= 0) a.beta_s[k * a.ns + so] = bv;
+            else a.beta_l[k * a.nl - 1 - so] = bv;
+        }
+    }
+    if (I == 0 && tid < a.ncopy) {
+        const int st = mono ? DBSLMM_BLOCK_MONOMORPHIC
+                            : a.cnv[B.sco + tid] == 0 ? DBSLMM_BLOCK_NOT_CONVERGED : DBSLMM_BLOCK_OK;
+        a.status[tid * a.nbk + a.blk_id[B.blk]] = st;
+    }
+}

@@ -39,6 +39,7 @@
 #include "chol_tiled.hip"
 #include "variance.hip"
 #include "trsv.hip"
+#include "pcg.hip"
 
 namespace {
 // events per timed run: [0] start, [1] after unpack, [2] after gram, [3] after chol_large,
@@ -256,6 +257,38 @@ struct dbslmm_plan {
     int32_t ms_runs = 0;
     bool ran = false;
     bool stopped = false;          // the last run stopped after the Gram (debug_stop = 1): no betas
+    int32_t m_copies = 0;          // block-matrix copies allocated in d_M (<= n_copies)
+    std::vector<int32_t> h_ms, h_row0;   // per non-empty block: small SNPs, first slot
+    bool has_large = false;        // some block has large SNPs
+    // ---- PCG route (dbslmm_options.solver, pcg.hip)
+    int32_t solver = 0;            // 0 auto, 1 factorisation, 2 PCG
+    double pcg_tol = 1e-12;
+    int32_t pcg_maxit = 1000;
+    bool force_factor = false;     // the variance's re-solve
+    bool pcg_g16 = false;          // n_ref <= 16383: the integer Gram fits uint16
+    int32_t pcg_m_blocks = -1;     // blocks with missing calls (fp64 Sigma products); -1 unknown
+    uint16_t* d_G16 = nullptr;     // integer Gram: per block Tb*128 x Tb*128 (zero past m)
+    int64_t* d_off16 = nullptr;    // ... its offset per block
+    int32_t* d_ld16 = nullptr;     // ... its row stride per block (Tb * 128)
+    std::vector<int64_t> h_off16;
+    int32_t pcg_n = 0;             // copies the PCG buffers are laid out for
+    PcgBlk* d_pblk = nullptr;
+    int4* d_pitem = nullptr;
+    int2* d_prow = nullptr;
+    int32_t n_pblk = 0, n_pitem = 0, n_prow = 0;
+    double *d_pvec = nullptr, *d_ppart = nullptr, *d_pdot = nullptr, *d_pqs = nullptr;
+    int32_t *d_pcnv = nullptr, *d_pitb = nullptr, *d_pdone = nullptr, *d_pact = nullptr;
+    int64_t pcg_vstride = 0;
+    int32_t* h_pmon = nullptr;     // pinned: [active | itb per block] after a chunk
+    int32_t pcg_it = 0;            // iterations enqueued by the current run
+    int32_t pcg_need = 0;          // iterations the latest finished run needed (its slowest block)
+    bool pcg_pending = false;      // a PCG run whose convergence has not been checked yet
+    bool pcg_ran = false;          // the latest run took the PCG route
+    bool pcg_pending_var = false;  // ... so the variance needs a factorisation first
+    std::vector<char> run_route;   // per pending timed run: 1 = PCG
+    double pcg_bytes = 0.0, pcg_part_bytes = 0.0, pcg_flops = 0.0;   // per iteration (workload)
+    PcgArgs pcg_args{};            // the arguments of the latest PCG run (continuation chunks)
+    hipEvent_t pcg_ev_end = nullptr;   // its timing end event (re-recorded by a continuation)
 };
 
 #define HIP_TRY(ctx, expr)                                                               \
@@ -814,6 +847,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
     }
     (void)hipSetDevice(p->ctx->device);
     if (p->h_pin) (void)hipHostFree(p->h_pin);
+    if (p->h_pmon) (void)hipHostFree(p->h_pmon);
     if (p->bed_shared) p->d_bed = nullptr;      // the context's cached image: not ours to free
     p->bed_shared.reset();
     void* bufs[] = {p->d_bed, p->d_G, p->d_slot_pos, p->d_slot_block, p->d_slot_out, p->d_z,
@@ -822,7 +856,9 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_M, p->d_beta_s, p->d_beta_l, p->d_tlist, p->d_btiles, p->d_htiles, p->d_dshift,
                     p->d_tlist_multi, p->d_tri_f, p->d_tri_b, p->d_foff, p->d_tflags, p->d_tb,
                     p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items,
-                    p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv, p->d_cgit};
+                    p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv, p->d_cgit, p->d_G16, p->d_pblk,
+                    p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
+                    p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -872,7 +908,12 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    op.debug_delay_us >= -100000 && op.debug_delay_us <= 100000 &&
                    (op.debug_stop == 0 || op.debug_stop == 1) && op.sub_split >= -1 && op.sub_split <= 2 &&
                    op.sub_grid_lead >= 0 && op.sub_grid_rest >= 0 && op.shard_copies >= 0 &&
-                   op.shard_copies <= 64 && op.h2f_iter >= 0 && op.h2f_iter <= 2, "bad dbslmm_options");
+                   op.shard_copies <= 64 && op.h2f_iter >= 0 && op.h2f_iter <= 2 && op.solver >= 0 &&
+                   op.solver <= 2 && op.pcg_tol >= 0.0 && op.pcg_maxit >= 0, "bad dbslmm_options");
+    p->solver = op.solver;
+    if (op.pcg_tol > 0.0) p->pcg_tol = std::max(1e-15, op.pcg_tol);
+    if (op.pcg_maxit > 0) p->pcg_maxit = op.pcg_maxit;
+    p->pcg_g16 = 4 * static_cast<int64_t>(pr->n_ref) <= 65535;
     p->h2f_mode = op.h2f_mode;
     p->cheb_fused = op.cheb_fused == 1;
     p->h2f_cg = op.h2f_iter != 1;
@@ -1026,6 +1067,9 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
     }
     p->n_nonempty = static_cast<int32_t>(row0.size());
     p->n_slots = static_cast<int32_t>(slot_pos.size());
+    p->h_ms = msv;
+    p->h_row0 = row0;
+    for (size_t b = 0; b < mv.size(); ++b) p->has_large = p->has_large || mv[b] > msv[b];
     p->h_slot_out = slot_out;
     p->n_tiles = static_cast<int32_t>(tiles.size());
     std::vector<GramTile> btiles;
@@ -1313,7 +1357,11 @@ static int collect_timing(dbslmm_plan* p) {
         float t[kEvPerRun] = {0.f};
         for (int k = 1; k < kEvPerRun; ++k) HIP_TRY(ctx, hipEventElapsedTime(&t[k], e[0], e[k]));
         const float fend = std::max(t[8], t[11]), cstart = std::min(t[8], t[11]);
-        const float span[DBSLMM_K_COUNT] = {t[1], t[2] - t[1], t[3] - t[2], t[5] - t[4], fend - t[6], t[7] - cstart};
+        float span[DBSLMM_K_COUNT] = {t[1], t[2] - t[1], t[3] - t[2], t[5] - t[4], fend - t[6], t[7] - cstart, 0.f};
+        if (r < static_cast<int>(p->run_route.size()) && p->run_route[r]) {   // PCG: unpack, Gram, iterations
+            for (int k = 2; k < DBSLMM_K_COUNT; ++k) span[k] = 0.f;
+            span[DBSLMM_K_PCG] = t[7] - t[2];
+        }
         for (int k = 0; k < DBSLMM_K_COUNT; ++k) p->ms_acc[k] += span[k];
         // the lead group's Gram (9 -> 10) sits between the two unpack launches (0 -> 1)
         float lg = 0.f;
@@ -1323,6 +1371,7 @@ static int collect_timing(dbslmm_plan* p) {
         p->ms_runs++;
     }
     p->runs_pending = 0;
+    p->run_route.clear();
     return DBSLMM_OK;
 }
 
@@ -1384,10 +1433,14 @@ static int enqueue_tiled(dbslmm_plan* p, double isn, const std::vector<TLaunch>&
     return DBSLMM_OK;
 }
 
-// Grow the per-copy buffers to n factorisation copies (contents are rebuilt by the next run).
-static int ensure_copies(dbslmm_plan* p, int n) {
+// Grow the per-copy buffers to n solve copies (betas, status, sigma scalars, scratch) and mc
+// block-matrix copies (the factorisation route factors mc = n copies of the Gram; the PCG route
+// reads one Sigma, copy 0).  Contents are rebuilt by the next run.
+static int ensure_copies(dbslmm_plan* p, int n, int mc) {
     dbslmm_ctx* ctx = p->ctx;
-    if (n <= p->n_copies) return DBSLMM_OK;
+    if (n <= p->n_copies && mc <= p->m_copies) return DBSLMM_OK;
+    n = std::max(n, p->n_copies);
+    mc = std::max(mc, p->m_copies);
     std::lock_guard<std::mutex> lk(g_capture_mu);   // device-wide sync + synchronous memset
     HIP_TRY(ctx, hipDeviceSynchronize());
     void* old[] = {p->d_M, p->d_dshift, p->d_y, p->d_beta_s, p->d_beta_l, p->d_status};
@@ -1395,9 +1448,10 @@ static int ensure_copies(dbslmm_plan* p, int n) {
         if (q) (void)hipFree(q);
     p->d_M = p->d_dshift = p->d_y = p->d_beta_s = p->d_beta_l = nullptr;
     p->d_status = nullptr;
-    const size_t nn = static_cast<size_t>(n);
-    HIP_TRY(ctx, hipMalloc(&p->d_M, std::max<size_t>(1, nn * p->M_elems) * sizeof(double)));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_M, 0, std::max<size_t>(1, nn * p->M_elems) * sizeof(double), ctx->stream));
+    const size_t nn = static_cast<size_t>(n), nm = static_cast<size_t>(mc);
+    // (+ 256 elements: the PCG product's masked row segments may run past the last block's rows)
+    HIP_TRY(ctx, hipMalloc(&p->d_M, (std::max<size_t>(1, nm * p->M_elems) + 256) * sizeof(double)));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_M, 0, (std::max<size_t>(1, nm * p->M_elems) + 256) * sizeof(double), ctx->stream));
     HIP_TRY(ctx, hipMalloc(&p->d_dshift, nn * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_y, nn * std::max<int64_t>(1, p->n_slots) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_beta_s, nn * std::max<int64_t>(1, p->n_s) * sizeof(double)));
@@ -1405,6 +1459,7 @@ static int ensure_copies(dbslmm_plan* p, int n) {
     HIP_TRY(ctx, hipMalloc(&p->d_status, nn * p->nbk * sizeof(int32_t)));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     p->n_copies = n;
+    p->m_copies = mc;
     // captured graphs hold the old pointers
     if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
     if (p->graph_multi) (void)hipGraphExecDestroy(p->graph_multi);
@@ -1901,13 +1956,288 @@ static int run_tcheb(dbslmm_plan* p, double isn, const ChebPlan& cp, hipStream_t
     return DBSLMM_OK;
 }
 
+// ---------------------------------------------------------------- PCG route (pcg.hip)
+// Does this run take the PCG route?  solver 2 forces it and 0 (auto) picks it when every copy's
+// prior shift d_c = 1/(sigma_c n) keeps the system well conditioned (d_c >= kPcgDmin: kappa <=
+// 1 + lambda_LD / (d + 1 - tau) ~ 6 at lambda_LD ~ 10, tools/cg_gate.py); both need a data-free
+// lower bound on lambda_min (tau < 1, or no large SNPs: then d_c + 1 - tau), at most
+// pcg::kMaxNC copies and no debug stop after the Gram.
+constexpr double kPcgDmin = 2.0;
+static bool pcg_route(const dbslmm_plan* p, const double* sigmas, int n) {
+    if (p->force_factor || p->solver == 1 || p->n_nonempty == 0 || p->debug_stop) return false;
+    if (n > pcg::kMaxNC || !(p->tau > 0.0 && p->tau <= 1.0) || (p->tau >= 1.0 && p->has_large)) return false;
+    if (p->solver == 2) return true;
+    for (int c = 0; c < n; ++c)
+        if (1.0 / (sigmas[c] * static_cast<double>(p->n_obs)) < kPcgDmin) return false;
+    return true;
+}
+
+// Lay the PCG buffers out for n copies: per block its tile rows (128 slots), the product's work
+// items (runs of kRun tiles along a tile row, biggest blocks first), vectors [5][copy][slots],
+// partial slots, dots and the recurrence state.
+static int pcg_layout(dbslmm_plan* p, int n) {
+    dbslmm_ctx* ctx = p->ctx;
+    if (p->pcg_g16 && !p->d_G16) {
+        // the integer Gram: block b at off16, Tb 128 x Tb 128, zero past m (set once: the Gram
+        // writes only rows and columns < m), so the product reads whole 16-B row segments unmasked
+        std::vector<int64_t> off;
+        std::vector<int32_t> ldv;
+        int64_t o = 0;
+        for (int b = 0; b < p->n_nonempty; ++b) {
+            const int64_t l = (p->h_m[b] + pcg::kT - 1) / pcg::kT * pcg::kT;
+            off.push_back(o);
+            ldv.push_back(static_cast<int32_t>(l));
+            o += l * l;
+        }
+        const size_t e = static_cast<size_t>(o) + 256;
+        HIP_TRY(ctx, hipMalloc(&p->d_G16, e * sizeof(uint16_t)));
+        HIP_TRY(ctx, hipMemsetAsync(p->d_G16, 0, e * sizeof(uint16_t), ctx->stream));
+        HIP_TRY(ctx, dev_upload(&p->d_off16, off, ctx->stream));
+        HIP_TRY(ctx, dev_upload(&p->d_ld16, ldv, ctx->stream));
+        p->h_off16 = off;
+    }
+    if (!p->h_pmon) HIP_TRY(ctx, hipHostMalloc(&p->h_pmon, (1 + std::max(1, p->n_nonempty)) * sizeof(int32_t),
+                                               hipHostMallocDefault));
+    if (p->pcg_n == n) return DBSLMM_OK;
+    void* old[] = {p->d_pblk, p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
+                   p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16};
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (void* q : old)
+        if (q) (void)hipFree(q);
+    using namespace pcg;
+    std::vector<PcgBlk> blk;
+    std::vector<int4> items;
+    std::vector<int2> rows;
+    int64_t vo = 0, po = 0, dof = 0;
+    int32_t sco = 0;
+    double bytes = 0.0, pbytes = 0.0, flops = 0.0;
+    const double esz = p->pcg_g16 ? 2.0 : 8.0;
+    for (int b = 0; b < p->n_nonempty; ++b) {
+        const int32_t m = p->h_m[b], Tb = (m + kT - 1) / kT, nrun = (Tb + kRun - 1) / kRun;
+        PcgBlk k{b, p->h_row0[b], m, p->h_ms[b], p->h_ld[b], Tb, Tb + nrun, sco, p->h_matoff[b], vo, po, dof,
+                 p->h_off16.empty() ? 0 : p->h_off16[b]};
+        const int bi = static_cast<int>(blk.size());
+        blk.push_back(k);
+        vo += static_cast<int64_t>(Tb) * kT;
+        po += static_cast<int64_t>(Tb) * k.Ns * n * kT;
+        dof += static_cast<int64_t>(Tb) * kNDot * n;
+        sco += n;
+        for (int I = 0; I < Tb; ++I) {
+            rows.push_back(int2{bi, I});
+            for (int J0 = 0; J0 <= I; J0 += kRun) items.push_back(int4{bi, I, J0, std::min(I, J0 + kRun - 1)});
+        }
+        bytes += 0.5 * m * (m + 1.0) * esz;
+        flops += 4.0 * n * 0.5 * m * (m + 1.0);
+        // partials written and read once: a column slot per tile (I, J <= I), a row slot per run
+        pbytes += 2.0 * 8.0 * n * kT * (0.5 * Tb * (Tb + 1.0) + Tb * 0.5 * (nrun + 1.0));
+    }
+    // biggest blocks' items first (their tile rows are the longest runs of work)
+    std::stable_sort(items.begin(), items.end(), [&](const int4& x, const int4& y) { return blk[x.x].Tb > blk[y.x].Tb; });
+    p->n_pblk = static_cast<int32_t>(blk.size());
+    p->n_pitem = static_cast<int32_t>(items.size());
+    p->n_prow = static_cast<int32_t>(rows.size());
+    p->pcg_vstride = vo;
+    p->pcg_bytes = bytes;
+    p->pcg_part_bytes = pbytes;
+    p->pcg_flops = flops;
+    HIP_TRY(ctx, dev_upload(&p->d_pblk, blk, ctx->stream));
+    HIP_TRY(ctx, dev_upload(&p->d_pitem, items, ctx->stream));
+    HIP_TRY(ctx, dev_upload(&p->d_prow, rows, ctx->stream));
+    HIP_TRY(ctx, hipMalloc(&p->d_pvec, std::max<int64_t>(1, 5 * n * vo) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_ppart, std::max<int64_t>(1, po) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pdot, std::max<int64_t>(1, dof) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pqs, std::max<int32_t>(1, sco) * 4 * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pcnv, std::max<int32_t>(1, sco) * sizeof(int32_t)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pitb, std::max<int32_t>(1, p->n_pblk) * sizeof(int32_t)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pdone, std::max<int32_t>(1, p->n_pblk) * sizeof(int32_t)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pact, sizeof(int32_t)));
+    p->pcg_n = n;
+    return DBSLMM_OK;
+}
+
+// Iterations the first chunk of a run enqueues: the previous run's count (same data), else the
+// Chebyshev bound of the well-conditioned case, kappa = 1 + 12 / (d_min + 1 - tau), + 2, + 4 when
+// large SNPs add outlying eigenvalues (tools/cg_gate.py: +4 at 10 large SNPs in a block).
+static int pcg_first_chunk(const dbslmm_plan* p, const double* sigmas, int n) {
+    if (p->pcg_need > 0) return std::min(p->pcg_need, p->pcg_maxit);
+    double dmin = INFINITY;
+    for (int c = 0; c < n; ++c) dmin = std::min(dmin, 1.0 / (sigmas[c] * static_cast<double>(p->n_obs)));
+    const double kap = 1.0 + 12.0 / std::max(1e-3, dmin + 1.0 - p->tau);
+    const double q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
+    const int k = static_cast<int>(std::ceil(std::log(2.0 / p->pcg_tol) / -std::log(q))) + 2 + (p->has_large ? 4 : 0);
+    return std::clamp(k, 1, p->pcg_maxit);
+}
+
+// K iterations (product, rows, update) and the tail (betas, status, convergence read-back).
+static int pcg_iters(dbslmm_plan* p, int K) {
+    dbslmm_ctx* ctx = p->ctx;
+    hipStream_t s = ctx->stream;
+    for (int k = 0; k < K; ++k) {
+        const dim3 g((p->n_pitem + pcg::kWaves - 1) / pcg::kWaves);
+        if (p->pcg_g16)
+            hipLaunchKernelGGL(dbslmm_pcg_symv16, g, dim3(pcg::kThreads), pcg::lds_bytes(p->pcg_n), s, p->pcg_args,
+                               p->d_pitem, p->n_pitem);
+        if (!p->pcg_g16 || p->pcg_m_blocks != 0)   // (-1: not known yet)
+            hipLaunchKernelGGL(dbslmm_pcg_symv64, g, dim3(pcg::kThreads), pcg::lds_bytes(p->pcg_n), s, p->pcg_args,
+                               p->d_pitem, p->n_pitem);
+        hipLaunchKernelGGL(dbslmm_pcg_rows, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
+        hipLaunchKernelGGL(dbslmm_pcg_update, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    p->pcg_it += K;
+    hipLaunchKernelGGL(dbslmm_pcg_final, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(p->h_pmon, p->d_pact, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipMemcpyAsync(p->h_pmon + 1, p->d_pitb, p->n_pblk * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (p->pcg_ev_end) HIP_TRY(ctx, hipEventRecord(p->pcg_ev_end, s));
+    return DBSLMM_OK;
+}
+
+// Wait for a PCG run; while blocks still iterate (and the cap allows), enqueue further chunks.
+static int pcg_finish(dbslmm_plan* p) {
+    dbslmm_ctx* ctx = p->ctx;
+    while (p->pcg_pending) {
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        int32_t need = 0;
+        for (int b = 0; b < p->n_pblk; ++b) need = std::max(need, p->h_pmon[1 + b]);
+        if (p->h_pmon[0] <= 0 || p->pcg_it >= p->pcg_maxit) {
+            p->pcg_pending = false;
+            p->pcg_need = p->h_pmon[0] <= 0 ? need : p->pcg_maxit;
+            if (p->pcg_m_blocks < 0) {   // missing-call flags are data: read once, after the first run
+                std::vector<int32_t> fl(std::max(1, p->n_nonempty));
+                HIP_TRY(ctx, hipMemcpy(fl.data(), p->d_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+                p->pcg_m_blocks = 0;
+                for (int b = 0; b < p->n_nonempty; ++b) p->pcg_m_blocks += fl[b] & 1;
+            }
+            break;
+        }
+        const int K = std::min(std::max(4, p->pcg_it / 4), p->pcg_maxit - p->pcg_it);
+        if (const int rc = pcg_iters(p, K)) return rc;
+    }
+    return DBSLMM_OK;
+}
+
+// One run on the PCG route: unpack + Gram (the integer Gram as uint16 where it fits, Sigma in fp64
+// for the other blocks), then the iterations of every block and copy together.
+static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
+    dbslmm_ctx* ctx = p->ctx;
+    if (const int rc = ensure_copies(p, n, 1)) return rc;
+    if (const int rc = pcg_layout(p, n)) return rc;
+    hipStream_t s = ctx->stream;
+    hipEvent_t* ev = nullptr;
+    if (p->timing) {
+        const size_t need = kEvPerRun * static_cast<size_t>(p->runs_pending + 1);
+        while (p->ev.size() < need) {
+            hipEvent_t e;
+            HIP_TRY(ctx, hipEventCreate(&e));
+            p->ev.push_back(e);
+        }
+        ev = &p->ev[kEvPerRun * p->runs_pending];
+        p->runs_pending++;
+        p->run_route.resize(p->runs_pending);
+        p->run_route.back() = 1;
+    }
+    p->pcg_ev_end = ev ? ev[7] : nullptr;
+    p->trsv_failed = false;
+    p->stopped = false;
+    const size_t nbk = static_cast<size_t>(p->nbk);
+    HIP_TRY(ctx, hipMemsetAsync(p->d_flags, 0, nbk * sizeof(int32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_status, 0, n * nbk * sizeof(int32_t), s));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_pact, 0, sizeof(int32_t), s));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], s));
+    for (int c = 0; c < n; ++c)
+        hipLaunchKernelGGL(dbslmm_set_scalar, dim3(1), dim3(1), 0, s, p->d_dshift + c,
+                           1.0 / (sigmas[c] * static_cast<double>(p->n_obs)));
+    if (p->n_slots > 0)
+        hipLaunchKernelGGL(dbslmm_unpack_stats, dim3((p->n_slots + 3) / 4), dim3(256), 0, s, p->d_bed, p->n_ref,
+                           p->bytes_per_snp, p->d_slot_pos, p->d_slot_block, p->n_slots, p->d_G, p->kpad, p->d_S,
+                           p->d_mu, p->d_rsd, p->d_flags, nullptr);
+    HIP_TRY(ctx, hipGetLastError());
+    if (ev) for (int k : {1, 9, 10}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
+    uint16_t* g16 = p->pcg_g16 ? p->d_G16 : nullptr;
+    const double nrd = static_cast<double>(p->n_ref), padk = static_cast<double>(p->kpad - p->n_ref);
+    if (p->n_htiles > 0)
+        hipLaunchKernelGGL(dbslmm_gram_huge, dim3(p->n_htiles), dim3(512), gram::kHLdsBytes, s, p->d_G, p->kpad,
+                           p->d_htiles, p->n_htiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
+                           p->d_mu, p->d_rsd, nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
+    if (p->n_tiles > 0)
+        hipLaunchKernelGGL(dbslmm_gram_i8, dim3((p->n_tiles + 3) / 4), dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
+                           p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
+                           nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
+    if (p->n_btiles > 0)
+        hipLaunchKernelGGL(dbslmm_gram_big, dim3(p->n_btiles), dim3(256), gram::kLdsBytes, s, p->d_G, p->kpad,
+                           p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
+                           p->d_mu, p->d_rsd, nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
+    HIP_TRY(ctx, hipGetLastError());
+    if (ev) for (int k : {2, 3, 4, 5, 6, 8, 11}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
+    PcgArgs a{};
+    a.blk = p->d_pblk;
+    a.G16 = g16;
+    a.M = p->d_M;
+    a.flags = p->d_flags;
+    a.S = p->d_S;
+    a.rsd = p->d_rsd;
+    a.z = p->d_z;
+    a.slot_out = p->d_slot_out;
+    a.blk_id = p->d_blk_id;
+    a.dshift = p->d_dshift;
+    const int64_t vs = static_cast<int64_t>(n) * p->pcg_vstride;
+    a.X = p->d_pvec;
+    a.R = a.X + vs;
+    a.P = a.R + vs;
+    a.Sv = a.P + vs;
+    a.W = a.Sv + vs;
+    a.part = p->d_ppart;
+    a.dot = p->d_pdot;
+    a.qs = p->d_pqs;
+    a.cnv = p->d_pcnv;
+    a.itb = p->d_pitb;
+    a.done = p->d_pdone;
+    a.active = p->d_pact;
+    a.beta_s = p->d_beta_s;
+    a.beta_l = p->d_beta_l;
+    a.status = p->d_status;
+    a.vstride = p->pcg_vstride;
+    a.ns = p->n_s;
+    a.nl = p->n_l;
+    a.nbk = p->nbk;
+    a.tau = p->tau;
+    a.rn = 1.0 / nrd;
+    a.c0 = p->tau * (nrd - 1.0) / nrd + 1.0 - p->tau;
+    a.tol = p->pcg_tol;
+    a.inv_sqrt_n = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
+    a.ncopy = n;
+    p->pcg_args = a;
+    hipLaunchKernelGGL(dbslmm_pcg_init, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, a, p->d_prow);
+    HIP_TRY(ctx, hipGetLastError());
+    p->pcg_it = 0;
+    p->pcg_pending = true;
+    if (const int rc = pcg_iters(p, pcg_first_chunk(p, sigmas, n))) return rc;
+    p->ran = true;
+    p->n_runs++;
+    p->sigma_run = sigmas[n - 1];
+    p->var_copy = n - 1;
+    p->pcg_ran = true;
+    p->pcg_pending_var = true;
+    p->cheb_base = -1;
+    p->cg_ran = false;
+    p->cheb_pending_var = false;
+    p->wl[14] = 0;
+    p->wl[15] = -1;
+    p->wl[16] = 0;
+    return DBSLMM_OK;
+}
+
 // One run: unpack + Gram (front; else the Gram of the previous front run is reused), then n
 // factorisations + solves of it, copy c with sigma_s = sigmas[c] (n > 1: h2f tuning; copies
 // 1.. are device copies of the Gram, all factored by one merged tiled sequence).
 static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
     dbslmm_ctx* ctx = p->ctx;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (const int rc = ensure_copies(p, n)) return rc;
+    if (const int rc = pcg_finish(p)) return rc;   // a PCG run still pending (plan_run without sync)
+    if (front && pcg_route(p, sigmas, n)) return run_pcg(p, sigmas, n);
+    if (const int rc = ensure_copies(p, n, n)) return rc;
     if (n > 1) {
         if (p->multi_n != n) {
             std::lock_guard<std::mutex> lk(g_capture_mu);   // synchronous upload below
@@ -1942,7 +2272,11 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
         }
         ev = &p->ev[kEvPerRun * p->runs_pending];
         p->runs_pending++;
+        p->run_route.resize(p->runs_pending);
+        p->run_route.back() = 0;
     }
+    p->pcg_ran = false;
+    p->pcg_pending_var = false;
     const size_t nbk = static_cast<size_t>(p->nbk);
     // Substitution tile flags are epochs (trsv.hip): a run takes at most kEpochsPerRun of them
     // (backward solves and Chebyshev passes of every group and copy).  When the counter could wrap
@@ -1998,7 +2332,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_htiles + t0, nt, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems, tmin_copy, tcopy);
+                           p->tau, p->d_M, n, p->M_elems, tmin_copy, tcopy, nullptr, nullptr, nullptr);
     };
     if (front && p->n_htiles_lead > 0) {
         gram_huge(0, p->n_htiles_lead);
@@ -2034,7 +2368,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, static_cast<double>(p->n_ref),
                            static_cast<double>(p->kpad - p->n_ref), p->tau, p->d_M, n, p->M_elems,
-                           tmin_copy, tcopy);
+                           tmin_copy, tcopy, nullptr, nullptr, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     if (front && p->n_htiles > p->n_htiles_tiled) {
@@ -2046,7 +2380,7 @@ static int run_impl(dbslmm_plan* p, bool front, const double* sigmas, int n) {
                            p->kpad, p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld,
                            p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
                            static_cast<double>(p->n_ref), static_cast<double>(p->kpad - p->n_ref),
-                           p->tau, p->d_M, n, p->M_elems, tmin_copy, tcopy);
+                           p->tau, p->d_M, n, p->M_elems, tmin_copy, tcopy, nullptr, nullptr, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     // (the factorisation overwrites its matrix: the Gram epilogues write all n copies)
@@ -2236,6 +2570,7 @@ static int download_copies(dbslmm_plan* p, int c0, int n, double* beta_s, double
     if (!p->ran) { ctx->err = "plan_download before plan_run"; return DBSLMM_E_STATE; }
     if (p->stopped) { ctx->err = "plan_download after a run stopped at the Gram (debug_stop)"; return DBSLMM_E_STATE; }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (const int rc = pcg_finish(p)) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (const int rc = check_trsv(p)) return rc;
     const size_t nbs = beta_s ? static_cast<size_t>(n) * p->n_s : 0;
@@ -2322,10 +2657,12 @@ int dbslmm_plan_sync(dbslmm_plan* p) {
     if (!p) return DBSLMM_E_ARG;
     if (p->mp) return mp_sync(p);
     HIP_TRY(p->ctx, hipSetDevice(p->ctx->device));
+    if (const int rc = pcg_finish(p)) return rc;
     HIP_TRY(p->ctx, hipStreamSynchronize(p->ctx->stream));
     if (const int rc = check_trsv(p)) return rc;
     if (p->timing) return collect_timing(p);
     p->runs_pending = 0;
+    p->run_route.clear();
     return DBSLMM_OK;
 }
 
@@ -2368,7 +2705,7 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
             double w[DBSLMM_WORKLOAD_LEN];
             dbslmm_plan_workload(sh.plan, w);
             for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i)
-                out[i] = (i == 12 || i == 14) ? std::max(out[i], w[i])
+                out[i] = (i == 12 || i == 14 || i == 17 || i == 18) ? std::max(out[i], w[i])
                          : ((i == 0 || i == 6) && sh.copy > 0) ? out[i] : out[i] + w[i];
         }
         double w0[DBSLMM_WORKLOAD_LEN];
@@ -2377,6 +2714,11 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
         return DBSLMM_OK;
     }
     for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = p->wl[i];
+    out[17] = p->pcg_ran ? 1.0 : 0.0;
+    out[18] = p->pcg_ran ? p->pcg_need : 0.0;
+    out[19] = p->pcg_ran ? p->pcg_bytes : 0.0;
+    out[20] = p->pcg_ran ? p->pcg_part_bytes : 0.0;
+    out[21] = p->pcg_ran ? p->pcg_flops : 0.0;
     if (p->cg_ran && p->d_cgit) {   // the passes each tiled block ran before it converged (run_multi is synchronous)
         std::vector<int32_t> it(std::max(1, p->n_nonempty));
         if (hipSetDevice(p->ctx->device) != hipSuccess ||
@@ -2406,7 +2748,7 @@ int dbslmm_plan_block_matrix(dbslmm_plan* p, int32_t block, int32_t copy, double
                 }
         ARG_CHECK(ctx, false, "block has no SNPs");
     }
-    ARG_CHECK(ctx, copy >= 0 && copy < p->n_copies, "copy out of range");
+    ARG_CHECK(ctx, copy >= 0 && copy < p->m_copies, "copy out of range");
     const auto it = std::find(p->h_blk_id.begin(), p->h_blk_id.end(), block);
     ARG_CHECK(ctx, it != p->h_blk_id.end(), "block has no SNPs");
     const size_t nb = static_cast<size_t>(it - p->h_blk_id.begin());
@@ -2414,6 +2756,7 @@ int dbslmm_plan_block_matrix(dbslmm_plan* p, int32_t block, int32_t copy, double
     if (ld_out) *ld_out = static_cast<int32_t>(ld);
     if (!out) return DBSLMM_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (const int rc = pcg_finish(p)) return rc;
     std::lock_guard<std::mutex> lk(g_capture_mu);   // device-wide sync + synchronous copy
     HIP_TRY(ctx, hipDeviceSynchronize());
     HIP_TRY(ctx, hipMemcpy(out, p->d_M + static_cast<int64_t>(copy) * p->M_elems + p->h_matoff[nb],
@@ -2448,10 +2791,15 @@ int dbslmm_est(dbslmm_ctx* ctx, const dbslmm_problem* pr, double* beta_s, double
 // A multi-device plan does this for every shard (and waits) before any shard's variance starts,
 // so no shard captures a graph while another runs the variance's synchronous calls.
 static int variance_factor(dbslmm_plan* p) {
-    if (!p->cheb_pending_var) return DBSLMM_OK;
+    if (const int rc = pcg_finish(p)) return rc;
+    if (!p->cheb_pending_var && !p->pcg_pending_var) return DBSLMM_OK;
     const double sg = p->sigma_run;
     p->cheb_pending_var = false;
-    return run_impl(p, true, &sg, 1);
+    p->pcg_pending_var = false;
+    p->force_factor = true;          // the variance needs the factor of this sigma
+    const int rc = run_impl(p, true, &sg, 1);
+    p->force_factor = false;
+    return rc;
 }
 
 // Test-set variance: compact the test panel to the plan's slots and the

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 11
+#define DBSLMM_ABI_VERSION 12
 
 enum {
     DBSLMM_OK = 0,
@@ -46,8 +46,14 @@ enum {
     DBSLMM_BLOCK_EMPTY = 1,        /* no SNP in this block */
     DBSLMM_BLOCK_NOT_PD = 2,       /* joint LD matrix not positive definite -> beta = NaN
                                       (reference: PCG "Matrix is Singular!", dbslmmfit.cpp:664) */
-    DBSLMM_BLOCK_MONOMORPHIC = 3   /* a SNP with zero variance -> NaN column in the reference
+    DBSLMM_BLOCK_MONOMORPHIC = 3,  /* a SNP with zero variance -> NaN column in the reference
                                       (dtpr.cpp:375-380); beta = NaN for the whole block */
+    DBSLMM_BLOCK_NOT_CONVERGED = 4 /* an iterative solve stopped at its iteration cap without
+                                      meeting its error bound: beta = the last iterate (the
+                                      reference's PCG prints "Matrix is Singular!" at maxiter and
+                                      returns its iterate, dbslmmfit.cpp:664-666).  The PCG route
+                                      (solver, pcg_maxit) and the h2f copies iterated on a base
+                                      factor (h2f_iter: CG / Chebyshev at their caps) report it. */
 };
 
 typedef struct dbslmm_ctx dbslmm_ctx;
@@ -64,10 +70,12 @@ typedef struct dbslmm_plan dbslmm_plan;
  * h2f_mode       plan_run_multi: 0 = tiled blocks factored once, the other sigmas solved by
  *                Chebyshev iteration on that factor when the bound allows (tau in (0, 1],
  *                <= 60 iterations); 1 = one factorisation per sigma (the merged sequence)
- * cheb_tol       relative error target of the Chebyshev iteration (default 1e-9: four orders below
- *                the 1e-5 parity bar on beta, one below the reference PCG's own deviation from the
- *                exact solution (~1e-8); the measured error is ~0.2 x the target: 7 iterations at
- *                h2f 0.8 / 1 / 1.2)
+ * cheb_tol       relative error target of the h2f copies iterated on the base copy's factor (default
+ *                1e-9: four orders below the 1e-5 parity bar on beta, one below the reference PCG's
+ *                own deviation from the exact solution (~1e-8)).  CG (the default h2f_iter) stops a
+ *                block once |r| <= cheb_tol lambda_min(M_c) |x| (5.03 iterations per tiled block at
+ *                config 4); Chebyshev runs its a priori count (7 at h2f 0.8 / 1 / 1.2), which is
+ *                also CG's cap
  * lead_min       tiled blocks with m >= lead_min form the lead group: their Gram tiles run first
  *                and their factorisation (the longest dependency chains) starts right after
  *                them, beside the rest of the Gram and the other blocks' factorisation (default
@@ -108,9 +116,26 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                (a priori coefficients and iteration count), 2 = preconditioned CG on the same
  *                factor (Chronopoulos-Gear form, dbslmm_cg_update / dbslmm_chol_cheb): stops per
  *                block once |r| <= cheb_tol lambda_min(M_c) |x|,
- *                capped at the Chebyshev count; 0 = the default (2).  Both within cheb_tol; the
+ *                capped at the Chebyshev count (a copy still above the bound there is reported
+ *                DBSLMM_BLOCK_NOT_CONVERGED); 0 = the default (2).  Both within cheb_tol; the
  *                base copy is bit-identical either way.  (cheb_fused = 1 and the whole-block rest
  *                group of sub_split = 2 iterate by Chebyshev.)
+ * solver         how a run solves its blocks (ABI 12): 1 = factorisation (fp64 Cholesky of every
+ *                block, the paths above); 2 = PCG: the reference's own algorithm (Jacobi-PCG,
+ *                dbslmmfit.cpp:629-678) on the joint matrix of every block, all h2f copies as
+ *                right-hand sides of one iteration, the LD matrix streamed from the Gram as exact
+ *                integers (uint16; fp64 Sigma for blocks with missing calls or n_ref > 16383);
+ *                0 = auto: PCG when every copy is well conditioned by its prior shift
+ *                (1/(sigma_s n) >= 2, so that kappa <= ~6 and <= ~35 iterations), 0 < tau < 1
+ *                (or no large SNPs), at most 4 copies and no debug_stop; the factorisation
+ *                otherwise.  dbslmm_plan_variance needs the factor: after a PCG run it
+ *                re-solves the latest sigma by factorisation first.
+ * pcg_tol        PCG: relative error bound per block and copy, |x - x*| <= pcg_tol |x*| in the
+ *                2-norm, enforced as |r| <= pcg_tol lambda |x| with lambda = 1/(sigma_s n) + 1 - tau
+ *                (blocks without large SNPs) or 1 - tau, lower bounds of lambda_min that hold for
+ *                any data (0 = default 1e-12)
+ * pcg_maxit      PCG: iteration cap (0 = default 1000, the reference's maxiter); a copy still
+ *                above its bound there is reported DBSLMM_BLOCK_NOT_CONVERGED with its iterate
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -128,6 +153,9 @@ typedef struct dbslmm_options {
     int32_t sub_grid_rest;
     int32_t shard_copies;
     int32_t h2f_iter;
+    int32_t solver;
+    double pcg_tol;
+    int32_t pcg_maxit;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.
@@ -165,8 +193,9 @@ typedef struct dbslmm_problem {
 /* Kernel timing slots reported by dbslmm_plan_kernel_ms. */
 enum {
     DBSLMM_K_UNPACK = 0,      /* dbslmm_unpack_stats: 2-bit .bed rows -> 2-bit dosage codes + stats */
-    DBSLMM_K_GRAM = 1,        /* dbslmm_gram_i8 / _big / _huge: i8-MFMA grouped syrk (codes expanded
-                                 on the fly) + fp64 standardising epilogue */
+    DBSLMM_K_GRAM = 1,        /* dbslmm_gram_i8 / _big / _huge: FP4-MFMA grouped syrk of the exact
+                                 integer dosages (2-bit codes expanded on the fly) + fp64
+                                 standardising epilogue (PCG route: the integer Gram as uint16) */
     DBSLMM_K_CHOL_LARGE = 2,  /* dbslmm_chol_large: blocks with 64 <= m+1 and m below the tiled
                                  threshold, one workgroup each */
     DBSLMM_K_CHOL_SMALL = 3,  /* dbslmm_chol_small: blocks with <= 63 SNPs, one wave each
@@ -175,9 +204,11 @@ enum {
                                  (dbslmm_options.tiled_min; default 384, or 256 when no block
                                  reaches 512), many workgroups per block,
                                  one launch per panel phase (third stream); the whole sequence */
-    DBSLMM_K_TRSV = 5,        /* dbslmm_trsv_fwd/bwd: h2f tuning's Chebyshev iterations of the
+    DBSLMM_K_TRSV = 5,        /* dbslmm_trsv_fwd/bwd: h2f tuning's CG / Chebyshev iterations of the
                                  tiled blocks on the base copy's factor (run_multi; 0 otherwise) */
-    DBSLMM_K_COUNT = 6
+    DBSLMM_K_PCG = 6,         /* dbslmm_pcg_*: the PCG route's iterations (init to final; 0 on the
+                                 factorisation route) */
+    DBSLMM_K_COUNT = 7
 };
 
 int dbslmm_abi_version(void);
@@ -276,15 +307,19 @@ int dbslmm_plan_enable_timing(dbslmm_plan* plan, int enable);
 int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/, int32_t* launches_out);
 
 /* Workload figures of the plan (for rooflines): [0] SNPs, [1] packed bytes read by the unpack,
- * [2] Gram operand (2-bit dosage code) bytes written by the unpack, [3] Gram int8 ops (2 per MAC, algorithmic
+ * [2] Gram operand (2-bit dosage code) bytes written by the unpack, [3] Gram ops (2 per MAC, algorithmic
  * sum_b n_ref*m_b*(m_b+1)), [4] Gram ops as executed on padded tiles, [5] Cholesky+solve fp64
  * flops of the large blocks (sum_b m_b^3/3 + 2 m_b^2), [6] non-empty blocks, [7] gram tiles,
  * [8] the same fp64 flops for the small blocks, [9] large blocks, [10] the same fp64 flops for
  * the tiled blocks, [11] tiled blocks, [12] launches of the tiled sequence per run, [13] bytes of
  * the factor read by one substitution launch over the tiled blocks (64-row tiles), [14] Chebyshev
  * iterations of the latest run_multi (0: none; with CG their cap), [15] its base copy (-1: none),
- * [16] factor bytes its h2f passes read (CG: each tiled block's own iteration count). */
-#define DBSLMM_WORKLOAD_LEN 17
+ * [16] factor bytes its h2f passes read (CG: each tiled block's own iteration count),
+ * [17] 1 when the latest run took the PCG route, [18] its iterations (the slowest block),
+ * [19] bytes one PCG iteration's product streams (the blocks' lower-triangle LD matrices in their
+ * storage: uint16 integer Gram / fp64 Sigma), [20] its partial-sum bytes (written + read once),
+ * [21] the product's fp64 flops per iteration (2 per stored element and copy, both directions). */
+#define DBSLMM_WORKLOAD_LEN 22
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
 
 /* Diagnostics (parity tests): after plan_sync, the working matrix of block `block` (original
