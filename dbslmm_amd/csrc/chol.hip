@@ -593,8 +593,9 @@ __device__ __forceinline__ void cg_sum4(double (&v)[4], double* red, int tid) {
     __syncthreads();
 }
 
-__device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, int nr, int iters,
-                           const double* __restrict__ coef, double* lds, const CgStop& cgs) {
+// Returns (CG) the copies still above their bound when the cap ended the loop: bit q = copy q.
+__device__ uint32_t cheb_block(const double* __restrict__ A, int ld, int m, int ms, int nr, int iters,
+                               const double* __restrict__ coef, double* lds, const CgStop& cgs) {
     constexpr int NT = kChebThreads, NG = NT / kT;
     const int tid = threadIdx.x;
     double* X = lds;                                 // [kChebR][kChebMaxM] each
@@ -606,6 +607,7 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
     double* red = Dt + kTileD;                       // [kChebR][NG][32] partial sums
     const int T = (m + kT - 1) / kT;
     double gp[kChebR] = {0.0, 0.0}, ap[kChebR] = {0.0, 0.0};   // CG: gamma, alpha of the previous iteration
+    uint32_t open = 0;                                   // CG: copies above their bound after the last update
     for (int k = 0; k < iters; ++k) {
         for (int e = tid; e < nr * kChebMaxM; e += NT) V[e] = R[e];
         __syncthreads();
@@ -747,13 +749,13 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
                 w[2 * q + 1] += x * x;
             }
             cg_sum4(w, red, tid);
-            bool done = true;
+            open = 0;
 #pragma unroll
             for (int q = 0; q < kChebR; ++q) {
                 const double t = cgs.tol * (ms == m ? cgs.fs[q] : cgs.fl);
-                if (q < nr) done = done && w[2 * q] <= t * t * w[2 * q + 1];   // NaN: not converged
+                if (q < nr && !(w[2 * q] <= t * t * w[2 * q + 1])) open |= 1u << q;   // NaN: not converged
             }
-            if (done) break;   // uniform: every thread holds the same totals
+            if (!open) break;   // uniform: every thread holds the same totals
             continue;
         }
         // Chebyshev update (V = M_b^{-1} r)
@@ -773,6 +775,7 @@ __device__ void cheb_block(const double* __restrict__ A, int ld, int m, int ms, 
         }
         __syncthreads();
     }
+    return cgs.on ? open : 0u;
 }
 
 }  // namespace chol
@@ -814,7 +817,10 @@ extern "C" __global__ __launch_bounds__(chol::kChebThreads) void dbslmm_chol_che
             Sv[e] = 0.0;
         }
         __syncthreads();
-        cheb_block(M_base + blk_matoff[b], ld, m, ms, nr, iters, coef, lds, cgs);
+        const uint32_t open = cheb_block(M_base + blk_matoff[b], ld, m, ms, nr, iters, coef, lds, cgs);
+        // CG reached its cap (the Chebyshev count) above the bound: reported, not silent
+        if (tid < nr && (open >> tid & 1u))
+            status[(tid == 0 ? c0 : c1) * st_stride + blk_id[b]] = DBSLMM_BLOCK_NOT_CONVERGED;
     }
     for (int e = tid; e < nr * m; e += kChebThreads) {
         const int q = e / m, i = e - q * m;

@@ -295,7 +295,8 @@ struct dbslmm_plan {
     do {                                                                                 \
         hipError_t e_ = (expr);                                                          \
         if (e_ != hipSuccess) {                                                          \
-            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+            (ctx)->err = std::string(#expr) + " (plan.hip:" + std::to_string(__LINE__) + "): " + \
+                         hipGetErrorString(e_);                                          \
             return DBSLMM_E_HIP;                                                         \
         }                                                                                \
     } while (0)
@@ -860,7 +861,13 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
                     p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16};
     for (void* b : bufs)
-        if (b) (void)hipFree(b);
+        if (b) {
+            const hipError_t e = hipFree(b);
+#ifdef DBSLMM_DIAG
+            if (e != hipSuccess) fprintf(stderr, "plan_destroy: hipFree(%p) -> %s\n", b, hipGetErrorString(e));
+#endif
+            (void)e;
+        }
     for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : p->dl_ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : p->tev) (void)hipEventDestroy(e);
@@ -1654,6 +1661,9 @@ static bool cheb_plan(const dbslmm_plan* p, const double* sigmas, int n, ChebPla
             K = std::max(K, k);
         }
         if (K > 60) return false;
+        // CG (h2f_iter 2) iterates adaptively with the Chebyshev count as its cap; pcg_maxit lowers
+        // that cap (tests drive a copy to it: DBSLMM_BLOCK_NOT_CONVERGED)
+        if (p->h2f_cg && !p->cheb_fused) K = std::min(K, p->pcg_maxit);
         cp.iters.push_back(K);
         cp.coef_off.push_back(cp.coef.size());
         std::vector<double> rho(nr);
@@ -1699,6 +1709,9 @@ static int cheb_prepare(dbslmm_plan* p, const ChebPlan& cp, hipStream_t st) {
         HIP_TRY(ctx, hipMalloc(&p->d_cgconv, nb * sizeof(int32_t)));
         HIP_TRY(ctx, hipMalloc(&p->d_cgit, nb * sizeof(int32_t)));
     }
+    // every block's CG pass count starts at 0 each run (the rest group of sub_split = 2 iterates by
+    // Chebyshev and never writes it; workload[16] sums it over every tiled block: ADVICE r05)
+    if (p->d_cgit) HIP_TRY(ctx, hipMemsetAsync(p->d_cgit, 0, std::max(1, p->n_nonempty) * sizeof(int32_t), st));
     // the coefficients depend only on the sigmas: uploaded when they change, synchronously (the
     // host vector is a temporary of the run; an asynchronous copy from pageable memory may still
     // be pending when it is freed) after every earlier run that reads d_coef has finished
@@ -1868,6 +1881,8 @@ static int run_cheb(dbslmm_plan* p, double isn, const ChebPlan& cp, const TGroup
                 ca.beta_l = p->d_beta_l;
                 ca.ns_stride = p->n_s;
                 ca.nl_stride = p->n_l;
+                ca.status = p->d_status;
+                ca.st_stride = p->nbk;
             }
             for (int k = 0; k < K; ++k) {
                 for (int pass = 0; pass < 2; ++pass) {
@@ -2000,7 +2015,7 @@ static int pcg_layout(dbslmm_plan* p, int n) {
                                                hipHostMallocDefault));
     if (p->pcg_n == n) return DBSLMM_OK;
     void* old[] = {p->d_pblk, p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
-                   p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16};
+                   p->d_pitb, p->d_pdone, p->d_pact};
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (void* q : old)
         if (q) (void)hipFree(q);
@@ -2122,8 +2137,26 @@ static int pcg_finish(dbslmm_plan* p) {
 // for the other blocks), then the iterations of every block and copy together.
 static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
     dbslmm_ctx* ctx = p->ctx;
+#ifdef DBSLMM_DIAG
+    {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) fprintf(stderr, "run_pcg: stale error on entry: %s\n", hipGetErrorString(e));
+    }
+#endif
     if (const int rc = ensure_copies(p, n, 1)) return rc;
+#ifdef DBSLMM_DIAG
+    {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) fprintf(stderr, "run_pcg: error after ensure_copies: %s\n", hipGetErrorString(e));
+    }
+#endif
     if (const int rc = pcg_layout(p, n)) return rc;
+#ifdef DBSLMM_DIAG
+    {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) fprintf(stderr, "run_pcg: error after pcg_layout: %s\n", hipGetErrorString(e));
+    }
+#endif
     hipStream_t s = ctx->stream;
     hipEvent_t* ev = nullptr;
     if (p->timing) {
@@ -2672,6 +2705,7 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* p, double* ms_out, int32_t* launches_out)
         int32_t runs = INT32_MAX;
         for (int k = 0; k < DBSLMM_K_COUNT; ++k) ms_out[k] = 0.0;
         for (auto& sh : p->mp->shards) {
+            if (p->ran && sh.run_copies.empty()) continue;   // a job the latest run skipped (stale)
             double ms[DBSLMM_K_COUNT];
             int32_t n = 0;
             dbslmm_plan_kernel_ms(sh.plan, ms, &n);
@@ -2701,7 +2735,10 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     if (p->mp) {   // sums over the jobs; [12] launches, [14] iterations: the max; [15] job 0's;
                    // SNPs [0] and blocks [6] once per block (not per split h2f copy)
         for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = 0.0;
+        out[15] = -1;
+        if (p->mp->shards.empty()) return DBSLMM_OK;   // a units plan whose device owns no unit
         for (auto& sh : p->mp->shards) {
+            if (p->ran && sh.run_copies.empty()) continue;   // a job the latest run skipped (stale)
             double w[DBSLMM_WORKLOAD_LEN];
             dbslmm_plan_workload(sh.plan, w);
             for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i)

@@ -508,7 +508,7 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_cheb_init(
 }
 
 // ---------------------------------------------------------------- h2f by conjugate gradients
-// The copies' iteration as preconditioned CG (dbslmm_options.h2f_iter = 1) instead of Chebyshev:
+// The copies' iteration as preconditioned CG (dbslmm_options.h2f_iter = 2, the default) instead of Chebyshev:
 // same operator M_c = M_b + delta P_s, same preconditioner (the base factor: one forward and one
 // backward pass per iteration), same state vectors (D = p, S = q = M_c p), and no product with
 // M_b either -- the Chronopoulos-Gear form takes both inner products from r and z = M_b^{-1} r:
@@ -553,6 +553,8 @@ struct CGArgs {
     double* beta_l;
     int64_t ns_stride, nl_stride;
     int32_t cix[kMaxR];
+    int32_t* status;             // per copy (cix) and original block: NOT_CONVERGED at the cap
+    int64_t st_stride;
 };
 // sums of v[0..4) over the workgroup, in a fixed order; every thread gets the totals
 __device__ __forceinline__ void cg_sum4(double (&v)[4], double (*red)[4], int tid) {
@@ -631,15 +633,18 @@ extern "C" __global__ __launch_bounds__(trsv::kCGThreads) void dbslmm_cg_update(
             w[2 * c + 1] += x * x;
         }
     cg_sum4(w, red, tid);
-    bool done = a.last || fail;
-    if (!done) {
-        done = true;
+    bool conv = true;
 #pragma unroll
-        for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
-            const double t = a.tol * (ms == m ? a.floor_s[c] : a.floor_l);
-            done = done && w[2 * c] <= t * t * w[2 * c + 1];   // NaN: not converged
-        }
+    for (int c = 0; c < kMaxR; ++c) if (c < a.nr) {
+        const double t = a.tol * (ms == m ? a.floor_s[c] : a.floor_l);
+        const bool cc = w[2 * c] <= t * t * w[2 * c + 1];   // NaN: not converged
+        conv = conv && cc;
+        // the cap (the Chebyshev count) reached without the bound: the copy keeps this iterate and
+        // reports it (the cap was silent); a failed base factor keeps its own status
+        if (a.last && !cc && !fail && tid == 0 && a.status)
+            a.status[a.cix[c] * a.st_stride + a.blk_id[b]] = DBSLMM_BLOCK_NOT_CONVERGED;
     }
+    const bool done = a.last || fail || conv;
     if (!done) return;
     for (int i = tid; i < m; i += kCGThreads) {   // this thread's own x entries
         const int so = a.slot_out[g0 + i];

@@ -135,7 +135,9 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                (blocks without large SNPs) or 1 - tau, lower bounds of lambda_min that hold for
  *                any data (0 = default 1e-12)
  * pcg_maxit      PCG: iteration cap (0 = default 1000, the reference's maxiter); a copy still
- *                above its bound there is reported DBSLMM_BLOCK_NOT_CONVERGED with its iterate
+ *                above its bound there is reported DBSLMM_BLOCK_NOT_CONVERGED with its iterate.
+ *                Also lowers the cap of the factorisation route's h2f CG (h2f_iter 2) below its
+ *                default, the Chebyshev count.
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;

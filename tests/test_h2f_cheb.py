@@ -274,3 +274,36 @@ def test_cg_with_lead_group(split):
             np.testing.assert_array_equal(_cat(got), _cat(ref))
         else:
             assert _finite_normwise(_cat(got), _cat(ref)) < CHEB_TOL, c
+
+
+@pytest.mark.parametrize("tiled_min", ["64", "512"])
+def test_cg_cap_reports_not_converged(tiled_min):
+    """an h2f copy that stops at the CG cap without meeting |r| <= cheb_tol
+    lambda_min |x| was written with BLOCK_OK.  With the cap lowered to one iteration and a tight
+    bound, every iterated copy of a tiled (tiled_min 64) or single-workgroup (512) block reports
+    DBSLMM_BLOCK_NOT_CONVERGED with a finite iterate; the base copy (factored) stays OK; the
+    default cap converges every copy (status OK)."""
+    from dbslmm_amd import BLOCK_NOT_CONVERGED, Context, Plan
+    prob = _problem(seed=5)
+    prob.opts.update(tiled_min=int(tiled_min), solver=1, pcg_maxit=1, cheb_tol=1e-13)
+    sig = [prob.sigma_s * f for f in (0.8, 1.0, 1.2)]
+    plan = Plan(Context(0), prob)
+    out = plan.run_multi(sig)
+    base = 1
+    m_b = np.diff(prob.s_ptr) + np.diff(prob.l_ptr)
+    it_blocks = m_b + 1 > 64          # blocks iterated on the base factor (tiled / chol_large)
+    assert it_blocks.sum() > 0
+    for c in range(3):
+        st = out[c][2]
+        assert np.all(np.isfinite(_cat(out[c])))
+        if c == base:
+            assert np.all(st == 0)
+        else:
+            assert np.all(st[it_blocks] == BLOCK_NOT_CONVERGED), (c, st)
+            assert np.all(st[~it_blocks] == 0)
+    plan.close()
+    prob.opts.update(pcg_maxit=0, cheb_tol=0.0)
+    plan = Plan(Context(0), prob)
+    for bs, bl, st in plan.run_multi(sig):
+        assert np.all(st == 0)
+    plan.close()
