@@ -54,10 +54,11 @@ constexpr int kMaxNC = 4;         // h2f copies per run (right-hand sides) on th
 constexpr int kWaves = 4;         // symv items per 256-thread workgroup
 constexpr int kVS = kT + 8;       // LDS stride of a staged vector column (doubles)
 constexpr int kNDot = 5;          // per tile row and copy: r.u, w.u, r.r, x.x, S.(rsd o u)
+constexpr int kQS = 8;            // recurrence state doubles per block and copy
 constexpr int kThreads = 256;
-// symv LDS per wave: the staged rsd o u of the item's tile row and of the current tile column, and
-// the reduce-scattered row / column sums ([2][copy][64] each)
-constexpr int wave_lds_doubles(int nc) { return 2 * nc * kVS + 4 * nc * 64; }
+// symv LDS per wave: the staged rsd o u of the item's tile row and of two tile columns, and the
+// reduce-scattered row / column sums ([2][copy][64] each)
+constexpr int wave_lds_doubles(int nc) { return 3 * nc * kVS + 4 * nc * 64; }
 constexpr size_t lds_bytes(int nc) { return sizeof(double) * kWaves * wave_lds_doubles(nc); }
 }  // namespace pcg
 
@@ -69,6 +70,8 @@ struct PcgBlk {
     int64_t matoff, vo, po, dof;    // vectors (per copy Tb * kT), partials, dots
     int64_t off16;                  // the integer Gram: Tb kT x Tb kT uint16 at off16 (rows and
                                     // columns past m stay zero: no masks in the product)
+    int32_t nc;                     // product columns: 1 (multi-shift block) or the copies
+    int32_t mshift;                 // 1: no large SNP and several copies -> one Krylov sequence
 };
 
 struct PcgArgs {
@@ -85,7 +88,8 @@ struct PcgArgs {
     double *X, *R, *P, *Sv, *W;     // state vectors, [copy][Tb * kT] per block
     double* part;                   // symv partial slots
     double* dot;                    // per tile row [kNDot][copy]
-    double* qs;                     // per block copy: {gamma, alpha} x 2 parities
+    double* qs;                     // per block copy: {gamma, alpha} x 2 parities, then the
+                                    // multi-shift {zeta_k, zeta_k-1} x 2 parities (kQS doubles)
     int32_t* cnv;                   // per block copy: iteration + 1 at convergence (0: running)
     int32_t* itb;                   // per block: rows launches since init
     int32_t* done;                  // per block: 0 iterating, 1 converged, 2 monomorphic
@@ -97,6 +101,7 @@ struct PcgArgs {
     int64_t ns, nl, nbk;            // beta / status strides per copy
     double tau, rn, c0, tol, inv_sqrt_n;
     int32_t ncopy;
+    int32_t seed;                   // multi-shift seed: the copy with the smallest shift
 };
 
 namespace pcg {
@@ -149,9 +154,15 @@ __device__ __forceinline__ bool on_u16(const PcgArgs& a, const PcgBlk& B) {
     return a.G16 != nullptr && (a.flags[B.blk] & 1) == 0;
 }
 
-// Jacobi diagonal of M_c at block slot i (c0 + d_c on small SNPs)
+// Jacobi diagonal of M_c at block slot i (c0 + d_c on small SNPs); 1 on a multi-shift block
+// (no large SNP: the diagonal is the constant c0 + d_c, and the shifted systems share one Krylov
+// space only without a preconditioner)
 __device__ __forceinline__ double jdiag(const PcgArgs& a, const PcgBlk& B, int i, double dc) {
-    return i < B.ms ? a.c0 + dc : a.c0;
+    return B.mshift ? 1.0 : i < B.ms ? a.c0 + dc : a.c0;
+}
+// the shift of product column k (the seed's on a multi-shift block)
+__device__ __forceinline__ double col_shift(const PcgArgs& a, const PcgBlk& B, int k) {
+    return a.dshift[B.mshift ? a.seed : k];
 }
 
 // uint16 -> fp64 of the low / high half of a dword.  Volatile asm: the conversions stay inside the
@@ -253,7 +264,7 @@ __device__ __forceinline__ void quad_mul64(const double* __restrict__ base, int6
 __device__ __forceinline__ void stage_v(const PcgArgs& a, const PcgBlk& B, bool u16, int T, int nc, int lane,
                                         double* v) {
     for (int k = 0; k < nc; ++k) {
-        const double dc = a.dshift[k];
+        const double dc = col_shift(a, B, k);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int rr = lane + 64 * h, i = T * kT + rr;
@@ -267,54 +278,126 @@ __device__ __forceinline__ void stage_v(const PcgArgs& a, const PcgBlk& B, bool 
     }
 }
 
-// One symv item on one wave.  LDS (wave-private): vI, vJ = rsd o u of the item's tile row and of
-// the current tile column ([copy][kVS]); rsum / csum = the reduce-scattered row results of the run
-// and column results of the current tile ([qi or qj][copy][lane]).
+// the same in two halves, so a tile column's vector loads can be issued ahead of the next
+// quadrant's row segments (vmcnt counts in issue order: waiting for loads issued after the
+// prefetch would drain it)
+struct StageRegs {
+    double r[kMaxNC][2], s[2];
+};
+__device__ __forceinline__ void stage_load(const PcgArgs& a, const PcgBlk& B, bool u16, int T, int nc, int lane,
+                                           StageRegs& g) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = T * kT + lane + 64 * h;
+        const bool in = i < B.m;
+        g.s[h] = in && u16 ? a.rsd[B.row0 + i] : 1.0;
+#pragma unroll
+        for (int k = 0; k < kMaxNC; ++k)
+            g.r[k][h] = k < nc && in ? a.R[k * a.vstride + B.vo + i] : 0.0;
+    }
+}
+__device__ __forceinline__ void stage_store(const PcgArgs& a, const PcgBlk& B, int T, int nc, int lane,
+                                            const StageRegs& g, double* v) {
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k) {
+        if (k >= nc) break;
+        const double dc = col_shift(a, B, k);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int rr = lane + 64 * h, i = T * kT + rr;
+            v[k * kVS + rr] = g.r[k][h] / jdiag(a, B, i, dc) * g.s[h];
+        }
+    }
+}
+
+// One symv item on one wave.  LDS (wave-private): vI = rsd o u of the item's tile row, vJ[2] = the
+// same of the current and the next tile column ([copy][kVS] each), rsum / csum = the
+// reduce-scattered row results of the run and column results of the current tile
+// ([qi or qj][copy][lane]).  The item's active quadrants are visited in order (tiles J0 .. J1,
+// quadrants q = 2 qi + qj: a diagonal tile has no upper quadrant, quadrants wholly past m are
+// skipped), software-pipelined: the next quadrant's 8 KB of row segments and, at a tile change,
+// the next column vector are in flight while the current quadrant is multiplied.
+__device__ __forceinline__ bool quad_active(const PcgBlk& B, int I, int J, int q) {
+    const int qi = q >> 1, qj = q & 1;
+    return !(J == I && qj > qi) && I * kT + 64 * qi < B.m && J * kT + 64 * qj < B.m;
+}
+// the next active quadrant after (J, q) within tiles .. J1; false at the end
+__device__ __forceinline__ bool next_quad(const PcgBlk& B, int I, int J1, int& J, int& q) {
+    for (;;) {
+        if (++q == 4) {
+            q = 0;
+            if (++J > J1) return false;
+        }
+        if (quad_active(B, I, J, q)) return true;
+    }
+}
+
 template <bool U16>
-__device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, double* vJ, double* rsum,
+__device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, double* vJb, double* rsum,
                           double* csum) {
     const PcgBlk B = a.blk[item.x];
     if (a.done[item.x] || on_u16(a, B) != U16) return;
-    const int I = item.y, J0 = item.z, J1 = item.w, nc = a.ncopy;
+    const int I = item.y, J0 = item.z, J1 = item.w, nc = B.nc;
     constexpr bool u16 = U16;
     const int64_t ld16 = static_cast<int64_t>(B.Tb) * kT;
     const int rg = lane >> 3, cg = lane & 7;
-    stage_v(a, B, u16, I, nc, lane, vI);
-    for (int q = 0; q < 2 * nc; ++q) rsum[q * 64 + lane] = 0.0;
-    for (int J = J0; J <= J1; ++J) {
-        const double* vj = vI;
-        if (J != I) {
-            wave_fence();                     // every lane is done with the previous tile's vJ
-            stage_v(a, B, u16, J, nc, lane, vJ);
-            vj = vJ;
-        }
-        for (int q = 0; q < 2 * nc; ++q) csum[q * 64 + lane] = 0.0;
-        wave_fence();
-        for (int qi = 0; qi < 2; ++qi)
-            for (int qj = 0; qj < 2; ++qj) {
-                if (J == I && qj > qi) continue;              // upper quadrant of a diagonal tile
-                const int i0 = I * kT + 64 * qi, j0 = J * kT + 64 * qj;
-                if (i0 >= B.m || j0 >= B.m) continue;         // quadrant wholly past the block
-                const bool dq = J == I && qi == qj;
-                double* rs = rsum + qi * nc * 64;
-                double* cs = csum + qj * nc * 64;
-                if constexpr (U16) {
-                    // the quadrant's 8 KB: one 16-B row segment per lane and row (zero past m)
-                    const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(i0 + 8 * rg) * ld16 + j0 + 8 * cg;
-                    pcg_u4 raw[8];
+    auto vj_of = [&](int J) -> double* { return J == I ? vI : vJb + ((J - J0) & 1) * nc * kVS; };
+    auto load = [&](int J, int q, pcg_u4 (&raw)[8]) {
+        if constexpr (U16) {
+            const int i0 = I * kT + 64 * (q >> 1), j0 = J * kT + 64 * (q & 1);
+            const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(i0 + 8 * rg) * ld16 + j0 + 8 * cg;
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) raw[r] = *reinterpret_cast<const pcg_u4*>(q16 + r * ld16);
-                    quad_mul16(raw, dq, lane, nc, vI + 64 * qi, vj + 64 * qj, rs, cs);
-                } else {
-                    const int ib = i0 + 8 * rg, jb = j0 + 8 * cg;
-                    quad_mul64(a.M + B.matoff + static_cast<int64_t>(ib) * B.ld + jb, B.ld, B.m - ib, B.m - jb,
-                               dq, lane, nc, vI + 64 * qi, vj + 64 * qj, rs, cs);
-                }
-            }
-        // column partial of tile (I, J): slot I of tile row J (the diagonal tile: slot I of row I)
+            for (int r = 0; r < 8; ++r) raw[r] = *reinterpret_cast<const pcg_u4*>(q16 + r * ld16);
+        }
+    };
+    auto mult = [&](int J, int q, const pcg_u4 (&raw)[8]) {
+        const int qi = q >> 1, qj = q & 1;
+        const bool dq = J == I && qi == qj;
+        const double* vj = vj_of(J);
+        double* rs = rsum + qi * nc * 64;
+        double* cs = csum + qj * nc * 64;
+        if constexpr (U16) {
+            quad_mul16(raw, dq, lane, nc, vI + 64 * qi, vj + 64 * qj, rs, cs);
+        } else {
+            const int ib = I * kT + 64 * qi + 8 * rg, jb = J * kT + 64 * qj + 8 * cg;
+            quad_mul64(a.M + B.matoff + static_cast<int64_t>(ib) * B.ld + jb, B.ld, B.m - ib, B.m - jb, dq,
+                       lane, nc, vI + 64 * qi, vj + 64 * qj, rs, cs);
+        }
+    };
+    auto flush = [&](int J) {   // column partial of tile (I, J): slot I of tile row J
         double* dst = a.part + B.po + (static_cast<int64_t>(J) * B.Ns + I) * nc * kT;
         for (int qj = 0; qj < 2; ++qj)
-            for (int k = 0; k < nc; ++k) dst[k * kT + 64 * qj + 8 * cg + rg] = csum[(qj * nc + k) * 64 + lane];
+            for (int k = 0; k < nc; ++k) {
+                dst[k * kT + 64 * qj + 8 * cg + rg] = csum[(qj * nc + k) * 64 + lane];
+                csum[(qj * nc + k) * 64 + lane] = 0.0;
+            }
+    };
+    pcg_u4 ra[8], rb[8];
+    int J = J0, q = 0;                       // quadrant 0 of a tile of the run is always active
+    load(J, q, ra);
+    stage_v(a, B, u16, I, nc, lane, vI);
+    if (J != I) stage_v(a, B, u16, J, nc, lane, vj_of(J));
+    for (int t = 0; t < 2 * nc; ++t) rsum[t * 64 + lane] = csum[t * 64 + lane] = 0.0;
+    wave_fence();
+    // one pipeline step: prefetch the next quadrant into `nxt` (and, at a tile change, the next
+    // column vector: its loads first, so waiting for them leaves the row segments in flight),
+    // multiply the current one from `cur`; false when the item is done
+    auto step = [&](pcg_u4 (&cur)[8], pcg_u4 (&nxt)[8]) -> bool {
+        int Jn = J, qn = q;
+        const bool more = next_quad(B, I, J1, Jn, qn);
+        const bool newcol = more && Jn != J && Jn != I;
+        StageRegs sg;
+        if (newcol) stage_load(a, B, u16, Jn, nc, lane, sg);
+        if (more) load(Jn, qn, nxt);
+        if (newcol) stage_store(a, B, Jn, nc, lane, sg, vj_of(Jn));
+        mult(J, q, cur);
+        if (!more || Jn != J) flush(J);
+        wave_fence();                        // the next column vector is in LDS before its use
+        J = Jn;
+        q = qn;
+        return more;
+    };
+    while (step(ra, rb) && step(rb, ra)) {
     }
     // row partial of the run: slot Tb + run of tile row I
     double* dst = a.part + B.po + (static_cast<int64_t>(I) * B.Ns + B.Tb + J0 / kRun) * nc * kT;
@@ -326,9 +409,9 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
 
 // ------------------------------------------------------------------------------------------
 // Right-hand sides and state.  One workgroup per (block, 128-row tile row): x = p = s = w = 0,
-// r = z (every copy), the partial S.(rsd o u) of the first product.  Tile row 0 also resets the
-// block's counters and flags a monomorphic block (a zero-variance SNP: the reference's 0/0 column,
-// beta NaN for the whole block, status MONOMORPHIC) as done.
+// r = z (every product column), the partial S.(rsd o u) of the first product.  Tile row 0 also
+// resets the block's counters and recurrence state and flags a monomorphic block (a zero-variance
+// SNP: the reference's 0/0 column, beta NaN for the whole block, status MONOMORPHIC) as done.
 // ------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_init(PcgArgs a, const int2* __restrict__ rows) {
     using namespace pcg;
@@ -338,6 +421,7 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_init(PcgA
     const int bi = it.x, I = it.y, tid = threadIdx.x;
     const PcgBlk B = a.blk[bi];
     const bool u16 = on_u16(a, B);
+    const int n = a.ncopy, nc = B.nc;
     if (I == 0) {
         if (tid == 0) mono_s = 0;
         __syncthreads();
@@ -345,38 +429,49 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_init(PcgA
         for (int i = tid; i < B.m; i += kThreads) mono |= !(a.rsd[B.row0 + i] < INFINITY);
         if (mono) atomicOr(&mono_s, 1);
         __syncthreads();
-        if (tid < a.ncopy) a.cnv[B.sco + tid] = 0;
+        if (tid < n) {
+            a.cnv[B.sco + tid] = 0;
+            double* q = a.qs + static_cast<int64_t>(B.sco + tid) * kQS;
+            q[4] = q[5] = 1.0;           // zeta_0 = zeta_-1 = 1 (parity 0)
+        }
         if (tid == 0) {
             a.itb[bi] = 0;
             a.done[bi] = mono_s ? 2 : 0;
             if (!mono_s) atomicAdd(a.active, 1);
         }
     }
-    // rows 0..127 of the tile row, two halves of the copies
+    // rows 0..127 of the tile row, two halves of the columns
     const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
     const bool in = i < B.m;
     double sv[kMaxNC];
 #pragma unroll
     for (int k = 0; k < kMaxNC; ++k) sv[k] = 0.0;
-    for (int k = h; k < a.ncopy; k += 2) {
-        const int64_t o = k * a.vstride + B.vo + i;
+    for (int c = h; c < n; c += 2) {
+        const int64_t o = c * a.vstride + B.vo + i;
         const double rhs = in ? a.z[B.row0 + i] : 0.0;
         a.X[o] = 0.0;
         a.P[o] = 0.0;
-        a.Sv[o] = 0.0;
-        a.W[o] = 0.0;
-        a.R[o] = rhs;
-        if (in && u16) sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rhs / jdiag(a, B, i, a.dshift[k]));
+        if (c < nc) {
+            a.Sv[o] = 0.0;
+            a.W[o] = 0.0;
+            a.R[o] = rhs;
+        }
     }
+#pragma unroll
+    for (int k = 0; k < kMaxNC; ++k)
+        if (k < nc && (k & 1) == h && in && u16) {
+            const double rhs = a.z[B.row0 + i];
+            sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rhs / jdiag(a, B, i, col_shift(a, B, k)));
+        }
 #pragma unroll
     for (int k = 0; k < kMaxNC; ++k) sv[k] = wave_sum(sv[k]);
     if ((tid & 63) == 0)
 #pragma unroll
         for (int k = 0; k < kMaxNC; ++k) red[tid >> 6][k] = sv[k];
     __syncthreads();
-    if (tid < a.ncopy) {
-        const int hk = tid & 1;   // the half that handled copy tid: waves 2 hk, 2 hk + 1
-        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * a.ncopy + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
+    if (tid < nc) {
+        const int hk = tid & 1;   // the half that handled column tid: waves 2 hk, 2 hk + 1
+        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * n + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
     }
 }
 
@@ -396,10 +491,10 @@ __device__ __forceinline__ void symv_body(const PcgArgs& a, const int4* __restri
     if (e >= n_items) return;
     const int nc = a.ncopy;
     double* w = vlds + wave * wave_lds_doubles(nc);
-    symv_item<U16>(a, items[e], lane, w, w + nc * kVS, w + 2 * nc * kVS, w + 2 * nc * kVS + 2 * nc * 64);
+    symv_item<U16>(a, items[e], lane, w, w + nc * kVS, w + 3 * nc * kVS, w + 3 * nc * kVS + 2 * nc * 64);
 }
 #ifndef PCG_SYMV_WAVES
-#define PCG_SYMV_WAVES 3   // waves per SIMD the uint16 product is compiled for (4: 37 VGPRs spilled)
+#define PCG_SYMV_WAVES 2   // waves per SIMD the uint16 product is compiled for (a whole tile in flight per wave)
 #endif
 extern "C" __global__ __launch_bounds__(pcg::kThreads) __attribute__((amdgpu_waves_per_eu(PCG_SYMV_WAVES, 8)))
 void dbslmm_pcg_symv16(PcgArgs a, const int4* __restrict__ items, int32_t n_items) {
@@ -411,7 +506,8 @@ void dbslmm_pcg_symv64(PcgArgs a, const int4* __restrict__ items, int32_t n_item
 }
 
 // ------------------------------------------------------------------------------------------
-// w = M_c u for one tile row from its partial slots (fixed order), and the partial dots.
+// w = M_c u for one tile row from its partial slots (fixed order), and the partial dots: per
+// product column r.u, w.u, r.r; per copy x.x (a multi-shift block's copies share its one column).
 // ------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgArgs a, const int2* __restrict__ rows) {
     using namespace pcg;
@@ -422,9 +518,9 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgA
     if (a.done[bi]) return;
     const PcgBlk B = a.blk[bi];
     const bool u16 = on_u16(a, B);
-    const int nc = a.ncopy;
+    const int n = a.ncopy, nc = B.nc;
     if (tid < nc)                        // sigma_k = S . (rsd o u) over the block (fixed order)
-        sig[tid] = ordered_sum(a.dot + B.dof + 4 * nc + tid, kNDot * nc, 0, B.Tb, 0.0);
+        sig[tid] = ordered_sum(a.dot + B.dof + 4 * n + tid, kNDot * n, 0, B.Tb, 0.0);
     __syncthreads();
     const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
     const bool in = i < B.m;
@@ -437,24 +533,27 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgA
         for (int f = 0; f < 4; ++f) dv[k][f] = 0.0;
 #pragma unroll
     for (int k = 0; k < kMaxNC; ++k) {
-        if (k >= nc || (k & 1) != h) continue;
-        const double* pp = a.part + B.po + static_cast<int64_t>(I) * B.Ns * nc * kT + k * kT + r;
-        double y = ordered_sum(pp, nc * kT, I, B.Tb, 0.0);
-        y = ordered_sum(pp, nc * kT, B.Tb, B.Tb + nrun, y);
+        if (k >= n || (k & 1) != h) continue;
         const int64_t o = k * a.vstride + B.vo + i;
-        const double dc = a.dshift[k];
-        const double rv = a.R[o], xv = a.X[o];
-        const double u = in ? rv / jdiag(a, B, i, dc) : 0.0;
-        const double sh = i < B.ms ? dc : 0.0;
-        double w = 0.0;
-        if (in) {
-            if (u16) w = a.tau * a.rn * ri * __builtin_fma(-Si, sig[k] * a.rn, y) + (1.0 - a.tau + sh) * u;
-            else w = y + sh * u;
+        if (k < nc) {
+            const double* pp = a.part + B.po + static_cast<int64_t>(I) * B.Ns * nc * kT + k * kT + r;
+            double y = ordered_sum(pp, nc * kT, I, B.Tb, 0.0);
+            y = ordered_sum(pp, nc * kT, B.Tb, B.Tb + nrun, y);
+            const double dc = col_shift(a, B, k);
+            const double rv = a.R[o];
+            const double u = in ? rv / jdiag(a, B, i, dc) : 0.0;
+            const double sh = i < B.ms ? dc : 0.0;
+            double w = 0.0;
+            if (in) {
+                if (u16) w = a.tau * a.rn * ri * __builtin_fma(-Si, sig[k] * a.rn, y) + (1.0 - a.tau + sh) * u;
+                else w = y + sh * u;
+            }
+            a.W[o] = w;
+            dv[k][0] = rv * u;
+            dv[k][1] = w * u;
+            dv[k][2] = rv * rv;
         }
-        a.W[o] = w;
-        dv[k][0] = rv * u;
-        dv[k][1] = w * u;
-        dv[k][2] = rv * rv;
+        const double xv = a.X[o];
         dv[k][3] = xv * xv;
     }
 #pragma unroll
@@ -467,9 +566,10 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgA
 #pragma unroll
             for (int f = 0; f < 4; ++f) red[tid >> 6][k][f] = dv[k][f];
     __syncthreads();
-    if (tid < 4 * nc) {
+    if (tid < 4 * n) {
         const int k = tid >> 2, f = tid & 3, hk = k & 1;
-        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + f) * nc + k] = red[2 * hk][k][f] + red[2 * hk + 1][k][f];
+        if (f == 3 || k < nc)
+            a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + f) * n + k] = red[2 * hk][k][f] + red[2 * hk + 1][k][f];
     }
     if (I == 0 && tid == 0) a.itb[bi] += 1;
 }
@@ -479,11 +579,22 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgA
 // block's dots in the same order, so every tile row takes the same decisions; tile row 0 alone
 // writes the recurrence state (the other parity than the one read), the convergence iteration
 // and the block's done flag.
+//   per-copy blocks: Jacobi-PCG per copy in the Chronopoulos-Gear form
+//       gamma = r.u, delta = w.u, beta = gamma / gamma_prev, alpha = gamma / (delta - beta gamma / alpha_prev)
+//       p = u + beta p, s = w + beta s, x += alpha p, r -= alpha s
+//   multi-shift blocks (tools/multishift_check.py): the same for the seed (smallest shift, column
+//   0, no preconditioner); copy c (shift e = d_c - d_seed >= 0) follows from the seed's scalars,
+//   c' = alpha_k beta_k-1 / alpha_k-1:
+//       zeta_k+1 = zeta_k zeta_k-1 / ((1 + c' + alpha_k e) zeta_k-1 - c' zeta_k)
+//       alpha_c = alpha_k zeta_k+1 / zeta_k, beta_c = (zeta_k / zeta_k-1)^2 beta_k-1
+//       p_c = zeta_k r + beta_c p_c, x_c += alpha_c p_c, |r_c| = |zeta_k| |r|
+// Stopping per copy: |r_c| <= tol lambda_c |x_c|.
 // ------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(PcgArgs a, const int2* __restrict__ rows) {
     using namespace pcg;
     __shared__ double tot[kMaxNC][4];
-    __shared__ double coef[kMaxNC][2];
+    __shared__ double coef[kMaxNC][3];   // per copy: alpha, beta, zeta_k (multi-shift; 1 otherwise)
+    __shared__ double seedc[2];          // multi-shift: the seed's alpha, beta
     __shared__ int run_s[kMaxNC];
     __shared__ double red[kThreads / 64][kMaxNC];
     const int2 it = rows[blockIdx.x];
@@ -491,45 +602,90 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
     if (a.done[bi]) return;
     const PcgBlk B = a.blk[bi];
     const bool u16 = on_u16(a, B);
-    const int nc = a.ncopy;
+    const int n = a.ncopy, nc = B.nc;
     const int itn = a.itb[bi] - 1;       // the iteration whose dots the rows launch wrote
-    if (tid < 4 * nc) {
+    const int par = itn & 1;
+    if (tid < 4 * n) {
         const int k = tid >> 2, f = tid & 3;
-        tot[k][f] = ordered_sum(a.dot + B.dof + f * nc + k, kNDot * nc, 0, B.Tb, 0.0);
+        tot[k][f] = (f == 3 || k < nc) ? ordered_sum(a.dot + B.dof + f * n + k, kNDot * n, 0, B.Tb, 0.0) : 0.0;
     }
     __syncthreads();
-    if (tid < nc) {
-        const int k = tid;
-        const double gam = tot[k][0], del = tot[k][1], rr = tot[k][2], xx = tot[k][3];
-        const double lam = B.ms == B.m ? a.dshift[k] + 1.0 - a.tau : 1.0 - a.tau;
-        const double t = a.tol * lam;
-        // converged: |r| <= tol lambda_min |x| (a bound on the relative error of x), or r = 0;
-        // NaN never converges (the cap then reports it)
-        const bool conv = a.cnv[B.sco + k] != 0 || rr == 0.0 || rr <= t * t * xx;
-        double al = 0.0, be = 0.0;
-        if (!conv) {
-            const int par = itn & 1;
-            double* q = a.qs + static_cast<int64_t>(B.sco + k) * 4;
+    if (B.mshift) {
+        if (tid == 0) {                  // the seed's coefficients (identical in every workgroup)
+            const double gam = tot[0][0], del = tot[0][1];
+            const double* q = a.qs + static_cast<int64_t>(B.sco) * kQS;
+            double al, be = 0.0;
             if (itn == 0) {
                 al = gam / del;
             } else {
                 be = gam / q[2 * par];
                 al = gam / (del - be * gam / q[2 * par + 1]);
             }
-            if (I == 0) {
-                q[2 * (par ^ 1)] = gam;
-                q[2 * (par ^ 1) + 1] = al;
-            }
-        } else if (I == 0 && a.cnv[B.sco + k] == 0) {
-            a.cnv[B.sco + k] = itn + 1;
+            seedc[0] = al;
+            seedc[1] = be;
         }
-        coef[k][0] = al;
-        coef[k][1] = be;
-        run_s[k] = conv ? 0 : 1;
+        __syncthreads();
+        if (tid < n) {
+            const int c = tid;
+            double* q = a.qs + static_cast<int64_t>(B.sco + c) * kQS;
+            const double al = seedc[0], be = seedc[1];
+            const double zk = q[4 + 2 * par], zk1 = q[4 + 2 * par + 1];
+            const double rr = tot[0][2] * zk * zk, xx = tot[c][3];
+            const double t = a.tol * (a.dshift[c] + 1.0 - a.tau);
+            const bool conv = a.cnv[B.sco + c] != 0 || rr == 0.0 || rr <= t * t * xx;
+            const double e = a.dshift[c] - a.dshift[a.seed];
+            const double cp = itn == 0 ? 0.0 : al * be / a.qs[static_cast<int64_t>(B.sco) * kQS + 2 * par + 1];
+            const double zn = zk * zk1 / ((1.0 + cp + al * e) * zk1 - cp * zk);
+            coef[c][0] = al * zn / zk;
+            coef[c][1] = zk1 != 0.0 ? (zk / zk1) * (zk / zk1) * be : 0.0;
+            coef[c][2] = zk;
+            run_s[c] = conv ? 0 : 1;
+            if (I == 0) {
+                if (conv && a.cnv[B.sco + c] == 0) a.cnv[B.sco + c] = itn + 1;
+                q[4 + 2 * (par ^ 1)] = zn;
+                q[4 + 2 * (par ^ 1) + 1] = zk;
+            }
+        }
+        __syncthreads();
+        if (I == 0 && tid == 0) {        // the seed's recurrence state (after every reader above)
+            double* q = a.qs + static_cast<int64_t>(B.sco) * kQS;
+            q[2 * (par ^ 1)] = tot[0][0];
+            q[2 * (par ^ 1) + 1] = seedc[0];
+        }
+    } else {
+        if (tid < n) {
+            const int k = tid;
+            const double gam = tot[k][0], del = tot[k][1], rr = tot[k][2], xx = tot[k][3];
+            const double lam = B.ms == B.m ? a.dshift[k] + 1.0 - a.tau : 1.0 - a.tau;
+            const double t = a.tol * lam;
+            // converged: |r| <= tol lambda_min |x| (a bound on the relative error of x), or r = 0;
+            // NaN never converges (the cap then reports it)
+            const bool conv = a.cnv[B.sco + k] != 0 || rr == 0.0 || rr <= t * t * xx;
+            double al = 0.0, be = 0.0;
+            if (!conv) {
+                double* q = a.qs + static_cast<int64_t>(B.sco + k) * kQS;
+                if (itn == 0) {
+                    al = gam / del;
+                } else {
+                    be = gam / q[2 * par];
+                    al = gam / (del - be * gam / q[2 * par + 1]);
+                }
+                if (I == 0) {
+                    q[2 * (par ^ 1)] = gam;
+                    q[2 * (par ^ 1) + 1] = al;
+                }
+            } else if (I == 0 && a.cnv[B.sco + k] == 0) {
+                a.cnv[B.sco + k] = itn + 1;
+            }
+            coef[k][0] = al;
+            coef[k][1] = be;
+            coef[k][2] = 1.0;
+            run_s[k] = conv ? 0 : 1;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     int running = 0;
-    for (int k = 0; k < nc; ++k) running += run_s[k];
+    for (int k = 0; k < n; ++k) running += run_s[k];
     if (running == 0) {
         if (I == 0 && tid == 0) {
             a.done[bi] = 1;
@@ -542,22 +698,45 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
     double sv[kMaxNC];
 #pragma unroll
     for (int k = 0; k < kMaxNC; ++k) sv[k] = 0.0;
+    if (B.mshift) {
+        if (in) {
+            const int64_t o0 = B.vo + i;
+            const double rv = a.R[o0];
 #pragma unroll
-    for (int k = 0; k < kMaxNC; ++k) {
-        if (k >= nc || (k & 1) != h || !run_s[k] || !in) continue;
-        const int64_t o = k * a.vstride + B.vo + i;
-        const double al = coef[k][0], be = coef[k][1];
-        const double dg = jdiag(a, B, i, a.dshift[k]);
-        const double u = a.R[o] / dg;
-        const double p = __builtin_fma(be, a.P[o], u);
-        const double s = __builtin_fma(be, a.Sv[o], a.W[o]);
-        const double x = __builtin_fma(al, p, a.X[o]);
-        const double rn = __builtin_fma(-al, s, a.R[o]);
-        a.P[o] = p;
-        a.Sv[o] = s;
-        a.X[o] = x;
-        a.R[o] = rn;
-        if (u16) sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rn / dg);
+            for (int c = 0; c < kMaxNC; ++c) {
+                if (c >= n || (c & 1) != h || !run_s[c]) continue;
+                const int64_t o = c * a.vstride + o0;
+                const double p = __builtin_fma(coef[c][1], a.P[o], coef[c][2] * rv);
+                a.P[o] = p;
+                a.X[o] = __builtin_fma(coef[c][0], p, a.X[o]);
+            }
+            if (h == 0) {                // the seed's residual (column 0); P / X of the seed copy above
+                const double al = seedc[0], be = seedc[1];
+                const double sn = __builtin_fma(be, a.Sv[o0], a.W[o0]);
+                const double rn = __builtin_fma(-al, sn, rv);
+                a.Sv[o0] = sn;
+                a.R[o0] = rn;
+                if (u16) sv[0] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * rn;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMaxNC; ++k) {
+            if (k >= n || (k & 1) != h || !run_s[k] || !in) continue;
+            const int64_t o = k * a.vstride + B.vo + i;
+            const double al = coef[k][0], be = coef[k][1];
+            const double dg = jdiag(a, B, i, a.dshift[k]);
+            const double u = a.R[o] / dg;
+            const double p = __builtin_fma(be, a.P[o], u);
+            const double s = __builtin_fma(be, a.Sv[o], a.W[o]);
+            const double x = __builtin_fma(al, p, a.X[o]);
+            const double rn = __builtin_fma(-al, s, a.R[o]);
+            a.P[o] = p;
+            a.Sv[o] = s;
+            a.X[o] = x;
+            a.R[o] = rn;
+            if (u16) sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rn / dg);
+        }
     }
 #pragma unroll
     for (int k = 0; k < kMaxNC; ++k) sv[k] = wave_sum(sv[k]);
@@ -565,9 +744,9 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
 #pragma unroll
         for (int k = 0; k < kMaxNC; ++k) red[tid >> 6][k] = sv[k];
     __syncthreads();
-    if (tid < nc && run_s[tid]) {
+    if (tid < nc && (B.mshift || run_s[tid])) {
         const int hk = tid & 1;
-        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * nc + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
+        a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * n + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
     }
 }
 

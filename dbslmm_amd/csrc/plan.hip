@@ -2029,12 +2029,16 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     const double esz = p->pcg_g16 ? 2.0 : 8.0;
     for (int b = 0; b < p->n_nonempty; ++b) {
         const int32_t m = p->h_m[b], Tb = (m + kT - 1) / kT, nrun = (Tb + kRun - 1) / kRun;
+        // a block without large SNPs solves n scalar shifts of one matrix: one Krylov sequence
+        // (multi-shift CG, one product column); with large SNPs each copy iterates on its own
+        const bool msh = n > 1 && p->h_ms[b] == m;
+        const int32_t nc = msh ? 1 : n;
         PcgBlk k{b, p->h_row0[b], m, p->h_ms[b], p->h_ld[b], Tb, Tb + nrun, sco, p->h_matoff[b], vo, po, dof,
-                 p->h_off16.empty() ? 0 : p->h_off16[b]};
+                 p->h_off16.empty() ? 0 : p->h_off16[b], nc, msh ? 1 : 0};
         const int bi = static_cast<int>(blk.size());
         blk.push_back(k);
         vo += static_cast<int64_t>(Tb) * kT;
-        po += static_cast<int64_t>(Tb) * k.Ns * n * kT;
+        po += static_cast<int64_t>(Tb) * k.Ns * nc * kT;
         dof += static_cast<int64_t>(Tb) * kNDot * n;
         sco += n;
         for (int I = 0; I < Tb; ++I) {
@@ -2042,9 +2046,9 @@ static int pcg_layout(dbslmm_plan* p, int n) {
             for (int J0 = 0; J0 <= I; J0 += kRun) items.push_back(int4{bi, I, J0, std::min(I, J0 + kRun - 1)});
         }
         bytes += 0.5 * m * (m + 1.0) * esz;
-        flops += 4.0 * n * 0.5 * m * (m + 1.0);
+        flops += 4.0 * nc * 0.5 * m * (m + 1.0);
         // partials written and read once: a column slot per tile (I, J <= I), a row slot per run
-        pbytes += 2.0 * 8.0 * n * kT * (0.5 * Tb * (Tb + 1.0) + Tb * 0.5 * (nrun + 1.0));
+        pbytes += 2.0 * 8.0 * nc * kT * (0.5 * Tb * (Tb + 1.0) + Tb * 0.5 * (nrun + 1.0));
     }
     // biggest blocks' items first (their tile rows are the longest runs of work)
     std::stable_sort(items.begin(), items.end(), [&](const int4& x, const int4& y) { return blk[x.x].Tb > blk[y.x].Tb; });
@@ -2061,7 +2065,7 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     HIP_TRY(ctx, hipMalloc(&p->d_pvec, std::max<int64_t>(1, 5 * n * vo) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_ppart, std::max<int64_t>(1, po) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_pdot, std::max<int64_t>(1, dof) * sizeof(double)));
-    HIP_TRY(ctx, hipMalloc(&p->d_pqs, std::max<int32_t>(1, sco) * 4 * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pqs, std::max<int32_t>(1, sco) * pcg::kQS * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_pcnv, std::max<int32_t>(1, sco) * sizeof(int32_t)));
     HIP_TRY(ctx, hipMalloc(&p->d_pitb, std::max<int32_t>(1, p->n_pblk) * sizeof(int32_t)));
     HIP_TRY(ctx, hipMalloc(&p->d_pdone, std::max<int32_t>(1, p->n_pblk) * sizeof(int32_t)));
@@ -2241,6 +2245,9 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
     a.tol = p->pcg_tol;
     a.inv_sqrt_n = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
     a.ncopy = n;
+    a.seed = 0;                          // the multi-shift seed: the smallest shift (largest sigma)
+    for (int c = 1; c < n; ++c)
+        if (sigmas[c] > sigmas[a.seed]) a.seed = c;
     p->pcg_args = a;
     hipLaunchKernelGGL(dbslmm_pcg_init, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, a, p->d_prow);
     HIP_TRY(ctx, hipGetLastError());

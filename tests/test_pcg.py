@@ -117,8 +117,9 @@ def test_auto_pcg_h2f_matches_factorisation(factors):
 
 
 def test_pcg_repeatable_and_equal_to_single_copy_runs():
-    """Bit-identical across runs, and every copy of a multi-copy run equals a one-copy run of its
-    sigma bit for bit (each block and copy iterates on its own: the multi-device shards rely on it)."""
+    """Bit-identical across runs; every copy of a multi-copy run agrees with a one-copy run of its
+    sigma: bit for bit on blocks with large SNPs (each copy iterates on its own), to the stopping
+    bound on the others (one multi-shift Krylov sequence serves every copy there)."""
     from dbslmm_amd import Context, Plan
     prob = _problem(seed=3, n_ref=384, miss_rate=0.0)
     prob.sigma_s = 0.5 / 5e5           # d = 10 (config 3)
@@ -128,9 +129,18 @@ def test_pcg_repeatable_and_equal_to_single_copy_runs():
     b = plan.run_multi(sig)
     for x, y in zip(a, b):
         assert all(np.array_equal(u, v) for u, v in zip(x, y))
+    nl = np.diff(prob.l_ptr)
     for c, sg in enumerate(sig):
         (one,), _ = _run(prob, [sg])
-        assert np.array_equal(_cat(one), _cat(a[c])) and np.array_equal(one[2], a[c][2]), c
+        assert np.array_equal(one[2], a[c][2])
+        for blk in range(prob.num_block):
+            s0, s1, l0, l1 = prob.s_ptr[blk], prob.s_ptr[blk + 1], prob.l_ptr[blk], prob.l_ptr[blk + 1]
+            g = np.concatenate([a[c][0][s0:s1], a[c][1][l0:l1]])
+            o = np.concatenate([one[0][s0:s1], one[1][l0:l1]])
+            if nl[blk]:
+                assert np.array_equal(g, o), (c, blk)
+            else:
+                assert normwise(g, o) < 1e-11, (c, blk, normwise(g, o))
     plan.close()
 
 
