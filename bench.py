@@ -378,13 +378,13 @@ def predict_leg(args, full, sigmas, m_b, ctx):
     included (~0.1 ms)."""
     import numpy as np
     from dbslmm_amd import Plan
-    from dbslmm_amd.dist import shard_units
+    from dbslmm_amd.dist import shard_units_problem
     K = len(sigmas) if sigmas else 1
     sig = sigmas if sigmas else [full.sigma_s]
     k = 5
     out = {}
     for N in [int(x) for x in args.predict.split(",")]:
-        ud, model = shard_units(m_b, full.n_ref, N, K)
+        ud, model = shard_units_problem(full, sig, N)
         split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
         per = []
         for d in range(N):
@@ -608,7 +608,7 @@ def main():
     cdev = "cuda" if args.dist_backend == "nccl" else "cpu"    # collective tensors
 
     from dbslmm_amd import Context, KERNEL_NAMES, Plan, synth
-    from dbslmm_amd.dist import UnitGather, shard_units
+    from dbslmm_amd.dist import UnitGather, shard_units_problem
 
     def barrier():
         if dist is not None:
@@ -633,17 +633,17 @@ def main():
         full.opts["shard_copies"] = n_copies   # multi-device context: h2f copies may be split
     gather = None
     prob = full
+    sig_run = sigmas if sigmas else [full.sigma_s]
     ctx = Context(devices if in_proc else devices[0])
     if sharded:
         # this rank's (block, h2f copy) units of the library's shard plan (dbslmm_shard_plan),
         # gathered to rank 0 by one RCCL gather per step
-        ud, _ = shard_units(m_b, full.n_ref, world, n_copies)
+        ud, _ = shard_units_problem(full, sig_run, world)
         plan = Plan.units(ctx, full, ud, rank)
         gather = UnitGather(full, ud, device=cdev)
     else:
         plan = Plan(ctx, prob)
     wl = plan.workload()
-    sig_run = sigmas if sigmas else [full.sigma_s]
 
     outs = None
     if sigmas or sharded:   # the caller's result buffers, reused every step (as an application would)
@@ -707,7 +707,7 @@ def main():
 
     n_solve = len(sigmas) if sigmas else 1
     kernels = [kernel_roofline(KERNEL_NAMES[k], float(kms[k]), wl, n_solve) for k in range(len(KERNEL_NAMES))]
-    if n_gpus == 1 and not args.no_isolated:
+    if n_gpus == 1 and not args.no_isolated and not wl.get("pcg_route"):   # (no lead group on PCG)
         # The lead group's unpack, Gram and factorisation overlap the others', so the phase spans
         # above include that contention.  One untimed plan with the lead group off times every
         # phase without it (outside the timed region; reported beside the spans, never as `value`).

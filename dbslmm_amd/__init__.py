@@ -215,6 +215,13 @@ class Plan:
                 "pcg_partial_bytes", "pcg_flops")
         return dict(zip(keys, w.tolist()))
 
+    def block_iters(self) -> np.ndarray:
+        """PCG iterations of each block in the latest run (dbslmm_plan_block_iters; 0: empty block
+        or the factorisation route)."""
+        out = np.zeros(max(1, self.prob.num_block), dtype=np.int32)
+        self.ctx.check(self.ctx.lib.dbslmm_plan_block_iters(self.h, _ptr(out)), "plan_block_iters")
+        return out[:self.prob.num_block]
+
     def shard_info(self) -> np.ndarray:
         """Device index (in the context's device order) solving each block; -1 = empty block."""
         out = np.zeros(self.prob.num_block, dtype=np.int32)

@@ -20,10 +20,11 @@ EXPORTS = (
     "dbslmm_bed_maf", "dbslmm_read_snp_std", "dbslmm_valid_blocks", "dbslmm_plan_variance",
     "dbslmm_ctx_create_multi", "dbslmm_ctx_num_devices", "dbslmm_plan_shard_info",
     "dbslmm_ctx_cache_bed", "dbslmm_ctx_cache_bed_fd", "dbslmm_plan_block_matrix",
-    "dbslmm_shard_plan", "dbslmm_plan_create_units",
+    "dbslmm_shard_plan", "dbslmm_plan_create_units", "dbslmm_shard_plan_problem",
+    "dbslmm_plan_block_iters",
 )
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED, K_TRSV, K_PCG = 0, 1, 2, 3, 4, 5, 6
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv", "dbslmm_pcg")
@@ -108,6 +109,8 @@ def load(path: str | None = None):
     L.dbslmm_ctx_cache_bed_fd.argtypes = [V, C.c_int, C.c_int64, V]
     L.dbslmm_shard_plan.argtypes = [C.c_int32, V, C.c_int32, C.c_int32, C.c_int32, V, V]
     L.dbslmm_plan_create_units.argtypes = [V, P(Problem), C.c_int32, V, C.c_int32, P(V)]
+    L.dbslmm_shard_plan_problem.argtypes = [P(Problem), V, C.c_int32, C.c_int32, V, V]
+    L.dbslmm_plan_block_iters.argtypes = [V, V]
     if hasattr(L, "dbslmm_plan_block_matrix"):   # (tools/race_probe.py loads older builds for A/B)
         L.dbslmm_plan_block_matrix.argtypes = [V, C.c_int32, C.c_int32, V, V]
     if L.dbslmm_abi_version() != ABI_VERSION:

@@ -121,23 +121,48 @@ __device__ __forceinline__ void split_missing(uint32_t x, uint32_t& g, uint32_t&
 //                  1/sd with the N-1 divisor (nomalizeVec), sum of observed dosages.
 //   block_flags    bit 0 set when a slot of the block has a missing call.
 //   slot_list      optional: unpack only these n_slots slots (the plan unpacks its lead group first)
+// A row starts at any byte (3 + pos * bytes_per_snp): lane q of a pass handles the row's 16-B
+// chunk q (64 individuals) from the two aligned 16-B loads covering it (the second only when the
+// row is not 16-B aligned), so a wave issues whole-dwordx4 loads for its row up front, kU chunks
+// per lane, and writes dwordx4 stores.  The image is followed by kBedPad (64) allocated bytes, so
+// the last row's loads stay inside the allocation; bytes past n_ref are masked.
 // ------------------------------------------------------------------------------------------
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4v load_u4(const uint8_t* p) { return *reinterpret_cast<const u4v*>(p); }
+// 16 bytes at byte offset 4 d + bs (d, bs wave-uniform) of the 32-byte pair (x | y)
+__device__ __forceinline__ u4v shift_pair(u4v x, u4v y, int d, int bs) {
+    uint32_t w[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    uint32_t o[5];
+    switch (d) {   // (wave-uniform: a scalar branch, register moves only)
+        case 0: o[0] = w[0]; o[1] = w[1]; o[2] = w[2]; o[3] = w[3]; o[4] = w[4]; break;
+        case 1: o[0] = w[1]; o[1] = w[2]; o[2] = w[3]; o[3] = w[4]; o[4] = w[5]; break;
+        case 2: o[0] = w[2]; o[1] = w[3]; o[2] = w[4]; o[3] = w[5]; o[4] = w[6]; break;
+        default: o[0] = w[3]; o[1] = w[4]; o[2] = w[5]; o[3] = w[6]; o[4] = w[7]; break;
+    }
+    u4v r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = __builtin_amdgcn_alignbyte(o[j + 1], o[j], static_cast<uint32_t>(bs));
+    return r;
+}
+
 extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
     const uint8_t* __restrict__ bed, int32_t n_ref, int64_t bytes_per_snp,
     const int32_t* __restrict__ slot_pos, const int32_t* __restrict__ slot_block, int32_t n_slots,
     uint32_t* __restrict__ Gp, int64_t kpad,
     double* __restrict__ S_out, double* __restrict__ mu_out, double* __restrict__ rsd_out,
     int32_t* __restrict__ block_flags, const int32_t* __restrict__ slot_list) {
+    constexpr int kU = 4;                       // chunks per lane per pass (loads in flight)
     const int lane = threadIdx.x & (kWave - 1);
     const int k = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     if (k >= n_slots) return;
     const int slot = slot_list ? slot_list[k] : k;   // a subset of the slots (n_slots of them)
     const int32_t pos = slot_pos ? slot_pos[slot] : slot;   // (null: slot k reads bed row k)
-    const int64_t n_words = kpad / 16;          // 16 individuals per lane-word
-    uint32_t* grow = Gp ? Gp + static_cast<int64_t>(slot) * n_words : nullptr;
+    const int64_t n_words = kpad / 16;          // 16 individuals per dword (kpad: a multiple of 64)
+    const int nq = static_cast<int>(n_words / 4);           // 16-B chunks of the Gp row
+    u4v* grow = Gp ? reinterpret_cast<u4v*>(Gp + static_cast<int64_t>(slot) * n_words) : nullptr;
     if (pos < 0) {                              // padding slot
         if (grow)
-            for (int64_t w = lane; w < n_words; w += kWave) grow[w] = 0u;
+            for (int q = lane; q < nq; q += kWave) grow[q] = u4v{0u, 0u, 0u, 0u};
         if (lane == 0) {
             if (S_out) S_out[slot] = 0.0;
             if (mu_out) mu_out[slot] = 0.0;
@@ -146,23 +171,46 @@ extern "C" __global__ __launch_bounds__(256) void dbslmm_unpack_stats(
         return;
     }
     const int64_t row_off = 3 + static_cast<int64_t>(pos) * bytes_per_snp;
+    const uint8_t* base = bed + (row_off & ~int64_t(15));
+    const int sh = static_cast<int>(row_off & 15), dsh = sh >> 2, bsh = sh & 3;
+    const int nqd = (n_ref + 63) / 64;          // chunks holding individuals
     int cnt = 0, sum = 0, sq = 0, nmiss = 0;
-    for (int64_t w = lane; w < n_words; w += kWave) {
-        const int64_t first = 16 * w;
-        const int nv = static_cast<int>(min<int64_t>(16, max<int64_t>(0, n_ref - first)));
-        uint32_t word = 0;
-        if (nv > 0) word = load_u32_any(bed, row_off + 4 * w);
-        const uint32_t vmask = nv >= 16 ? 0x55555555u : ((1u << (2 * nv)) - 1u) & 0x55555555u;
-        const uint32_t lo = word & vmask;
-        const uint32_t hi = (word >> 1) & vmask;
-        const int n_miss = __builtin_popcount(lo & ~hi);
-        const int n_two = __builtin_popcount(~lo & ~hi & vmask);
-        const int n_one = __builtin_popcount(~lo & hi);
-        nmiss += n_miss;
-        cnt += __builtin_popcount(vmask) - n_miss;
-        sum += 2 * n_two + n_one;
-        sq += 4 * n_two + n_one;
-        if (grow) grow[w] = dose_code16(word, vmask);
+    for (int q0 = 0; q0 < nq; q0 += kWave * kU) {
+        u4v lo[kU], hi[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int q = q0 + kWave * u + lane;
+            lo[u] = hi[u] = u4v{0u, 0u, 0u, 0u};
+            if (q < nqd) {
+                lo[u] = load_u4(base + 16 * static_cast<int64_t>(q));
+                if (sh) hi[u] = load_u4(base + 16 * static_cast<int64_t>(q) + 16);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int q = q0 + kWave * u + lane;
+            if (q >= nq) break;
+            const u4v wv = sh ? shift_pair(lo[u], hi[u], dsh, bsh) : lo[u];
+            u4v g;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int first = 64 * q + 16 * j;
+                const int nv = min(16, max(0, n_ref - first));
+                const uint32_t vmask = nv >= 16 ? 0x55555555u : ((1u << (2 * nv)) - 1u) & 0x55555555u;
+                const uint32_t word = wv[j];
+                const uint32_t lo2 = word & vmask;
+                const uint32_t hi2 = (word >> 1) & vmask;
+                const int n_miss = __builtin_popcount(lo2 & ~hi2);
+                const int n_two = __builtin_popcount(~lo2 & ~hi2 & vmask);
+                const int n_one = __builtin_popcount(~lo2 & hi2);
+                nmiss += n_miss;
+                cnt += __builtin_popcount(vmask) - n_miss;
+                sum += 2 * n_two + n_one;
+                sq += 4 * n_two + n_one;
+                g[j] = dose_code16(word, vmask);
+            }
+            if (grow) grow[q] = g;
+        }
     }
     cnt = wave_sum_i32(cnt);
     sum = wave_sum_i32(sum);

@@ -226,7 +226,130 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
     }
     for (int d = 0; d < G; ++d) dev_ms[d] = dev[d].time();
 }
+
+// ---------------------------------------------------------------- time model, PCG route
+// On the PCG route (pcg.hip) a device runs ONE sequence: unpack + Gram of its blocks, then
+// iterations in which every block still iterating streams its lower-triangle matrix once (product,
+// one wave per run of 128 x 128 tiles) and reduces its tile rows (rows + update) -- blocks never
+// wait on each other, so a device's step is its summed work plus a floor per iteration (three
+// dependent launches) and per run; the largest block alone (~1 ms at 9.7k SNPs) stays far below
+// the step, so no block needs splitting.  Rates: the round-6 one-GPU kernel trace of configs 3-5
+// (profiles/r06/cal: per-kernel average over 8 runs, per-block iteration counts from
+// dbslmm_plan_block_iters), DESIGN.md section 6.
+constexpr double kPcgGramOpsHuge = 3.0e15;   // dbslmm_gram_huge (FP4 MFMA, uint16 epilogue), ops/s
+constexpr double kPcgGramOpsBig = 1.9e15;    // dbslmm_gram_big / _i8
+constexpr double kPcgTileNs = 7.2;           // product: ns per 128 x 128 tile per iteration
+constexpr double kPcgRowNs = 12.0;           // rows + update: ns per tile row and copy column per iteration
+constexpr double kPcgIterFloorUs = 15.0;     // three launches per iteration on an idle device
+constexpr double kPcgRunMs = 0.10;           // per run: memsets, init, final, status read-back
+constexpr double kPcgDownloadMsPerM = 0.2;   // per million (SNP, copy) results downloaded
+
+// a priori iterations of a block: CG's bound at kappa = 1 + 12 / (d + 1 - tau) (pcg_first_chunk),
+// outlying eigenvalues of large SNPs + 2
+static int pcg_iters_model(double dmin, double tau, double tol, bool large) {
+    const double kap = 1.0 + 12.0 / std::max(1e-3, dmin + 1.0 - tau);
+    const double q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
+    return static_cast<int>(std::ceil(std::log(2.0 / tol) / -std::log(q))) + (large ? 2 : 0);
+}
+
+struct PcgCost {
+    double ms = 0.0;      // the block's share of a device step
+    int iters = 0;
+    double results = 0.0;
+};
+static PcgCost pcg_block_cost(double m, double ml, double n_ref, int copies, int iters) {
+    PcgCost c;
+    if (m <= 0) return c;
+    const double kp = std::ceil(n_ref / 128.0) * 128.0;
+    const double unpack = m * (std::ceil(n_ref / 4.0) + kp / 4.0) / kUnpackBps * 1e3;
+    const double huge_min = kp >= 4096 ? 384.0 : 768.0;
+    const double gram = n_ref * m * (m + 1.0) / (m >= huge_min ? kPcgGramOpsHuge : kPcgGramOpsBig) * 1e3;
+    const double Tb = std::ceil(m / 128.0);
+    const int nc = (copies > 1 && ml > 0) ? copies : 1;   // multi-shift: one column without large SNPs
+    c.iters = iters;
+    c.ms = unpack + gram + iters * (Tb * (Tb + 1.0) / 2.0 * kPcgTileNs + Tb * nc * kPcgRowNs) * 1e-6;
+    c.results = m * copies;
+    return c;
+}
+
+// Whole blocks -> devices, longest first onto the least-loaded device.  dev_ms[d] = summed work +
+// the iteration floor of its slowest block + per-run costs.
+static void plan_units_pcg(int32_t nb, const int32_t* m, const int32_t* ml, int32_t n_ref, int32_t G, int32_t K,
+                           const std::vector<int>& iters, std::vector<int32_t>& unit_device,
+                           std::vector<double>& dev_ms) {
+    K = std::max(1, K);
+    unit_device.assign(static_cast<size_t>(nb) * K, -1);
+    std::vector<PcgCost> cost(nb);
+    std::vector<int32_t> order;
+    for (int b = 0; b < nb; ++b) {
+        cost[b] = pcg_block_cost(m[b], ml ? ml[b] : 0, n_ref, K, iters[b]);
+        if (m[b] > 0) order.push_back(b);
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cost[x].ms > cost[y].ms; });
+    std::vector<double> load(G, 0.0), res(G, 0.0);
+    std::vector<int> itmax(G, 0);
+    for (int32_t b : order) {
+        const int d = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+        load[d] += cost[b].ms;
+        res[d] += cost[b].results;
+        itmax[d] = std::max(itmax[d], cost[b].iters);
+        for (int c = 0; c < K; ++c) unit_device[static_cast<size_t>(b) * K + c] = d;
+    }
+    dev_ms.assign(G, 0.0);
+    for (int d = 0; d < G; ++d)
+        dev_ms[d] = load[d] > 0 ? load[d] + itmax[d] * kPcgIterFloorUs * 1e-3 + kPcgRunMs + kPcgDownloadMsPerM * res[d] * 1e-6
+                                : 0.0;
+}
 }  // namespace shard
+
+// Does a plan of this problem take the PCG route for these sigmas?  (plan.hip pcg_route at the
+// problem level: the same options, tau, large-SNP and prior-shift rules.)
+static bool problem_pcg_route(const dbslmm_problem* pr, const double* sig, int n, bool has_large) {
+    const dbslmm_options* o = pr->opts;
+    const int solver = o ? o->solver : 0;
+    if (solver == 1 || (o && o->debug_stop) || n < 1) return false;
+    if (n > pcg::kMaxNC || !(pr->tau > 0.0 && pr->tau <= 1.0) || (pr->tau >= 1.0 && has_large)) return false;
+    if (solver == 2) return true;
+    for (int c = 0; c < n; ++c)
+        if (1.0 / (sig[c] * static_cast<double>(pr->n_obs)) < kPcgDmin) return false;
+    return true;
+}
+
+// The shard plan of a problem: the PCG model when its runs take the PCG route, else the
+// factorisation model (shard::plan_units).  m / ml: SNPs / large SNPs per block.
+static void plan_problem(const dbslmm_problem* pr, const double* sig, int n, int32_t G,
+                         const std::vector<int32_t>& m, const std::vector<int32_t>& ml,
+                         std::vector<int32_t>& ud, std::vector<double>& dev_ms) {
+    bool has_large = false;
+    for (int32_t x : ml) has_large |= x > 0;
+    if (!problem_pcg_route(pr, sig, n, has_large)) {
+        shard::plan_units(pr->num_block, m.data(), pr->n_ref, G, n, ud, dev_ms);
+        return;
+    }
+    double dmin = INFINITY;
+    for (int c = 0; c < n; ++c) dmin = std::min(dmin, 1.0 / (sig[c] * static_cast<double>(pr->n_obs)));
+    const double tol = pr->opts && pr->opts->pcg_tol > 0.0 ? std::max(1e-15, pr->opts->pcg_tol) : 1e-12;
+    std::vector<int> it(pr->num_block);
+    for (int b = 0; b < pr->num_block; ++b) it[b] = shard::pcg_iters_model(dmin, pr->tau, tol, ml[b] > 0);
+    shard::plan_units_pcg(pr->num_block, m.data(), ml.data(), pr->n_ref, G, n, it, ud, dev_ms);
+}
+
+// SNPs and large SNPs per block of a problem (checked CSR offsets)
+static int block_sizes(dbslmm_ctx* ctx, const dbslmm_problem* pr, std::vector<int32_t>& m, std::vector<int32_t>& ml) {
+    const bool has_l = pr->l_ptr != nullptr;
+    m.assign(pr->num_block, 0);
+    ml.assign(pr->num_block, 0);
+    for (int b = 0; b < pr->num_block; ++b) {
+        const int64_t ms = pr->s_ptr[b + 1] - pr->s_ptr[b], l = has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0;
+        if (ms < 0 || l < 0) {
+            if (ctx) ctx->err = "CSR offsets not monotone";
+            return DBSLMM_E_ARG;
+        }
+        m[b] = static_cast<int32_t>(ms + l);
+        ml[b] = static_cast<int32_t>(l);
+    }
+    return DBSLMM_OK;
+}
 
 // ---------------------------------------------------------------- jobs
 // Run f(i) for every job index on its own host thread; the first failing rc wins and its job's
@@ -390,19 +513,16 @@ static int mp_build(dbslmm_ctx* ctx, const dbslmm_problem* pr, int32_t K, const 
 
 static int mp_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** out) {
     ARG_CHECK(ctx, pr && out && pr->s_ptr && pr->num_block >= 0, "null problem/out");
-    const bool has_l = pr->l_ptr != nullptr;
-    std::vector<int32_t> m(pr->num_block);
-    for (int b = 0; b < pr->num_block; ++b) {
-        const int64_t ms = pr->s_ptr[b + 1] - pr->s_ptr[b], ml = has_l ? pr->l_ptr[b + 1] - pr->l_ptr[b] : 0;
-        ARG_CHECK(ctx, ms >= 0 && ml >= 0, "CSR offsets not monotone");
-        m[b] = static_cast<int32_t>(ms + ml);
-    }
+    std::vector<int32_t> m, ml;
+    if (const int rc = block_sizes(ctx, pr, m, ml)) return rc;
     const int G = static_cast<int>(ctx->subs.size());
     const int32_t K = pr->opts && pr->opts->shard_copies > 1 ? pr->opts->shard_copies : 1;
     ARG_CHECK(ctx, K <= 64, "shard_copies must be <= 64");
+    // the route is decided per run from its sigmas; the plan assumes K copies at the problem's sigma_s
+    std::vector<double> sig(K, pr->sigma_s);
     std::vector<int32_t> ud;
     std::vector<double> dev_ms;
-    shard::plan_units(pr->num_block, m.data(), pr->n_ref, G, K, ud, dev_ms);
+    plan_problem(pr, sig.data(), K, G, m, ml, ud, dev_ms);
     std::vector<int> devs(G);
     std::iota(devs.begin(), devs.end(), 0);
     return mp_build(ctx, pr, K, ud, devs, ctx->subs, false, out);
@@ -520,6 +640,25 @@ static int mp_sync(dbslmm_plan* p) {
     return fan_out(p, [&](int d) -> int { return S[d].run_copies.empty() ? DBSLMM_OK : dbslmm_plan_sync(S[d].plan); });
 }
 
+// per-block PCG iterations of the latest run, from every job (a block's max over its jobs)
+static int mp_block_iters(dbslmm_plan* p, int32_t* iters) {
+    auto& S = p->mp->shards;
+    if (!p->mp->partial) std::fill(iters, iters + p->num_block, 0);
+    std::vector<std::vector<int32_t>> sub(S.size());
+    const int rc = fan_out(p, [&](int j) -> int {
+        if (S[j].run_copies.empty()) return DBSLMM_OK;
+        sub[j].assign(std::max<size_t>(1, S[j].blocks.size()), 0);
+        return dbslmm_plan_block_iters(S[j].plan, sub[j].data());
+    });
+    if (rc != DBSLMM_OK) return rc;
+    for (size_t j = 0; j < S.size(); ++j)
+        for (size_t i = 0; i < S[j].blocks.size() && i < sub[j].size(); ++i) {
+            int32_t& o = iters[S[j].blocks[i]];
+            o = std::max(o, sub[j][i]);
+        }
+    return DBSLMM_OK;
+}
+
 static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diags, int32_t* n_test_out) {
     dbslmm_ctx* ctx = p->ctx;
     ARG_CHECK(ctx, tp && tp->indicator && tp->n_total > 0, "bad test panel");
@@ -633,6 +772,23 @@ int dbslmm_shard_plan(int32_t num_block, const int32_t* m, int32_t n_ref, int32_
     std::vector<int32_t> ud;
     std::vector<double> ms;
     shard::plan_units(num_block, m, n_ref, n_dev, n_copies, ud, ms);
+    std::copy(ud.begin(), ud.end(), unit_device);
+    if (dev_ms) std::copy(ms.begin(), ms.end(), dev_ms);
+    return DBSLMM_OK;
+}
+
+int dbslmm_shard_plan_problem(const dbslmm_problem* pr, const double* sigma_s, int32_t n_sigma, int32_t n_dev,
+                              int32_t* unit_device, double* dev_ms) {
+    if (!pr || !pr->s_ptr || pr->num_block < 0 || !sigma_s || n_sigma < 1 || n_sigma > 64 || n_dev <= 0 ||
+        !unit_device || pr->n_ref <= 1 || pr->n_obs <= 0)
+        return DBSLMM_E_ARG;
+    for (int c = 0; c < n_sigma; ++c)
+        if (!(sigma_s[c] > 0.0)) return DBSLMM_E_ARG;
+    std::vector<int32_t> m, ml;
+    if (const int rc = block_sizes(nullptr, pr, m, ml)) return rc;
+    std::vector<int32_t> ud;
+    std::vector<double> ms;
+    plan_problem(pr, sigma_s, n_sigma, n_dev, m, ml, ud, ms);
     std::copy(ud.begin(), ud.end(), unit_device);
     if (dev_ms) std::copy(ms.begin(), ms.end(), dev_ms);
     return DBSLMM_OK;

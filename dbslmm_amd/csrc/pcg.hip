@@ -278,38 +278,6 @@ __device__ __forceinline__ void stage_v(const PcgArgs& a, const PcgBlk& B, bool 
     }
 }
 
-// the same in two halves, so a tile column's vector loads can be issued ahead of the next
-// quadrant's row segments (vmcnt counts in issue order: waiting for loads issued after the
-// prefetch would drain it)
-struct StageRegs {
-    double r[kMaxNC][2], s[2];
-};
-__device__ __forceinline__ void stage_load(const PcgArgs& a, const PcgBlk& B, bool u16, int T, int nc, int lane,
-                                           StageRegs& g) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int i = T * kT + lane + 64 * h;
-        const bool in = i < B.m;
-        g.s[h] = in && u16 ? a.rsd[B.row0 + i] : 1.0;
-#pragma unroll
-        for (int k = 0; k < kMaxNC; ++k)
-            g.r[k][h] = k < nc && in ? a.R[k * a.vstride + B.vo + i] : 0.0;
-    }
-}
-__device__ __forceinline__ void stage_store(const PcgArgs& a, const PcgBlk& B, int T, int nc, int lane,
-                                            const StageRegs& g, double* v) {
-#pragma unroll
-    for (int k = 0; k < kMaxNC; ++k) {
-        if (k >= nc) break;
-        const double dc = col_shift(a, B, k);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int rr = lane + 64 * h, i = T * kT + rr;
-            v[k * kVS + rr] = g.r[k][h] / jdiag(a, B, i, dc) * g.s[h];
-        }
-    }
-}
-
 // One symv item on one wave.  LDS (wave-private): vI = rsd o u of the item's tile row, vJ[2] = the
 // same of the current and the next tile column ([copy][kVS] each), rsum / csum = the
 // reduce-scattered row results of the run and column results of the current tile
@@ -379,17 +347,16 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     if (J != I) stage_v(a, B, u16, J, nc, lane, vj_of(J));
     for (int t = 0; t < 2 * nc; ++t) rsum[t * 64 + lane] = csum[t * 64 + lane] = 0.0;
     wave_fence();
-    // one pipeline step: prefetch the next quadrant into `nxt` (and, at a tile change, the next
-    // column vector: its loads first, so waiting for them leaves the row segments in flight),
-    // multiply the current one from `cur`; false when the item is done
+    // one pipeline step: prefetch the next quadrant into `nxt` (and its column vector at a tile
+    // change), multiply the current one from `cur`; false when the item is done.  (Issuing the
+    // column vector's loads before the quadrant's was measured slower: 290 vs 257 us at config 4.)
     auto step = [&](pcg_u4 (&cur)[8], pcg_u4 (&nxt)[8]) -> bool {
         int Jn = J, qn = q;
         const bool more = next_quad(B, I, J1, Jn, qn);
-        const bool newcol = more && Jn != J && Jn != I;
-        StageRegs sg;
-        if (newcol) stage_load(a, B, u16, Jn, nc, lane, sg);
-        if (more) load(Jn, qn, nxt);
-        if (newcol) stage_store(a, B, Jn, nc, lane, sg, vj_of(Jn));
+        if (more) {
+            load(Jn, qn, nxt);
+            if (Jn != J && Jn != I) stage_v(a, B, u16, Jn, nc, lane, vj_of(Jn));
+        }
         mult(J, q, cur);
         if (!more || Jn != J) flush(J);
         wave_fence();                        // the next column vector is in LDS before its use

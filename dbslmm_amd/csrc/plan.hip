@@ -58,6 +58,7 @@ constexpr int kTiledMinDefault = 384;   // blocks with m >= this take the multi-
                                         // 44.1-44.3 -> 43.2-43.3 ms, one run in four 45.0; configs
                                         // 3 / 5 -0.1 / -0.2 ms; 512 before, 320 no better)
 constexpr int kTiledMinSmall = 256;     // the same when no block reaches 512 SNPs (config 2)
+constexpr int kBedPad = 64;            // zero bytes after every device .bed image (the unpack reads whole 16-B chunks)
 constexpr int kGramBigMinDefault = 96;  // blocks with m >= this take the 128 x 128 Gram kernel
 constexpr int kGramHugeMinDefault = 384; // ... and the 256 x 256 one from here (swept: configs 3, 5)
 constexpr int kTChebMaxM = 4096;         // whole-block Chebyshev passes: blocks of <= 64 tiles
@@ -316,6 +317,7 @@ static int mp_download(dbslmm_plan* p, int copy, double* beta_s, double* beta_l,
 static int mp_download_all(dbslmm_plan* p, int n, double* beta_s, double* beta_l, int32_t* block_status);
 static int mp_run(dbslmm_plan* p, const double* sigmas, int n, bool wait);
 static int mp_sync(dbslmm_plan* p);
+static int mp_block_iters(dbslmm_plan* p, int32_t* iters);
 static int mp_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* diags, int32_t* n_test_out);
 static int mp_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int32_t n_ref, int64_t n_snp, double* maf);
 // context-level tools on a multi-device context run on its first device
@@ -462,9 +464,9 @@ static void par_memcpy(void* dst, const void* src, size_t n) {
 }
 
 // The .bed image on the device: a device-to-device copy of the context's cached image when the
-// caller passes the same host range, else a staged upload.  dst holds bed_len + 16 bytes (zero pad).
+// caller passes the same host range, else a staged upload.  dst holds bed_len + kBedPad bytes (zero pad).
 static hipError_t bed_to_device(dbslmm_ctx* ctx, uint8_t* dst, const uint8_t* bed, int64_t bed_len) {
-    hipError_t e = hipMemsetAsync(dst + bed_len, 0, 16, ctx->stream);
+    hipError_t e = hipMemsetAsync(dst + bed_len, 0, kBedPad, ctx->stream);
     if (e != hipSuccess) return e;
     if (ctx->d_bed_cache && bed == ctx->bed_host && bed_len == ctx->bed_host_len) {
         e = hipMemcpyAsync(dst, ctx->d_bed_cache, bed_len, hipMemcpyDeviceToDevice, ctx->stream);
@@ -797,13 +799,13 @@ int dbslmm_ctx_cache_bed(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len) {
     ctx->bed_host_len = 0;
     if (!bed) return DBSLMM_OK;
     uint8_t* d = nullptr;
-    HIP_TRY(ctx, hipMalloc(&d, bed_len + 16));
+    HIP_TRY(ctx, hipMalloc(&d, bed_len + kBedPad));
     const int dev = ctx->device;
     ctx->bed_cache = std::shared_ptr<uint8_t>(d, [dev](uint8_t* q) {
         (void)hipSetDevice(dev);
         (void)hipFree(q);
     });
-    HIP_TRY(ctx, hipMemsetAsync(d + bed_len, 0, 16, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(d + bed_len, 0, kBedPad, ctx->stream));
     HIP_TRY(ctx, upload_staged(d, bed, bed_len, ctx->stream));
     ctx->d_bed_cache = d;
     ctx->bed_host = bed;
@@ -821,13 +823,13 @@ int dbslmm_ctx_cache_bed_fd(dbslmm_ctx* ctx, int fd, int64_t bed_len, const uint
     ctx->bed_host = nullptr;
     ctx->bed_host_len = 0;
     uint8_t* d = nullptr;
-    HIP_TRY(ctx, hipMalloc(&d, bed_len + 16));
+    HIP_TRY(ctx, hipMalloc(&d, bed_len + kBedPad));
     const int dev = ctx->device;
     ctx->bed_cache = std::shared_ptr<uint8_t>(d, [dev](uint8_t* q) {
         (void)hipSetDevice(dev);
         (void)hipFree(q);
     });
-    HIP_TRY(ctx, hipMemsetAsync(d + bed_len, 0, 16, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(d + bed_len, 0, kBedPad, ctx->stream));
     if (upload_staged_fd(d, fd, static_cast<size_t>(bed_len), ctx->stream) != hipSuccess) {
         ctx->bed_cache.reset();
         ctx->err = "reading / uploading the .bed from its file descriptor failed";
@@ -1284,7 +1286,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
         p->bed_shared = ctx->bed_cache;          // read-only: the cached image itself, no copy
         p->d_bed = p->bed_shared.get();
     } else {
-        if ((e = hipMalloc(&p->d_bed, pr->bed_len + 16)) != hipSuccess) return fail("hipMalloc bed");
+        if ((e = hipMalloc(&p->d_bed, pr->bed_len + kBedPad)) != hipSuccess) return fail("hipMalloc bed");
         if ((e = bed_to_device(ctx, p->d_bed, pr->bed, pr->bed_len)) != hipSuccess) return fail("upload bed");
     }
     // + kHT spare rows: a 256-row Gram tile may read past the last slot (results discarded)
@@ -2737,6 +2739,18 @@ extern "C" int dbslmm_diag_trsv_stamps(dbslmm_plan* p, unsigned long long* out, 
 }
 #endif
 
+int dbslmm_plan_block_iters(dbslmm_plan* p, int32_t* iters) {
+    if (!p || !iters) return DBSLMM_E_ARG;
+    if (p->mp) return mp_block_iters(p, iters);
+    HIP_TRY(p->ctx, hipSetDevice(p->ctx->device));
+    if (const int rc = pcg_finish(p)) return rc;
+    HIP_TRY(p->ctx, hipStreamSynchronize(p->ctx->stream));
+    std::fill(iters, iters + p->num_block, 0);
+    if (!p->pcg_ran) return DBSLMM_OK;
+    for (int b = 0; b < p->n_pblk; ++b) iters[p->h_blk_id[b]] = p->h_pmon[1 + b];
+    return DBSLMM_OK;
+}
+
 int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     if (!p || !out) return DBSLMM_E_ARG;
     if (p->mp) {   // sums over the jobs; [12] launches, [14] iterations: the max; [15] job 0's;
@@ -2896,8 +2910,8 @@ int dbslmm_plan_variance(dbslmm_plan* p, const dbslmm_test_panel* tp, double* di
     std::lock_guard<std::mutex> lk(g_capture_mu);
     do {
         hipError_t e;
-        if ((e = hipMalloc(&d_tbed, tp->bed_len + 16)) != hipSuccess ||
-            (e = hipMemsetAsync(d_tbed, 0, tp->bed_len + 16, st)) != hipSuccess ||
+        if ((e = hipMalloc(&d_tbed, tp->bed_len + kBedPad)) != hipSuccess ||
+            (e = hipMemsetAsync(d_tbed, 0, tp->bed_len + kBedPad, st)) != hipSuccess ||
             (e = upload_staged(d_tbed, tp->bed, tp->bed_len, st)) != hipSuccess ||
             (e = dev_upload(&d_tpos, tpos, ctx->stream)) != hipSuccess || (e = dev_upload(&d_sel, sel, ctx->stream)) != hipSuccess ||
             (e = dev_upload(&d_cpos, cpos, ctx->stream)) != hipSuccess ||
@@ -2953,7 +2967,7 @@ int dbslmm_bed_maf(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, int32_t
         hipError_t e;
         const bool cached = ctx->d_bed_cache && bed == ctx->bed_host && bed_len == ctx->bed_host_len;
         const size_t nd = static_cast<size_t>(n_snp) * sizeof(double);
-        if ((!cached && ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
+        if ((!cached && ((e = hipMalloc(&d_bed, bed_len + kBedPad)) != hipSuccess ||
                          (e = bed_to_device(ctx, d_bed, bed, bed_len)) != hipSuccess)) ||
             (e = hipMalloc(&d_work, 3 * nd + n_snp * sizeof(int32_t))) != hipSuccess ||
             (e = hipMemsetAsync(d_work + 3 * nd, 0, n_snp * sizeof(int32_t), ctx->stream)) != hipSuccess) {
@@ -3004,8 +3018,8 @@ int dbslmm_read_snp_std(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
     int rc = DBSLMM_OK;
     do {
         hipError_t e;
-        if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
-            (e = hipMemsetAsync(d_bed, 0, bed_len + 16, ctx->stream)) != hipSuccess ||
+        if ((e = hipMalloc(&d_bed, bed_len + kBedPad)) != hipSuccess ||
+            (e = hipMemsetAsync(d_bed, 0, bed_len + kBedPad, ctx->stream)) != hipSuccess ||
             (e = upload_staged(d_bed, bed, bed_len, ctx->stream)) != hipSuccess ||
             (e = dev_upload(&d_pos, hp, ctx->stream)) != hipSuccess ||
             (e = hipMalloc(&d_mu, n_rows * sizeof(double))) != hipSuccess ||
@@ -3076,8 +3090,8 @@ int dbslmm_valid_blocks(dbslmm_ctx* ctx, const uint8_t* bed, int64_t bed_len, in
     int rc = DBSLMM_OK;
     do {
         hipError_t e;
-        if ((e = hipMalloc(&d_bed, bed_len + 16)) != hipSuccess ||
-            (e = hipMemsetAsync(d_bed, 0, bed_len + 16, ctx->stream)) != hipSuccess ||
+        if ((e = hipMalloc(&d_bed, bed_len + kBedPad)) != hipSuccess ||
+            (e = hipMemsetAsync(d_bed, 0, bed_len + kBedPad, ctx->stream)) != hipSuccess ||
             (e = upload_staged(d_bed, bed, bed_len, ctx->stream)) != hipSuccess ||
             (e = dev_upload(&d_pos, hp, ctx->stream)) != hipSuccess || (e = dev_upload(&d_ptr, hptr, ctx->stream)) != hipSuccess ||
             (e = dev_upload(&d_z1, hz, ctx->stream)) != hipSuccess ||

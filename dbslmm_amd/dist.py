@@ -46,6 +46,24 @@ def shard_units(m_per_block, n_ref: int, world: int, n_copies: int = 1):
     return ud, ms
 
 
+def shard_units_problem(prob, sigmas, world: int):
+    """The route-aware shard plan of a problem (dbslmm_shard_plan_problem; host only,
+    deterministic): on the PCG route every block whole on one device by the PCG time model, on
+    the factorisation route shard_units' plan.  Returns unit_device [num_block, len(sigmas)] and
+    the model's predicted step of every device in ms."""
+    from . import _lib
+    L = _lib.load()
+    sig = np.ascontiguousarray(sigmas, dtype=np.float64).reshape(-1)
+    ud = np.zeros((prob.num_block, sig.size), dtype=np.int32)
+    ms = np.zeros(world, dtype=np.float64)
+    cs = prob.c_struct()
+    rc = L.dbslmm_shard_plan_problem(C.byref(cs), sig.ctypes.data_as(C.c_void_p), sig.size, int(world),
+                                     ud.ctypes.data_as(C.c_void_p), ms.ctypes.data_as(C.c_void_p))
+    if rc != 0:
+        raise _lib.DbslmmError(f"dbslmm_shard_plan_problem failed rc={rc}")
+    return ud, ms
+
+
 def shard_blocks(m_per_block: np.ndarray, n_ref: int, world: int) -> list[np.ndarray]:
     """Single-solve shard plan: the blocks of each rank (block order)."""
     ud, _ = shard_units(m_per_block, n_ref, world, 1)

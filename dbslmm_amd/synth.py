@@ -123,14 +123,15 @@ def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), se
              large_z: float = 8.0, n_obs: int = 100000, h2: float = 0.5,
              block_limit: int | None = None, engine: str = "numpy", device: int = 0) -> SynthPanel:
     """engine "numpy" (CPU, used by the parity fixtures) or "gpu" (libdbslmm_synth.so, same model
-    with a counter-hash RNG; for the 500k-1M SNP scale configs)."""
+    with a counter-hash RNG; for the 500k-1M SNP scale configs); "none": the "gpu" panel's blocks,
+    z-scores and large SNPs without genotypes (zero .bed rows, never touched: shard-plan tests)."""
     rng = np.random.default_rng(seed)
     blocks, chrom, ps, blk = _layout(m_total, pop, chroms, rng, block_limit)
     m = len(ps)
     af = rng.uniform(0.05, 0.5, size=m)
     thr = ndtri(af).astype(np.float32)
     nb = (n_ref + 3) // 4
-    bed = np.empty(3 + m * nb, dtype=np.uint8)
+    bed = (np.zeros if engine == "none" else np.empty)(3 + m * nb, dtype=np.uint8)
     bed[:3] = np.frombuffer(BED_MAGIC, dtype=np.uint8)
     rows = bed[3:].reshape(m, nb)
     a = np.float32(math.sqrt(1.0 - rho * rho))
@@ -141,6 +142,8 @@ def simulate(m_total: int, n_ref: int, pop: str = "EUR", chroms=range(1, 23), se
     chunk = 4096
     if engine == "gpu":
         _gpu_rows(rows, starts, ends, thr, n_ref, seed, rho, miss_rate, device)
+        starts = ends = []
+    elif engine == "none":
         starts = ends = []
     elif engine != "numpy":
         raise ValueError(f"engine {engine!r}")

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 12
+#define DBSLMM_ABI_VERSION 13
 
 enum {
     DBSLMM_OK = 0,
@@ -241,6 +241,16 @@ int dbslmm_ctx_create_multi(int32_t n_dev, const int32_t* device_ids, dbslmm_ctx
  * OpenMP schedule(dynamic) over blocks (scr/dbslmmfit.cpp:189-220). */
 int dbslmm_shard_plan(int32_t num_block, const int32_t* m, int32_t n_ref, int32_t n_dev, int32_t n_copies,
                       int32_t* unit_device, double* dev_ms);
+/* Shard plan of a problem (ABI 13): as dbslmm_shard_plan, for the route the problem's plans take
+ * with these n_sigma sigmas (dbslmm_options.solver and the prior shift, as dbslmm_plan_run_multi
+ * decides).  Factorisation route: dbslmm_shard_plan's model and units.  PCG route: whole blocks
+ * only (every copy of a block on one device: one Krylov sequence serves the copies of a block
+ * without large SNPs), longest first onto the least-loaded device by the PCG model (unpack + Gram
+ * at the measured kernel rates, then per iteration the block's tiles and tile rows; a priori
+ * iteration counts).  Outputs as dbslmm_shard_plan, n_copies = n_sigma.
+ * Host-only; deterministic. */
+int dbslmm_shard_plan_problem(const dbslmm_problem* p, const double* sigma_s, int32_t n_sigma, int32_t n_dev,
+                              int32_t* unit_device, double* dev_ms);
 /* A plan over ONE device's units of a shard plan (ABI 10), on a single-device context: the same
  * problem as dbslmm_plan_create (the whole .bed image and CSR arrays), solving only the units with
  * unit_device[b * n_copies + c] == device_index (its split units -- all of one h2f copy -- as one
@@ -323,6 +333,10 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * [21] the product's fp64 flops per iteration (2 per stored element and copy, both directions). */
 #define DBSLMM_WORKLOAD_LEN 22
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
+/* PCG iterations of each block in the latest run (ABI 13): iters[b] (num_block entries) = the
+ * iterations block b ran before its every copy met the stopping rule (pcg_maxit at the cap), 0 for
+ * empty blocks and after a run on the factorisation route.  Waits for the run. */
+int dbslmm_plan_block_iters(dbslmm_plan* plan, int32_t* iters);
 
 /* Diagnostics (parity tests): after plan_sync, the working matrix of block `block` (original
  * block id) in factorisation copy `copy`: ld x ld fp64, row-major, ld = *ld_out (out == NULL:

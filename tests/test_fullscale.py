@@ -5,10 +5,12 @@ block by block with the oracle's direct fp64 solve of the reference equations
 (scr/dbslmmfit.cpp:680-770; oracle/ref_numpy.py est_block_*_sigma, Cholesky on all host cores):
 
 * every block with m >= 2000 SNPs -- this includes the largest EUR block (~9.6k SNPs at 1M) and
-  the largest AFR block (~11.7k), i.e. the tiled sequence's long-chain regime (>= 37 super steps,
-  ~150-tile substitution chains) at n_ref = 10k, and for config 4 the Chebyshev h2f copies on
-  those blocks: normwise max|dbeta| / max|beta| <= 1e-10 per block (the Chebyshev-iterated h2f
-  copies: <= cheb_tol, CHEB_TOL), every h2f factor;
+  the largest AFR block (~11.7k): normwise max|dbeta| / max|beta| <= 1e-10 per block and h2f
+  copy.  By default these configs take the PCG route (dbslmm_options.solver = 0: the prior shift
+  d = 1/(sigma_s n) >= 2 keeps every block well conditioned), whose stopping rule bounds each
+  copy's relative error by pcg_tol = 1e-12; "4-factor" forces the factorisation route (the tiled
+  sequence's long-chain regime, >= 37 super steps, ~150-tile substitution chains, and the h2f
+  copies iterated on the base factor: those copies <= cheb_tol, CHEB_TOL);
 * the same blocks against the reference-faithful Jacobi-PCG (abs. tol 1e-7, :629-678): <= 1e-5;
 * a random sample of the smaller blocks through the C oracle (direct): <= 1e-10;
 * every block: status OK and beta finite.
@@ -84,7 +86,8 @@ def _diagnose(prob, b, sg, thr, devices=0):
     standardised Gram, then -- from a fresh full run -- the factor L (strict lower triangle and the
     stored 1 / L_ii), y = L^-1 z (row m) and beta, each against NumPy's Cholesky of the reference
     matrix (scr/dbslmmfit.cpp:697-729 restated as one joint solve).  Returns a dict
-    of normwise differences (phases of a block below the tiled threshold: Sigma and beta only)."""
+    of normwise differences (phases of a block below the tiled threshold: Sigma and beta only).
+    Runs the factorisation route (solver = 1): its beta is that route's, beside the failing one."""
     from scipy.linalg import solve_triangular
     from dbslmm_amd import Context, Plan
     s0, s1 = int(prob.s_ptr[b]), int(prob.s_ptr[b + 1])
@@ -109,14 +112,14 @@ def _diagnose(prob, b, sg, thr, devices=0):
     sigma0 = prob.sigma_s
     out = {}
     try:
-        prob.opts = dict(opts0, debug_stop=1)
+        prob.opts = dict(opts0, debug_stop=1, solver=1)
         plan = Plan(Context(devices), prob)
         plan.run()
         A = plan.block_matrix(b)
         plan.close()
         lo = np.tril_indices(m)
         out["sigma"] = float(np.max(np.abs(A[:m, :m][lo] - S[lo])) / np.max(np.abs(S)))
-        prob.opts = opts0
+        prob.opts = dict(opts0, solver=1)
         prob.sigma_s = sg
         plan = Plan(Context(devices), prob)
         plan.run()
@@ -149,29 +152,37 @@ def _got(prob, res, b):
     return np.concatenate([s, bl[prob.l_ptr[b]:prob.l_ptr[b + 1]]])
 
 
-@pytest.mark.parametrize("cfg,devices", [(3, 0), (4, 0), (5, 0), (3, [0, 0]), (4, [0, 0, 0, 0])],
-                         ids=["3", "4", "5", "3-multi", "4-multi"])
-def test_fullscale_blocks_match_oracle(cfg, devices):
+@pytest.mark.parametrize("cfg,devices,solver", [(3, 0, 0), (4, 0, 0), (5, 0, 0), (4, 0, 1), (3, [0, 0], 0),
+                                                (4, [0, 0, 0, 0], 0), (4, [0, 0, 0, 0], 1)],
+                         ids=["3", "4", "5", "4-factor", "3-multi", "4-multi", "4-multi-factor"])
+def test_fullscale_blocks_match_oracle(cfg, devices, solver):
     """devices = [0, 0] / [0] * 4: the product's multi-device context (dbslmm_ctx_create_multi: the
-    shard plan's (block, h2f copy) units, compact per-device .bed images, one host thread per job)
-    on the test GPU.  Its betas must equal the one-device solve bit for bit -- except, at config 4
-    on four devices, the non-base h2f copies of the block whose copies the shard plan splits over
-    devices: those are factored directly there (the one-device run iterates them), so they agree to
-    cheb_tol; the oracle comparison below holds every copy to its bar either way."""
+    shard plan's units, compact per-device .bed images, one host thread per job) on the test GPU.
+    Its betas must equal the one-device solve bit for bit -- on the PCG route every block is whole
+    on one device and iterates independently of the others; on the factorisation route
+    (solver = 1) except the non-base h2f copies of the block whose copies the shard plan splits
+    over devices at config 4: those are factored directly there (the one-device run iterates them),
+    so they agree to cheb_tol.  The oracle comparison below holds every copy to its bar either way."""
     from dbslmm_amd import synth
-    from dbslmm_amd.dist import shard_units
+    from dbslmm_amd.dist import shard_units_problem
     snps, n_ref, pop, lmm, factors = CONFIGS[cfg]
     panel = synth.simulate(snps, n_ref, pop=pop, seed=1, engine="gpu")
     prob = synth.make_problem(panel, lmm_only=lmm)
     del panel
+    if solver:
+        prob.opts["solver"] = solver
     sig, out, wl = _gpu_solve(prob, factors, devices)
+    pcg = bool(wl["pcg_route"])
+    assert pcg == (solver == 0), wl["pcg_route"]
     m_b = np.diff(prob.s_ptr) + (np.diff(prob.l_ptr) if prob.l_ptr is not None else 0)
     if isinstance(devices, list):
         prob.opts.pop("shard_copies", None)
         _, one, _ = _gpu_solve(prob, factors, 0)
-        ud, _ = shard_units(m_b, prob.n_ref, len(devices), len(factors))
+        ud, _ = shard_units_problem(prob, [prob.sigma_s] * len(factors), len(devices))
         split = np.flatnonzero(~np.all(ud == ud[:, :1], axis=1))
-        if cfg == 4:
+        if pcg:
+            assert split.size == 0                                              # whole blocks
+        elif cfg == 4:
             assert split.size >= 1 and m_b[split].max() == m_b.max(), split   # the 9.7k block
         ms = np.zeros(prob.n_s, dtype=bool)
         ml = np.zeros(prob.n_l, dtype=bool)
@@ -192,11 +203,12 @@ def test_fullscale_blocks_match_oracle(cfg, devices):
     for bs, bl, st in out:
         assert np.all((st == 0) | ((st == 1) & (m_b == 0))), np.flatnonzero((st != 0) & (m_b > 0))
         assert np.all(np.isfinite(bs)) and np.all(np.isfinite(bl))
-    if len(factors) > 1:
-        assert wl["cheb_iters"] > 0          # the Chebyshev h2f path is the one under test
-    # the base copy (median sigma) is solved directly, the others by Chebyshev on its factor
+    if len(factors) > 1 and not pcg:
+        assert wl["cheb_iters"] > 0          # the h2f iterations on the base factor are under test
+    # factorisation route: the base copy (median sigma) is solved directly, the others iterated on
+    # its factor to cheb_tol; PCG route: every copy to pcg_tol
     base = int(np.argsort(sig, kind="stable")[len(sig) // 2])
-    tol_c = [1e-10 if (len(sig) == 1 or c == base) else CHEB_TOL for c in range(len(sig))]
+    tol_c = [1e-10 if (pcg or len(sig) == 1 or c == base) else CHEB_TOL for c in range(len(sig))]
     thr = _threads()
     O.use_blas(True)
     O.blas_threads(thr)
