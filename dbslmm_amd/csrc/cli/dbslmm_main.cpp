@@ -555,6 +555,11 @@ long write_eff_files(const vector<string>& names, const vector<std::array<EffLis
 }  // namespace
 
 int main(int argc, char** argv) {
+    if (dbslmm_abi_version() != DBSLMM_ABI_VERSION) {   // a stale build against another library
+        std::fprintf(stderr, "ERROR: libdbslmm_hip has ABI %d, this dbslmm was built for %d: rebuild it\n",
+                     dbslmm_abi_version(), DBSLMM_ABI_VERSION);
+        return 1;
+    }
     Phases ph;
     if (argc <= 1) { print_header(); return 0; }
     if (argc == 2 && argv[1][0] == '-' && argv[1][1] == 'h') { print_help(); return 0; }

@@ -81,6 +81,11 @@ std::unordered_map<string, SummS> read_ext(const string& path) {
 }  // namespace
 
 int main(int argc, char** argv) {
+    if (dbslmm_abi_version() != DBSLMM_ABI_VERSION) {   // a stale build against another library
+        std::cerr << "ERROR: libdbslmm_hip has ABI " << dbslmm_abi_version() << ", this valid was built for "
+                  << DBSLMM_ABI_VERSION << ": rebuild it\n";
+        return 1;
+    }
     if (argc <= 1) {
         std::cout << "\n*************************************************************\n"
                   << "  Deterministic Bayesian Sparse Linear Mixed Model (DBSLMM)  \n"

@@ -86,6 +86,8 @@ struct PcgArgs {
     const int32_t* blk_id;          // plan block -> original block id
     const double* dshift;           // per copy: 1 / (sigma_c n)
     double *X, *R, *P, *Sv, *W;     // state vectors, [copy][Tb * kT] per block
+    double* U;                      // the product's input per product column: (rsd on the uint16
+                                    // path) o r / diag, zero past m -- written with r
     double* part;                   // symv partial slots
     double* dot;                    // per tile row [kNDot][copy]
     double* qs;                     // per block copy: {gamma, alpha} x 2 parities, then the
@@ -260,21 +262,14 @@ __device__ __forceinline__ void quad_mul64(const double* __restrict__ base, int6
     }
 }
 
-// the product's input of tile row T, copy k, block slot i: u = r / diag, times rsd on the u16 path
-__device__ __forceinline__ void stage_v(const PcgArgs& a, const PcgBlk& B, bool u16, int T, int nc, int lane,
-                                        double* v) {
+// the product's input of tile row T (every product column) into LDS: U = (rsd o) r / diag, as
+// the last update (or init) wrote it -- zero past m
+__device__ __forceinline__ void stage_v(const PcgArgs& a, const PcgBlk& B, int T, int nc, int lane, double* v) {
     for (int k = 0; k < nc; ++k) {
-        const double dc = col_shift(a, B, k);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int rr = lane + 64 * h, i = T * kT + rr;
-            double x = 0.0;
-            if (i < B.m) {
-                x = a.R[k * a.vstride + B.vo + i] / jdiag(a, B, i, dc);
-                if (u16) x *= a.rsd[B.row0 + i];
-            }
-            v[k * kVS + rr] = x;
-        }
+        const double* src = a.U + k * a.vstride + B.vo + static_cast<int64_t>(T) * kT;
+        const double x0 = src[lane], x1 = src[lane + 64];
+        v[k * kVS + lane] = x0;
+        v[k * kVS + lane + 64] = x1;
     }
 }
 
@@ -306,7 +301,6 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     const PcgBlk B = a.blk[item.x];
     if (a.done[item.x] || on_u16(a, B) != U16) return;
     const int I = item.y, J0 = item.z, J1 = item.w, nc = B.nc;
-    constexpr bool u16 = U16;
     const int64_t ld16 = static_cast<int64_t>(B.Tb) * kT;
     const int rg = lane >> 3, cg = lane & 7;
     auto vj_of = [&](int J) -> double* { return J == I ? vI : vJb + ((J - J0) & 1) * nc * kVS; };
@@ -343,8 +337,8 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     pcg_u4 ra[8], rb[8];
     int J = J0, q = 0;                       // quadrant 0 of a tile of the run is always active
     load(J, q, ra);
-    stage_v(a, B, u16, I, nc, lane, vI);
-    if (J != I) stage_v(a, B, u16, J, nc, lane, vj_of(J));
+    stage_v(a, B, I, nc, lane, vI);
+    if (J != I) stage_v(a, B, J, nc, lane, vj_of(J));
     for (int t = 0; t < 2 * nc; ++t) rsum[t * 64 + lane] = csum[t * 64 + lane] = 0.0;
     wave_fence();
     // one pipeline step: prefetch the next quadrant into `nxt` (and its column vector at a tile
@@ -355,7 +349,7 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
         const bool more = next_quad(B, I, J1, Jn, qn);
         if (more) {
             load(Jn, qn, nxt);
-            if (Jn != J && Jn != I) stage_v(a, B, u16, Jn, nc, lane, vj_of(Jn));
+            if (Jn != J && Jn != I) stage_v(a, B, Jn, nc, lane, vj_of(Jn));
         }
         mult(J, q, cur);
         if (!more || Jn != J) flush(J);
@@ -422,6 +416,12 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_init(PcgA
             a.Sv[o] = 0.0;
             a.W[o] = 0.0;
             a.R[o] = rhs;
+            double uv = 0.0;
+            if (in) {
+                uv = rhs / jdiag(a, B, i, col_shift(a, B, c));
+                if (u16) uv *= a.rsd[B.row0 + i];
+            }
+            a.U[o] = uv;
         }
     }
 #pragma unroll
@@ -683,6 +683,7 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
                 const double rn = __builtin_fma(-al, sn, rv);
                 a.Sv[o0] = sn;
                 a.R[o0] = rn;
+                a.U[o0] = u16 ? rn * a.rsd[B.row0 + i] : rn;
                 if (u16) sv[0] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * rn;
             }
         }
@@ -702,6 +703,7 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
             a.Sv[o] = s;
             a.X[o] = x;
             a.R[o] = rn;
+            a.U[o] = u16 ? (rn / dg) * a.rsd[B.row0 + i] : rn / dg;
             if (u16) sv[k] = a.S[B.row0 + i] * a.rsd[B.row0 + i] * (rn / dg);
         }
     }

@@ -2064,7 +2064,7 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     HIP_TRY(ctx, dev_upload(&p->d_pblk, blk, ctx->stream));
     HIP_TRY(ctx, dev_upload(&p->d_pitem, items, ctx->stream));
     HIP_TRY(ctx, dev_upload(&p->d_prow, rows, ctx->stream));
-    HIP_TRY(ctx, hipMalloc(&p->d_pvec, std::max<int64_t>(1, 5 * n * vo) * sizeof(double)));
+    HIP_TRY(ctx, hipMalloc(&p->d_pvec, std::max<int64_t>(1, 6 * n * vo) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_ppart, std::max<int64_t>(1, po) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_pdot, std::max<int64_t>(1, dof) * sizeof(double)));
     HIP_TRY(ctx, hipMalloc(&p->d_pqs, std::max<int32_t>(1, sco) * pcg::kQS * sizeof(double)));
@@ -2227,6 +2227,7 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
     a.P = a.R + vs;
     a.Sv = a.P + vs;
     a.W = a.Sv + vs;
+    a.U = a.W + vs;
     a.part = p->d_ppart;
     a.dot = p->d_pdot;
     a.qs = p->d_pqs;

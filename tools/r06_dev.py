@@ -17,7 +17,7 @@ CFG = {3: (500_000, 5_000, "EUR", False, (1.0,)), 4: (1_000_000, 10_000, "EUR", 
        5: (1_000_000, 10_000, "AFR", True, (1.0,))}
 
 
-def main(out, cfg=4, ns=(1, 2, 4, 8)):
+def main(out, cfg=4, ns=(1, 2, 4, 8), only=None):
     snps, n_ref, pop, lmm, f = CFG[cfg]
     pan = synth.simulate(snps, n_ref, pop=pop, seed=1, engine="gpu")
     prob = synth.make_problem(pan, lmm_only=lmm)
@@ -31,6 +31,8 @@ def main(out, cfg=4, ns=(1, 2, 4, 8)):
         ud, model = shard_units_problem(prob, sig, N)
         devs = []
         for d in range(N):
+            if only is not None and d != only:
+                continue
             plan = Plan.units(ctx, prob, ud, d)
             o = (np.zeros((K, prob.n_s)), np.zeros((K, prob.n_l)), np.zeros((K, prob.num_block), dtype=np.int32))
             for _ in range(3):
@@ -57,4 +59,5 @@ def main(out, cfg=4, ns=(1, 2, 4, 8)):
 if __name__ == "__main__":
     cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     ns = tuple(int(x) for x in sys.argv[3].split(",")) if len(sys.argv) > 3 else (1, 2, 4, 8)
-    main(sys.argv[1], cfg, ns)
+    only = int(sys.argv[4]) if len(sys.argv) > 4 else None      # one device of the plan (profiling)
+    main(sys.argv[1], cfg, ns, only)
