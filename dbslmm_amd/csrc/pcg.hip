@@ -32,7 +32,7 @@
 // ONCE: a 128 x 128 tile (I, J) adds G_IJ v_J to rows I and G_IJ^T v_I to rows J.
 //
 // Kernels (one launch each per iteration, every block of the plan in each):
-//   dbslmm_pcg_symv    one wave per item = a run of up to kRun tiles along a tile row; per lane an
+//   dbslmm_pcg_symv    one wave per item = a run of up to `run` tiles along a tile row; per lane an
 //                      8 x 8 sub-block of each 64 x 64 quadrant, row and column sums reduce-
 //                      scattered over the lanes (fixed order); writes the row partial of the run
 //                      and each tile's column partial into per-block slots (no atomics: the sums
@@ -49,13 +49,17 @@
 
 namespace pcg {
 constexpr int kT = 128;           // tile edge of the operator's lower triangle (slots of a block)
-constexpr int kRun = 8;           // tiles per symv item (along a tile row)
+constexpr int kRunMax = 8;        // tiles per symv item (along a tile row): 8, or fewer when the
+                                  // plan has too few items to fill the chip (PcgArgs::run)
 constexpr int kMaxNC = 4;         // h2f copies per run (right-hand sides) on this route
 constexpr int kWaves = 4;         // symv items per 256-thread workgroup
 constexpr int kVS = kT + 8;       // LDS stride of a staged vector column (doubles)
 constexpr int kNDot = 5;          // per tile row and copy: r.u, w.u, r.r, x.x, S.(rsd o u)
 constexpr int kQS = 8;            // recurrence state doubles per block and copy
 constexpr int kThreads = 256;
+constexpr int kFTb = 8;           // dbslmm_pcg_block: blocks of at most kFTb tile rows (1024 slots)
+constexpr int kFRows = kFTb * kT;
+constexpr int kFPer = kFRows / kThreads;   // rows per thread
 // symv LDS per wave: the staged rsd o u of the item's tile row and of two tile columns, and the
 // reduce-scattered row / column sums ([2][copy][64] each)
 constexpr int wave_lds_doubles(int nc) { return 3 * nc * kVS + 4 * nc * 64; }
@@ -72,6 +76,9 @@ struct PcgBlk {
                                     // columns past m stay zero: no masks in the product)
     int32_t nc;                     // product columns: 1 (multi-shift block) or the copies
     int32_t mshift;                 // 1: no large SNP and several copies -> one Krylov sequence
+    int32_t fused;                  // 1: one product column and <= kFTb tile rows -- on the uint16
+                                    // Gram the whole solve runs in dbslmm_pcg_block (done = 3)
+    int32_t pad_;
 };
 
 struct PcgArgs {
@@ -103,6 +110,7 @@ struct PcgArgs {
     int64_t ns, nl, nbk;            // beta / status strides per copy
     double tau, rn, c0, tol, inv_sqrt_n;
     int32_t ncopy;
+    int32_t run;                    // tiles per symv item (1, 2, 4 or 8)
     int32_t seed;                   // multi-shift seed: the copy with the smallest shift
 };
 
@@ -361,7 +369,7 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     while (step(ra, rb) && step(rb, ra)) {
     }
     // row partial of the run: slot Tb + run of tile row I
-    double* dst = a.part + B.po + (static_cast<int64_t>(I) * B.Ns + B.Tb + J0 / kRun) * nc * kT;
+    double* dst = a.part + B.po + (static_cast<int64_t>(I) * B.Ns + B.Tb + J0 / a.run) * nc * kT;
     for (int qi = 0; qi < 2; ++qi)
         for (int k = 0; k < nc; ++k) dst[k * kT + 64 * qi + 8 * rg + cg] = rsum[(qi * nc + k) * 64 + lane];
 }
@@ -397,8 +405,9 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_init(PcgA
         }
         if (tid == 0) {
             a.itb[bi] = 0;
-            a.done[bi] = mono_s ? 2 : 0;
-            if (!mono_s) atomicAdd(a.active, 1);
+            const bool fz = B.fused && u16;       // solved whole by dbslmm_pcg_block
+            a.done[bi] = mono_s ? 2 : fz ? 3 : 0;
+            if (!mono_s && !fz) atomicAdd(a.active, 1);
         }
     }
     // rows 0..127 of the tile row, two halves of the columns
@@ -492,7 +501,7 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_rows(PcgA
     const int r = tid & (kT - 1), h = tid >> 7, i = I * kT + r;
     const bool in = i < B.m;
     const double Si = in ? a.S[B.row0 + i] : 0.0, ri = in ? a.rsd[B.row0 + i] : 0.0;
-    const int nrun = (I + kRun) / kRun;   // runs of tile row I: ceil((I + 1) / kRun)
+    const int nrun = (I + a.run) / a.run;   // runs of tile row I: ceil((I + 1) / run)
     double dv[kMaxNC][4];
 #pragma unroll
     for (int k = 0; k < kMaxNC; ++k)
@@ -716,6 +725,286 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
     if (tid < nc && (B.mshift || run_s[tid])) {
         const int hk = tid & 1;
         a.dot[B.dof + (static_cast<int64_t>(I) * kNDot + 4) * n + tid] = red[2 * hk][tid] + red[2 * hk + 1][tid];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// The small blocks' whole solve in one launch (round 6).  A block with one product column (a
+// multi-shift block, or a single copy) and at most kFTb tile rows on the uint16 Gram is solved by
+// ONE workgroup from the right-hand side to convergence (a persistent grid of one workgroup per CU
+// walks the list, so the chip-wide kernels keep half of every CU): per iteration the block's quadrants are
+// streamed once (the 8 x 8 lane sub-blocks and reduce-scatters of quad_mul16, next quadrant in
+// flight), each wave adding its row and column sums into its own LDS copy of y (fixed order, no
+// atomics), then w, the dots, the coefficients, the convergence test and the update exactly as
+// dbslmm_pcg_rows / dbslmm_pcg_update compute them -- with no partial slots, no per-iteration
+// launches and no hand-off between workgroups.  Thread t owns slots t + 256 q (q < kFPer): r, s
+// and w in registers, x and p of every copy in the block's global vectors (private to this
+// workgroup); U = rsd o u in LDS.  The chip-wide kernels skip these blocks (init marks them
+// done = 3); dbslmm_pcg_final writes their betas and status from x and cnv as for the others.
+// ------------------------------------------------------------------------------------------
+namespace pcg {
+// sum of v over the workgroup, every thread gets the total (fixed order: lanes, then waves 0..3)
+template <int N>
+__device__ __forceinline__ void block_sum(double (&v)[N], double* red, int tid) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = wave_sum(v[k]);
+    __syncthreads();                          // (red free: its previous readers are past this)
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < N; ++k) red[(tid >> 6) * N + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = ((red[k] + red[N + k]) + red[2 * N + k]) + red[3 * N + k];
+}
+// LDS: y per wave, U, the block_sum scratch, the recurrence state and flags
+constexpr size_t block_lds_bytes() { return sizeof(double) * (5 * kFRows + 4 * (3 + kMaxNC) + 12 + 3 * kMaxNC + 4); }
+}  // namespace pcg
+
+__device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_t maxit) {
+    using namespace pcg;
+    extern __shared__ double blds[];
+    double* yw = blds;                       // [4][kFRows] per-wave product sums
+    double* Ul = blds + 4 * kFRows;          // [kFRows] rsd o u
+    double* red = Ul + kFRows;               // block_sum scratch
+    if (a.done[bi] != 3) return;             // (monomorphic, or missing calls: the chip-wide path)
+    const PcgBlk B = a.blk[bi];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = a.ncopy, m = B.m, Tb = B.Tb;
+    const bool msh = B.mshift != 0;
+    const double dc = col_shift(a, B, 0);    // the product column's shift (the seed's on a multi-shift block)
+    // ---- state: x = p = 0, r = z, s = w = 0, U = rsd o r / diag
+    double r[kFPer], sv[kFPer], wv[kFPer], sg[1] = {0.0};
+#pragma unroll
+    for (int q = 0; q < kFPer; ++q) {
+        const int i = tid + kThreads * q;
+        const bool in = i < m;
+        r[q] = in ? a.z[B.row0 + i] : 0.0;
+        sv[q] = wv[q] = 0.0;
+        double u = 0.0;
+        if (in) {
+            u = (r[q] / jdiag(a, B, i, dc)) * a.rsd[B.row0 + i];
+            sg[0] += a.S[B.row0 + i] * u;
+        }
+        Ul[i] = u;                           // (zero past m)
+        for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;   // (x = p = 0: dbslmm_pcg_init)
+    }
+    block_sum(sg, red, tid);
+    double sig = sg[0];
+    // quadrants of the block's lower triangle (rows and columns < m), dealt to the waves in turn
+    const int Q = (m + 63) / 64;
+    const int nq = Q * (Q + 1) / 2;
+    const int64_t ld16 = static_cast<int64_t>(Tb) * kT;
+    const int rg = lane >> 3, cg = lane & 7;
+    auto quad_of = [&](int t, int& qi, int& qj) {   // t-th lower-triangle quadrant, row-major
+        qi = static_cast<int>((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+        while (qi * (qi + 1) / 2 > t) --qi;
+        while ((qi + 1) * (qi + 2) / 2 <= t) ++qi;
+        qj = t - qi * (qi + 1) / 2;
+    };
+    auto load = [&](int t, pcg_u4 (&raw)[8]) {
+        int qi, qj;
+        quad_of(t, qi, qj);
+        const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(64 * qi + 8 * rg) * ld16 + 64 * qj + 8 * cg;
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) raw[rr] = *reinterpret_cast<const pcg_u4*>(q16 + rr * ld16);
+    };
+    auto mult = [&](int t, const pcg_u4 (&raw)[8]) {
+        int qi, qj;
+        quad_of(t, qi, qj);
+        const bool dq = qi == qj;
+        double vi[8], vj[8], racc[8], cacc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            vi[q] = Ul[64 * qi + 8 * rg + q];
+            vj[q] = Ul[64 * qj + 8 * cg + q];
+            racc[q] = cacc[q] = 0.0;
+        }
+        if (!dq) {
+#pragma unroll
+            for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t w = raw[rr][c >> 1];
+                    const double g = (c & 1) ? cvt_hi(w) : cvt_lo(w);
+                    racc[rr] = __builtin_fma(g, vj[c], racc[rr]);
+                    cacc[c] = __builtin_fma(g, vi[rr], cacc[c]);
+                }
+        } else {
+#pragma unroll
+            for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t w = raw[rr][c >> 1];
+                    const double g = (c & 1) ? cvt_hi(w) : cvt_lo(w);
+                    const int dd = 8 * (cg - rg) + c - rr;   // j - i
+                    racc[rr] = __builtin_fma(dd <= 0 ? g : 0.0, vj[c], racc[rr]);
+                    cacc[c] = __builtin_fma(dd < 0 ? g : 0.0, vi[rr], cacc[c]);
+                }
+        }
+        double* y = yw + wave * kFRows;
+        const int ri = 64 * qi + 8 * rg + cg, ci = 64 * qj + 8 * cg + rg;
+        y[ri] += rscatter8(racc, lane, 4, 2, 1);
+        wave_fence();                          // (a diagonal quadrant: the row sums land first)
+        y[ci] += rscatter8(cacc, lane, 32, 16, 8);
+    };
+    // recurrence state: thread 0 keeps it in LDS (kept out of the registers of the product loop)
+    double* st = red + 4 * (3 + kMaxNC);     // [0] gamma_prev, [1] alpha_prev, [2] alpha, [3] beta,
+                                             // [4 + c] zeta_k, [8 + c] zeta_k-1, [12 + 3c ..] coef
+    int* flag = reinterpret_cast<int*>(st + 12 + 3 * kMaxNC);   // [c] converged, [kMaxNC] running
+    if (tid == 0) {
+        for (int c = 0; c < kMaxNC; ++c) {
+            st[4 + c] = st[8 + c] = 1.0;
+            flag[c] = c >= n;
+        }
+    }
+    int it = 0;
+    for (; it < maxit; ++it) {
+        // ---- product y = G U (U in LDS since the last update)
+        __syncthreads();
+        {
+            pcg_u4 ra[8], rb[8];
+            int t = wave;
+            if (t < nq) load(t, ra);
+            while (t < nq) {
+                const int tn = t + 4;
+                if (tn < nq) load(tn, rb);
+                mult(t, ra);
+                t = tn;
+                if (t >= nq) break;
+                const int tn2 = t + 4;
+                if (tn2 < nq) load(tn2, ra);
+                mult(t, rb);
+                t = tn2;
+            }
+        }
+        __syncthreads();
+        // ---- w = M u, dots r.u, w.u, r.r and x.x per copy (dbslmm_pcg_rows)
+        double d[3 + kMaxNC];
+#pragma unroll
+        for (int k = 0; k < 3 + kMaxNC; ++k) d[k] = 0.0;
+#pragma unroll
+        for (int q = 0; q < kFPer; ++q) {
+            const int i = tid + kThreads * q;
+            double y = 0.0;
+            if (i < Tb * kT) {
+                y = ((yw[i] + yw[kFRows + i]) + yw[2 * kFRows + i]) + yw[3 * kFRows + i];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;
+            }
+            if (i < m) {
+                const double Si = a.S[B.row0 + i], ri = a.rsd[B.row0 + i];
+                const double u = r[q] / jdiag(a, B, i, dc);
+                const double sh = i < B.ms ? dc : 0.0;
+                const double w = a.tau * a.rn * ri * __builtin_fma(-Si, sig * a.rn, y) + (1.0 - a.tau + sh) * u;
+                wv[q] = w;
+                d[0] += r[q] * u;
+                d[1] += w * u;
+                d[2] += r[q] * r[q];
+                for (int c = 0; c < n; ++c) {
+                    const double xv = a.X[c * a.vstride + B.vo + i];
+                    d[3 + c] += xv * xv;
+                }
+            }
+        }
+        block_sum(d, red, tid);
+        // ---- coefficients and convergence (dbslmm_pcg_update), by thread 0
+        if (tid == 0) {
+            const double gam = d[0], del = d[1], rr = d[2];
+            double al, be = 0.0;
+            if (it == 0) {
+                al = gam / del;
+            } else {
+                be = gam / st[0];
+                al = gam / (del - be * gam / st[1]);
+            }
+            int running = 0;
+            if (msh) {
+                const double cp = it == 0 ? 0.0 : al * be / st[1];
+                for (int c = 0; c < n; ++c) {
+                    const double zk = st[4 + c], zk1 = st[8 + c];
+                    const double t = a.tol * (a.dshift[c] + 1.0 - a.tau);
+                    const double rrc = rr * zk * zk;
+                    if (!flag[c] && (rrc == 0.0 || rrc <= t * t * d[3 + c])) {
+                        flag[c] = 1;
+                        a.cnv[B.sco + c] = it + 1;
+                    }
+                    const double e = a.dshift[c] - a.dshift[a.seed];
+                    const double zn = zk * zk1 / ((1.0 + cp + al * e) * zk1 - cp * zk);
+                    st[12 + 3 * c] = al * zn / zk;
+                    st[12 + 3 * c + 1] = zk1 != 0.0 ? (zk / zk1) * (zk / zk1) * be : 0.0;
+                    st[12 + 3 * c + 2] = zk;
+                    st[8 + c] = zk;
+                    st[4 + c] = zn;
+                    running += flag[c] ? 0 : 1;
+                }
+            } else {                          // one copy (n = 1), Jacobi-preconditioned
+                const double lam = B.ms == B.m ? a.dshift[0] + 1.0 - a.tau : 1.0 - a.tau;
+                const double t = a.tol * lam;
+                if (rr == 0.0 || rr <= t * t * d[3]) {
+                    flag[0] = 1;
+                    a.cnv[B.sco] = it + 1;
+                }
+                running = flag[0] ? 0 : 1;
+            }
+            st[0] = gam;
+            st[1] = al;
+            st[2] = al;
+            st[3] = be;
+            flag[kMaxNC] = running;
+        }
+        __syncthreads();
+        if (flag[kMaxNC] == 0) break;
+        const double al = st[2], be = st[3];
+        // ---- update p, x (every running copy), s, r, U
+        double sg2[1] = {0.0};
+#pragma unroll
+        for (int q = 0; q < kFPer; ++q) {
+            const int i = tid + kThreads * q;
+            if (i >= m) continue;
+            const double rsd_i = a.rsd[B.row0 + i];
+            double rn;
+            if (msh) {
+                for (int c = 0; c < n; ++c) {
+                    if (flag[c]) continue;
+                    const int64_t o = c * a.vstride + B.vo + i;
+                    const double pv = __builtin_fma(st[12 + 3 * c + 1], a.P[o], st[12 + 3 * c + 2] * r[q]);
+                    a.P[o] = pv;
+                    a.X[o] = __builtin_fma(st[12 + 3 * c], pv, a.X[o]);
+                }
+                const double sn = __builtin_fma(be, sv[q], wv[q]);
+                rn = __builtin_fma(-al, sn, r[q]);
+                sv[q] = sn;
+                r[q] = rn;
+                Ul[i] = rn * rsd_i;
+            } else {
+                const int64_t o = B.vo + i;
+                const double dg = jdiag(a, B, i, dc);
+                const double u = r[q] / dg;
+                const double pv = __builtin_fma(be, a.P[o], u);
+                const double sn = __builtin_fma(be, sv[q], wv[q]);
+                a.P[o] = pv;
+                a.X[o] = __builtin_fma(al, pv, a.X[o]);
+                rn = __builtin_fma(-al, sn, r[q]);
+                sv[q] = sn;
+                r[q] = rn;
+                Ul[i] = (rn / dg) * rsd_i;
+            }
+            sg2[0] += a.S[B.row0 + i] * Ul[i];
+        }
+        block_sum(sg2, red, tid);
+        sig = sg2[0];
+    }
+    if (tid == 0) a.itb[bi] = it + (it < maxit ? 1 : 0);
+}
+
+#ifndef PCG_BLOCK_WAVES
+#define PCG_BLOCK_WAVES 2   // waves per SIMD dbslmm_pcg_block is compiled for (3: 94 VGPRs spilled)
+#endif
+extern "C" __global__ __launch_bounds__(pcg::kThreads) __attribute__((amdgpu_waves_per_eu(PCG_BLOCK_WAVES, 8)))
+void dbslmm_pcg_block(PcgArgs a, const int32_t* __restrict__ list, int32_t n_list, int32_t maxit) {
+    for (int e = blockIdx.x; e < n_list; e += gridDim.x) {   // (the list is biggest first)
+        __syncthreads();                     // (the previous block's LDS readers are done)
+        pcg_block_solve(a, list[e], maxit);
     }
 }
 

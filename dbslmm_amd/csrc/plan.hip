@@ -277,12 +277,19 @@ struct dbslmm_plan {
     int4* d_pitem = nullptr;
     int2* d_prow = nullptr;
     int32_t n_pblk = 0, n_pitem = 0, n_prow = 0;
+    int32_t pcg_run = pcg::kRunMax;  // tiles per product item (pcg_layout)
+    bool pcg_fused = true;         // small one-column blocks solved whole by dbslmm_pcg_block
+    int32_t* d_pflist = nullptr;   // ... their PcgBlk indices (biggest first)
+    int32_t n_pflist = 0;
+    std::vector<char> h_pfused;    // per PcgBlk: 1 = in that list
+    bool pcg_join = false;         // the main stream still has to wait for dbslmm_pcg_block
     double *d_pvec = nullptr, *d_ppart = nullptr, *d_pdot = nullptr, *d_pqs = nullptr;
     int32_t *d_pcnv = nullptr, *d_pitb = nullptr, *d_pdone = nullptr, *d_pact = nullptr;
     int64_t pcg_vstride = 0;
     int32_t* h_pmon = nullptr;     // pinned: [active | itb per block] after a chunk
     int32_t pcg_it = 0;            // iterations enqueued by the current run
-    int32_t pcg_need = 0;          // iterations the latest finished run needed (its slowest block)
+    int32_t pcg_need = -1;         // chip-wide iterations the latest finished run needed (-1: no run yet)
+    int32_t pcg_iters_max = 0;     // ... and the iterations of its slowest block (any path)
     bool pcg_pending = false;      // a PCG run whose convergence has not been checked yet
     bool pcg_ran = false;          // the latest run took the PCG route
     bool pcg_pending_var = false;  // ... so the variance needs a factorisation first
@@ -861,7 +868,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items,
                     p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv, p->d_cgit, p->d_G16, p->d_pblk,
                     p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
-                    p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16};
+                    p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16, p->d_pflist};
     for (void* b : bufs)
         if (b) {
             const hipError_t e = hipFree(b);
@@ -920,6 +927,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    op.shard_copies <= 64 && op.h2f_iter >= 0 && op.h2f_iter <= 2 && op.solver >= 0 &&
                    op.solver <= 2 && op.pcg_tol >= 0.0 && op.pcg_maxit >= 0, "bad dbslmm_options");
     p->solver = op.solver;
+    if (const char* e = std::getenv("DBSLMM_PCG_FUSED")) p->pcg_fused = std::atoi(e) != 0;   // (A/B)
     if (op.pcg_tol > 0.0) p->pcg_tol = std::max(1e-15, op.pcg_tol);
     if (op.pcg_maxit > 0) p->pcg_maxit = op.pcg_maxit;
     p->pcg_g16 = 4 * static_cast<int64_t>(pr->n_ref) <= 65535;
@@ -1990,7 +1998,7 @@ static bool pcg_route(const dbslmm_plan* p, const double* sigmas, int n) {
 }
 
 // Lay the PCG buffers out for n copies: per block its tile rows (128 slots), the product's work
-// items (runs of kRun tiles along a tile row, biggest blocks first), vectors [5][copy][slots],
+// items (runs of up to kRunMax tiles along a tile row, biggest blocks first), vectors [6][copy][slots],
 // partial slots, dots and the recurrence state.
 static int pcg_layout(dbslmm_plan* p, int n) {
     dbslmm_ctx* ctx = p->ctx;
@@ -2017,26 +2025,36 @@ static int pcg_layout(dbslmm_plan* p, int n) {
                                                hipHostMallocDefault));
     if (p->pcg_n == n) return DBSLMM_OK;
     void* old[] = {p->d_pblk, p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
-                   p->d_pitb, p->d_pdone, p->d_pact};
+                   p->d_pitb, p->d_pdone, p->d_pact, p->d_pflist};
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (void* q : old)
         if (q) (void)hipFree(q);
+    p->d_pflist = nullptr;               // (uploaded below only when some block is solved whole)
     using namespace pcg;
     std::vector<PcgBlk> blk;
+    std::vector<int32_t> flist;          // blocks solved whole by dbslmm_pcg_block
     std::vector<int4> items;
     std::vector<int2> rows;
     int64_t vo = 0, po = 0, dof = 0;
     int32_t sco = 0;
     double bytes = 0.0, pbytes = 0.0, flops = 0.0;
     const double esz = p->pcg_g16 ? 2.0 : 8.0;
+    // tiles per product item: one (measured at config 4: 10.65 / 10.90 / 11.13 / 11.34 ms per step
+    // at 1 / 2 / 4 / 8, and the N = 8 shards' product 114 -> ~45 us: many short items keep more
+    // row segments in flight than a few long ones)
+    int run = 1;
+    if (const char* e = std::getenv("DBSLMM_PCG_RUN")) run = std::clamp(std::atoi(e), 1, static_cast<int>(kRunMax));   // (A/B)
+    p->pcg_run = run;
     for (int b = 0; b < p->n_nonempty; ++b) {
-        const int32_t m = p->h_m[b], Tb = (m + kT - 1) / kT, nrun = (Tb + kRun - 1) / kRun;
+        const int32_t m = p->h_m[b], Tb = (m + kT - 1) / kT, nrun = (Tb + run - 1) / run;
         // a block without large SNPs solves n scalar shifts of one matrix: one Krylov sequence
         // (multi-shift CG, one product column); with large SNPs each copy iterates on its own
         const bool msh = n > 1 && p->h_ms[b] == m;
         const int32_t nc = msh ? 1 : n;
+        const bool fused = p->pcg_fused && nc == 1 && Tb <= kFTb && !p->h_off16.empty();
         PcgBlk k{b, p->h_row0[b], m, p->h_ms[b], p->h_ld[b], Tb, Tb + nrun, sco, p->h_matoff[b], vo, po, dof,
-                 p->h_off16.empty() ? 0 : p->h_off16[b], nc, msh ? 1 : 0};
+                 p->h_off16.empty() ? 0 : p->h_off16[b], nc, msh ? 1 : 0, fused ? 1 : 0, 0};
+        if (fused) flist.push_back(static_cast<int32_t>(blk.size()));
         const int bi = static_cast<int>(blk.size());
         blk.push_back(k);
         vo += static_cast<int64_t>(Tb) * kT;
@@ -2045,15 +2063,23 @@ static int pcg_layout(dbslmm_plan* p, int n) {
         sco += n;
         for (int I = 0; I < Tb; ++I) {
             rows.push_back(int2{bi, I});
-            for (int J0 = 0; J0 <= I; J0 += kRun) items.push_back(int4{bi, I, J0, std::min(I, J0 + kRun - 1)});
+            for (int J0 = 0; J0 <= I; J0 += run) items.push_back(int4{bi, I, J0, std::min(I, J0 + run - 1)});
         }
         bytes += 0.5 * m * (m + 1.0) * esz;
         flops += 4.0 * nc * 0.5 * m * (m + 1.0);
         // partials written and read once: a column slot per tile (I, J <= I), a row slot per run
         pbytes += 2.0 * 8.0 * nc * kT * (0.5 * Tb * (Tb + 1.0) + Tb * 0.5 * (nrun + 1.0));
     }
-    // biggest blocks' items first (their tile rows are the longest runs of work)
-    std::stable_sort(items.begin(), items.end(), [&](const int4& x, const int4& y) { return blk[x.x].Tb > blk[y.x].Tb; });
+    // biggest blocks' items first (their tile rows are the longest runs of work); the items of the
+    // blocks dbslmm_pcg_block solves last (they return at once unless the block has missing calls)
+    std::stable_sort(items.begin(), items.end(), [&](const int4& x, const int4& y) {
+        return blk[x.x].fused != blk[y.x].fused ? blk[x.x].fused < blk[y.x].fused : blk[x.x].Tb > blk[y.x].Tb;
+    });
+    std::stable_sort(flist.begin(), flist.end(), [&](int32_t x, int32_t y) { return blk[x].Tb > blk[y].Tb; });
+    p->h_pfused.assign(blk.size(), 0);
+    for (int32_t f : flist) p->h_pfused[f] = 1;
+    p->n_pflist = static_cast<int32_t>(flist.size());
+    if (!flist.empty()) HIP_TRY(ctx, dev_upload(&p->d_pflist, flist, ctx->stream));
     p->n_pblk = static_cast<int32_t>(blk.size());
     p->n_pitem = static_cast<int32_t>(items.size());
     p->n_prow = static_cast<int32_t>(rows.size());
@@ -2080,7 +2106,7 @@ static int pcg_layout(dbslmm_plan* p, int n) {
 // Chebyshev bound of the well-conditioned case, kappa = 1 + 12 / (d_min + 1 - tau), + 2, + 4 when
 // large SNPs add outlying eigenvalues (tools/cg_gate.py: +4 at 10 large SNPs in a block).
 static int pcg_first_chunk(const dbslmm_plan* p, const double* sigmas, int n) {
-    if (p->pcg_need > 0) return std::min(p->pcg_need, p->pcg_maxit);
+    if (p->pcg_need >= 0) return std::min(p->pcg_need, p->pcg_maxit);   // (0: every block solved whole)
     double dmin = INFINITY;
     for (int c = 0; c < n; ++c) dmin = std::min(dmin, 1.0 / (sigmas[c] * static_cast<double>(p->n_obs)));
     const double kap = 1.0 + 12.0 / std::max(1e-3, dmin + 1.0 - p->tau);
@@ -2106,6 +2132,10 @@ static int pcg_iters(dbslmm_plan* p, int K) {
     }
     HIP_TRY(ctx, hipGetLastError());
     p->pcg_it += K;
+    if (p->pcg_join) {   // dbslmm_pcg_block's x / cnv / itb before the betas and the read-back
+        HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->join, 0));
+        p->pcg_join = false;
+    }
     hipLaunchKernelGGL(dbslmm_pcg_final, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipMemcpyAsync(p->h_pmon, p->d_pact, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -2121,10 +2151,13 @@ static int pcg_finish(dbslmm_plan* p) {
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         int32_t need = 0;
-        for (int b = 0; b < p->n_pblk; ++b) need = std::max(need, p->h_pmon[1 + b]);
+        for (int b = 0; b < p->n_pblk; ++b)   // (the chip-wide blocks: the chunk sizes are theirs)
+            if (p->h_pfused.empty() || !p->h_pfused[b]) need = std::max(need, p->h_pmon[1 + b]);
         if (p->h_pmon[0] <= 0 || p->pcg_it >= p->pcg_maxit) {
             p->pcg_pending = false;
             p->pcg_need = p->h_pmon[0] <= 0 ? need : p->pcg_maxit;
+            p->pcg_iters_max = 0;
+            for (int b = 0; b < p->n_pblk; ++b) p->pcg_iters_max = std::max(p->pcg_iters_max, p->h_pmon[1 + b]);
             if (p->pcg_m_blocks < 0) {   // missing-call flags are data: read once, after the first run
                 std::vector<int32_t> fl(std::max(1, p->n_nonempty));
                 HIP_TRY(ctx, hipMemcpy(fl.data(), p->d_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -2248,12 +2281,26 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
     a.tol = p->pcg_tol;
     a.inv_sqrt_n = 1.0 / std::sqrt(static_cast<double>(p->n_obs));
     a.ncopy = n;
-    a.seed = 0;                          // the multi-shift seed: the smallest shift (largest sigma)
+    a.run = p->pcg_run;
+                         // the multi-shift seed: the smallest shift (largest sigma)
     for (int c = 1; c < n; ++c)
         if (sigmas[c] > sigmas[a.seed]) a.seed = c;
     p->pcg_args = a;
     hipLaunchKernelGGL(dbslmm_pcg_init, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, a, p->d_prow);
     HIP_TRY(ctx, hipGetLastError());
+    p->pcg_join = false;
+    if (p->n_pflist > 0) {   // the small blocks' whole solves beside the chip-wide iterations
+        HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+        int per_cu = 1;   // workgroups per CU: the chip-wide kernels of the big blocks keep the rest
+        if (const char* e = std::getenv("DBSLMM_PCG_FUSED_WG")) per_cu = std::max(1, std::atoi(e));   // (A/B)
+        const int grid = std::max(1, std::min(p->n_pflist, per_cu * ctx->n_cu));
+        hipLaunchKernelGGL(dbslmm_pcg_block, dim3(grid), dim3(pcg::kThreads), pcg::block_lds_bytes(), ctx->stream2, a,
+                           p->d_pflist, p->n_pflist, p->pcg_maxit);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
+        p->pcg_join = true;
+    }
     p->pcg_it = 0;
     p->pcg_pending = true;
     if (const int rc = pcg_iters(p, pcg_first_chunk(p, sigmas, n))) return rc;
@@ -2774,7 +2821,7 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     }
     for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = p->wl[i];
     out[17] = p->pcg_ran ? 1.0 : 0.0;
-    out[18] = p->pcg_ran ? p->pcg_need : 0.0;
+    out[18] = p->pcg_ran ? p->pcg_iters_max : 0.0;
     out[19] = p->pcg_ran ? p->pcg_bytes : 0.0;
     out[20] = p->pcg_ran ? p->pcg_part_bytes : 0.0;
     out[21] = p->pcg_ran ? p->pcg_flops : 0.0;
