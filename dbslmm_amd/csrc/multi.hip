@@ -359,10 +359,14 @@ static int fan_out(dbslmm_plan* p, F f) {
     auto& S = p->mp->shards;
     const int n = static_cast<int>(S.size());
     std::vector<int> rc(n, DBSLMM_OK);
-    std::vector<std::thread> th;
-    th.reserve(n);
-    for (int i = 0; i < n; ++i) th.emplace_back([&, i] { rc[i] = f(i); });
-    for (auto& t : th) t.join();
+    if (n == 1) {
+        rc[0] = f(0);   // one job (a units plan of one device): no thread to spawn per call
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(n);
+        for (int i = 0; i < n; ++i) th.emplace_back([&, i] { rc[i] = f(i); });
+        for (auto& t : th) t.join();
+    }
     for (int i = 0; i < n; ++i)
         if (rc[i] != DBSLMM_OK) {
             dbslmm_ctx* jc = S[i].plan ? S[i].plan->ctx : S[i].ctx;

@@ -47,7 +47,8 @@ def main(out, cfg=4, ns=(1, 2, 4, 8), only=None):
             mine = ud[:, 0] == d
             devs.append(dict(wall_ms=wall, phases={KERNEL_NAMES[k]: float(ms[k]) for k in range(len(ms))},
                              blocks=int(mine.sum()), snps=int(m[mine].sum()), max_m=int(m[mine].max()),
-                             iters_max=int(it.max()), model_ms=float(model[d])))
+                             iters_max=int(it.max()), model_ms=float(model[d]),
+                             block_ids=np.flatnonzero(mine).tolist(), iters=it[mine].tolist()))
             plan.close()
             print(f"N={N} dev {d}: wall {wall:.3f} ms model {model[d]:.3f}  " +
                   " ".join(f"{k[7:]}={v:.3f}" for k, v in devs[-1]["phases"].items() if v > 0) +
