@@ -228,52 +228,70 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
 }
 
 // ---------------------------------------------------------------- time model, PCG route
-// On the PCG route (pcg.hip) a device runs ONE sequence: unpack + Gram of its blocks, then
-// iterations in which every block still iterating streams its lower-triangle matrix once (product,
-// one wave per run of 128 x 128 tiles) and reduces its tile rows (rows + update) -- blocks never
-// wait on each other, so a device's step is its summed work plus a floor per iteration (three
-// dependent launches) and per run; the largest block alone (~1 ms at 9.7k SNPs) stays far below
-// the step, so no block needs splitting.  Rates: the round-6 one-GPU kernel trace of configs 3-5
-// (profiles/r06/cal: per-kernel average over 8 runs, per-block iteration counts from
-// dbslmm_plan_block_iters), DESIGN.md section 6.
-constexpr double kPcgGramOpsHuge = 3.0e15;   // dbslmm_gram_huge (FP4 MFMA, uint16 epilogue), ops/s
-constexpr double kPcgGramOpsBig = 1.9e15;    // dbslmm_gram_big / _i8
-constexpr double kPcgTileNs = 7.2;           // product: ns per 128 x 128 tile per iteration
-constexpr double kPcgRowNs = 12.0;           // rows + update: ns per tile row and copy column per iteration
-constexpr double kPcgIterFloorUs = 15.0;     // three launches per iteration on an idle device
-constexpr double kPcgRunMs = 0.10;           // per run: memsets, init, final, status read-back
-constexpr double kPcgDownloadMsPerM = 0.2;   // per million (SNP, copy) results downloaded
+// On the PCG route (pcg.hip) a device runs one sequence: unpack + Gram of its blocks, then two
+// concurrent paths -- dbslmm_pcg_block solving its small one-column blocks whole (cost per
+// quadrant and iteration) and the chip-wide iterations of the others (per tile and per tile row
+// and copy column, plus a floor per iteration: three dependent launches) -- then the result
+// download.  No block needs splitting: the largest (9.7k SNPs) is ~1 ms of work.  Rates fitted to
+// the round-6 one-GPU rehearsals of configs 3-5 at N = 1, 2, 4, 8 (45 devices:
+// tools/fit_shard_model.py on profiles/r06/shard/dev_c*.json; config 4 every device within 5 %,
+// config 5 12 %, config 3 20 %), iteration counts a priori (pcg_iters_model), DESIGN.md section 6.
+constexpr double kPcgUnpackMs0 = 0.017, kPcgUnpackBps = 4.79e12;     // dwordx4 unpack
+constexpr double kPcgGramMs0 = 0.0745;                               // Gram launches
+constexpr double kPcgGramOpsHuge = 3.06e15, kPcgGramOpsBig = 1.46e15;   // 256- / 128-tile kernels
+constexpr double kPcgFusedQuadNs = 3.19;     // dbslmm_pcg_block: per 64 x 64 quadrant and iteration
+constexpr double kPcgTileNs = 6.47;          // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
+constexpr double kPcgRowNs = 33.6;           // rows + update: per tile row, copy column and iteration
+constexpr double kPcgIterFloorUs = 31.5;     // per chip-wide iteration (launch chain)
+constexpr double kPcgShare = 0.66;           // both paths at once: 0.66 of their summed times
+constexpr double kPcgRunMs = 0.109;          // per run: memsets, init, final, read-back, host
+constexpr double kPcgDownloadMsPerM = 0.774; // per million (SNP, copy) results downloaded + scattered
+constexpr int kPcgFusedTb = 8;               // pcg::kFTb
 
-// a priori iterations of a block: CG's bound at kappa = 1 + 12 / (d + 1 - tau) (pcg_first_chunk),
-// outlying eigenvalues of large SNPs + 2
+// a priori iterations of a block at relative tolerance tol: CG's bound at kappa = 1 + 10 /
+// (d + 1 - tau) (fitted to the measured counts: 15.7 / 13.9 / 12.9 mean at d = 10 / 16.7 / 20),
+// + 2 for the outlying eigenvalues of large SNPs
 static int pcg_iters_model(double dmin, double tau, double tol, bool large) {
-    const double kap = 1.0 + 12.0 / std::max(1e-3, dmin + 1.0 - tau);
+    const double kap = 1.0 + 10.0 / std::max(1e-3, dmin + 1.0 - tau);
     const double q = (std::sqrt(kap) - 1.0) / (std::sqrt(kap) + 1.0);
     return static_cast<int>(std::ceil(std::log(2.0 / tol) / -std::log(q))) + (large ? 2 : 0);
 }
 
+// a device's PCG-route work, accumulated block by block
+struct PcgDev {
+    double front = 0.0, fused = 0.0, chip = 0.0, results = 0.0;
+    int chip_iters = 0;
+    double time() const {
+        if (front == 0.0 && results == 0.0) return 0.0;
+        const double p = std::max({chip, fused, kPcgShare * (chip + fused)}) + chip_iters * kPcgIterFloorUs * 1e-3;
+        return kPcgUnpackMs0 + kPcgGramMs0 + front + p + kPcgRunMs + kPcgDownloadMsPerM * results * 1e-6;
+    }
+};
 struct PcgCost {
-    double ms = 0.0;      // the block's share of a device step
-    int iters = 0;
-    double results = 0.0;
+    double front = 0.0, fused = 0.0, chip = 0.0, results = 0.0;
+    int chip_iters = 0;
+    double ms() const { return front + fused + chip; }   // (the ordering key)
 };
 static PcgCost pcg_block_cost(double m, double ml, double n_ref, int copies, int iters) {
     PcgCost c;
     if (m <= 0) return c;
     const double kp = std::ceil(n_ref / 128.0) * 128.0;
-    const double unpack = m * (std::ceil(n_ref / 4.0) + kp / 4.0) / kUnpackBps * 1e3;
     const double huge_min = kp >= 4096 ? 384.0 : 768.0;
-    const double gram = n_ref * m * (m + 1.0) / (m >= huge_min ? kPcgGramOpsHuge : kPcgGramOpsBig) * 1e3;
-    const double Tb = std::ceil(m / 128.0);
+    c.front = m * (std::ceil(n_ref / 4.0) + kp / 4.0) / kPcgUnpackBps * 1e3 +
+              n_ref * m * (m + 1.0) / (m >= huge_min ? kPcgGramOpsHuge : kPcgGramOpsBig) * 1e3;
+    const double Tb = std::ceil(m / 128.0), Q = std::ceil(m / 64.0);
     const int nc = (copies > 1 && ml > 0) ? copies : 1;   // multi-shift: one column without large SNPs
-    c.iters = iters;
-    c.ms = unpack + gram + iters * (Tb * (Tb + 1.0) / 2.0 * kPcgTileNs + Tb * nc * kPcgRowNs) * 1e-6;
+    if (nc == 1 && Tb <= kPcgFusedTb) {
+        c.fused = iters * Q * (Q + 1.0) / 2.0 * kPcgFusedQuadNs * 1e-6;
+    } else {
+        c.chip = iters * (Tb * (Tb + 1.0) / 2.0 * (1.0 + 0.5 * (nc - 1)) * kPcgTileNs + Tb * nc * kPcgRowNs) * 1e-6;
+        c.chip_iters = iters;
+    }
     c.results = m * copies;
     return c;
 }
 
-// Whole blocks -> devices, longest first onto the least-loaded device.  dev_ms[d] = summed work +
-// the iteration floor of its slowest block + per-run costs.
+// Whole blocks -> devices, longest first onto the device whose predicted step grows least.
 static void plan_units_pcg(int32_t nb, const int32_t* m, const int32_t* ml, int32_t n_ref, int32_t G, int32_t K,
                            const std::vector<int>& iters, std::vector<int32_t>& unit_device,
                            std::vector<double>& dev_ms) {
@@ -285,20 +303,28 @@ static void plan_units_pcg(int32_t nb, const int32_t* m, const int32_t* ml, int3
         cost[b] = pcg_block_cost(m[b], ml ? ml[b] : 0, n_ref, K, iters[b]);
         if (m[b] > 0) order.push_back(b);
     }
-    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cost[x].ms > cost[y].ms; });
-    std::vector<double> load(G, 0.0), res(G, 0.0);
-    std::vector<int> itmax(G, 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cost[x].ms() > cost[y].ms(); });
+    std::vector<PcgDev> dev(G);
+    auto with = [&](PcgDev d, const PcgCost& c) {
+        d.front += c.front;
+        d.fused += c.fused;
+        d.chip += c.chip;
+        d.results += c.results;
+        d.chip_iters = std::max(d.chip_iters, c.chip_iters);
+        return d;
+    };
     for (int32_t b : order) {
-        const int d = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-        load[d] += cost[b].ms;
-        res[d] += cost[b].results;
-        itmax[d] = std::max(itmax[d], cost[b].iters);
-        for (int c = 0; c < K; ++c) unit_device[static_cast<size_t>(b) * K + c] = d;
+        int best = 0;
+        double bt = 0.0;
+        for (int d = 0; d < G; ++d) {
+            const double v = with(dev[d], cost[b]).time();
+            if (d == 0 || v < bt - 1e-12) { best = d; bt = v; }
+        }
+        dev[best] = with(dev[best], cost[b]);
+        for (int c = 0; c < K; ++c) unit_device[static_cast<size_t>(b) * K + c] = best;
     }
     dev_ms.assign(G, 0.0);
-    for (int d = 0; d < G; ++d)
-        dev_ms[d] = load[d] > 0 ? load[d] + itmax[d] * kPcgIterFloorUs * 1e-3 + kPcgRunMs + kPcgDownloadMsPerM * res[d] * 1e-6
-                                : 0.0;
+    for (int d = 0; d < G; ++d) dev_ms[d] = dev[d].time();
 }
 }  // namespace shard
 

@@ -732,7 +732,7 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
 // The small blocks' whole solve in one launch (round 6).  A block with one product column (a
 // multi-shift block, or a single copy) and at most kFTb tile rows on the uint16 Gram is solved by
 // ONE workgroup from the right-hand side to convergence (a persistent grid of one workgroup per CU
-// walks the list, so the chip-wide kernels keep half of every CU): per iteration the block's quadrants are
+// takes the blocks from a counter, so the chip-wide kernels keep half of every CU): per iteration the block's quadrants are
 // streamed once (the 8 x 8 lane sub-blocks and reduce-scatters of quad_mul16, next quadrant in
 // flight), each wave adding its row and column sums into its own LDS copy of y (fixed order, no
 // atomics), then w, the dots, the coefficients, the convergence test and the update exactly as
@@ -1001,9 +1001,17 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
 #define PCG_BLOCK_WAVES 2   // waves per SIMD dbslmm_pcg_block is compiled for (3: 94 VGPRs spilled)
 #endif
 extern "C" __global__ __launch_bounds__(pcg::kThreads) __attribute__((amdgpu_waves_per_eu(PCG_BLOCK_WAVES, 8)))
-void dbslmm_pcg_block(PcgArgs a, const int32_t* __restrict__ list, int32_t n_list, int32_t maxit) {
-    for (int e = blockIdx.x; e < n_list; e += gridDim.x) {   // (the list is biggest first)
+void dbslmm_pcg_block(PcgArgs a, const int32_t* __restrict__ list, int32_t n_list, int32_t* __restrict__ next,
+                      int32_t maxit) {
+    // blocks taken in list order (biggest first) by whichever workgroup is free: the next index from
+    // one counter (zeroed before the launch); which workgroup solves a block never changes its result
+    __shared__ int e_s;
+    for (;;) {
         __syncthreads();                     // (the previous block's LDS readers are done)
+        if (threadIdx.x == 0) e_s = atomicAdd(next, 1);
+        __syncthreads();
+        const int e = e_s;
+        if (e >= n_list) break;
         pcg_block_solve(a, list[e], maxit);
     }
 }

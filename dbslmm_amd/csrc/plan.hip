@@ -280,6 +280,7 @@ struct dbslmm_plan {
     int32_t pcg_run = pcg::kRunMax;  // tiles per product item (pcg_layout)
     bool pcg_fused = true;         // small one-column blocks solved whole by dbslmm_pcg_block
     int32_t* d_pflist = nullptr;   // ... their PcgBlk indices (biggest first)
+    int32_t* d_pfnext = nullptr;   // ... the next list index to take (16 B, zeroed per run)
     int32_t n_pflist = 0;
     std::vector<char> h_pfused;    // per PcgBlk: 1 = in that list
     bool pcg_join = false;         // the main stream still has to wait for dbslmm_pcg_block
@@ -868,7 +869,7 @@ void dbslmm_plan_destroy(dbslmm_plan* p) {
                     p->d_cheb, p->d_coef, p->d_stamps, p->d_slot_order, p->d_tepi, p->d_cheb_items,
                     p->d_tcheb_blocks, p->d_cgrec, p->d_cgconv, p->d_cgit, p->d_G16, p->d_pblk,
                     p->d_pitem, p->d_prow, p->d_pvec, p->d_ppart, p->d_pdot, p->d_pqs, p->d_pcnv,
-                    p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16, p->d_pflist};
+                    p->d_pitb, p->d_pdone, p->d_pact, p->d_off16, p->d_ld16, p->d_pflist, p->d_pfnext};
     for (void* b : bufs)
         if (b) {
             const hipError_t e = hipFree(b);
@@ -2080,6 +2081,7 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     for (int32_t f : flist) p->h_pfused[f] = 1;
     p->n_pflist = static_cast<int32_t>(flist.size());
     if (!flist.empty()) HIP_TRY(ctx, dev_upload(&p->d_pflist, flist, ctx->stream));
+    if (!flist.empty() && !p->d_pfnext) HIP_TRY(ctx, hipMalloc(&p->d_pfnext, 16));
     p->n_pblk = static_cast<int32_t>(blk.size());
     p->n_pitem = static_cast<int32_t>(items.size());
     p->n_prow = static_cast<int32_t>(rows.size());
@@ -2295,8 +2297,9 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
         int per_cu = 1;   // workgroups per CU: the chip-wide kernels of the big blocks keep the rest
         if (const char* e = std::getenv("DBSLMM_PCG_FUSED_WG")) per_cu = std::max(1, std::atoi(e));   // (A/B)
         const int grid = std::max(1, std::min(p->n_pflist, per_cu * ctx->n_cu));
+        HIP_TRY(ctx, hipMemsetAsync(p->d_pfnext, 0, 16, ctx->stream2));
         hipLaunchKernelGGL(dbslmm_pcg_block, dim3(grid), dim3(pcg::kThreads), pcg::block_lds_bytes(), ctx->stream2, a,
-                           p->d_pflist, p->n_pflist, p->pcg_maxit);
+                           p->d_pflist, p->n_pflist, p->d_pfnext, p->pcg_maxit);
         HIP_TRY(ctx, hipGetLastError());
         HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
         p->pcg_join = true;
