@@ -234,18 +234,19 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
 // and copy column, plus a floor per iteration: three dependent launches) -- then the result
 // download.  No block needs splitting: the largest (9.7k SNPs) is ~1 ms of work.  Rates fitted to
 // the round-6 one-GPU rehearsals of configs 3-5 at N = 1, 2, 4, 8 (45 devices:
-// tools/fit_shard_model.py on profiles/r06/shard/dev_c*.json; config 4 every device within 5 %,
-// config 5 12 %, config 3 20 %), iteration counts a priori (pcg_iters_model), DESIGN.md section 6.
-constexpr double kPcgUnpackMs0 = 0.017, kPcgUnpackBps = 4.79e12;     // dwordx4 unpack
-constexpr double kPcgGramMs0 = 0.0745;                               // Gram launches
-constexpr double kPcgGramOpsHuge = 3.06e15, kPcgGramOpsBig = 1.46e15;   // 256- / 128-tile kernels
-constexpr double kPcgFusedQuadNs = 3.19;     // dbslmm_pcg_block: per 64 x 64 quadrant and iteration
-constexpr double kPcgTileNs = 6.47;          // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
-constexpr double kPcgRowNs = 33.6;           // rows + update: per tile row, copy column and iteration
-constexpr double kPcgIterFloorUs = 31.5;     // per chip-wide iteration (launch chain)
-constexpr double kPcgShare = 0.66;           // both paths at once: 0.66 of their summed times
-constexpr double kPcgRunMs = 0.109;          // per run: memsets, init, final, read-back, host
-constexpr double kPcgDownloadMsPerM = 0.774; // per million (SNP, copy) results downloaded + scattered
+// two rehearsals on two boxes, tools/fit_shard_model.py; config 4 devices within 14 % (mean 5 %),
+// config 5 18 % (5 %), config 3 20 % (12 %) -- the rehearsals themselves differ by up to 12 % box to
+// box), iteration counts a priori (pcg_iters_model), DESIGN.md section 6.
+constexpr double kPcgUnpackMs0 = 0.0172, kPcgUnpackBps = 4.70e12;     // dwordx4 unpack
+constexpr double kPcgGramMs0 = 0.0753;                               // Gram launches
+constexpr double kPcgGramOpsHuge = 3.10e15, kPcgGramOpsBig = 1.50e15;   // 256- / 128-tile kernels
+constexpr double kPcgFusedQuadNs = 2.39;     // dbslmm_pcg_block: per 64 x 64 quadrant and iteration
+constexpr double kPcgTileNs = 5.76;          // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
+constexpr double kPcgRowNs = 43.6;           // rows + update: per tile row, copy column and iteration
+constexpr double kPcgIterFloorUs = 32.9;     // per chip-wide iteration (launch chain)
+constexpr double kPcgShare = 0.69;           // both paths at once: 0.66 of their summed times
+constexpr double kPcgRunMs = 0.127;          // per run: memsets, init, final, read-back, host
+constexpr double kPcgDownloadMsPerM = 0.809; // per million (SNP, copy) results downloaded + scattered
 constexpr int kPcgFusedTb = 8;               // pcg::kFTb
 
 // a priori iterations of a block at relative tolerance tol: CG's bound at kappa = 1 + 10 /

@@ -38,10 +38,13 @@ def main(out, cfg=4, ns=(1, 2, 4, 8), only=None):
             for _ in range(3):
                 plan.run_multi(sig, out=o)
             plan.enable_timing(True)
-            t0 = time.perf_counter()
-            for _ in range(5):
-                plan.run_multi(sig, out=o)
-            wall = (time.perf_counter() - t0) / 5 * 1e3
+            batches = []
+            for _ in range(3):                    # the median of three batches of five solves
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    plan.run_multi(sig, out=o)
+                batches.append((time.perf_counter() - t0) / 5 * 1e3)
+            wall = float(np.median(batches))
             ms, n = plan.kernel_ms()
             it = plan.block_iters()
             mine = ud[:, 0] == d
