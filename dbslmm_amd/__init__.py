@@ -211,8 +211,8 @@ class Plan:
         keys = ("snps", "unpack_read_bytes", "unpack_write_bytes", "gram_ops_alg",
                 "gram_ops_exec", "chol_flops_large", "blocks", "gram_tiles", "chol_flops_small",
                 "blocks_large", "chol_flops_tiled", "blocks_tiled", "tiled_launches", "trsv_bytes",
-                "cheb_iters", "cheb_base", "h2f_pass_bytes", "pcg_route", "pcg_iters", "pcg_matrix_bytes",
-                "pcg_partial_bytes", "pcg_flops")
+                "cheb_iters", "cheb_base", "h2f_pass_bytes", "pcg_route", "pcg_iters", "pcg_chip_bytes",
+                "pcg_partial_bytes", "pcg_block_bytes")
         return dict(zip(keys, w.tolist()))
 
     def block_iters(self) -> np.ndarray:

@@ -24,10 +24,10 @@ EXPORTS = (
     "dbslmm_plan_block_iters",
 )
 
-ABI_VERSION = 13
-K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED, K_TRSV, K_PCG = 0, 1, 2, 3, 4, 5, 6
+ABI_VERSION = 14
+K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED, K_TRSV, K_PCG, K_PCG_BLOCK = 0, 1, 2, 3, 4, 5, 6, 7
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram", "dbslmm_chol_large", "dbslmm_chol_small",
-                "dbslmm_tchol", "dbslmm_trsv", "dbslmm_pcg")
+                "dbslmm_tchol", "dbslmm_trsv", "dbslmm_pcg", "dbslmm_pcg_block")
 WORKLOAD_LEN = 22
 BLOCK_OK, BLOCK_EMPTY, BLOCK_NOT_PD, BLOCK_MONOMORPHIC, BLOCK_NOT_CONVERGED = 0, 1, 2, 3, 4
 SOLVER_AUTO, SOLVER_FACTOR, SOLVER_PCG = 0, 1, 2

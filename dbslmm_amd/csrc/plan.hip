@@ -295,7 +295,9 @@ struct dbslmm_plan {
     bool pcg_ran = false;          // the latest run took the PCG route
     bool pcg_pending_var = false;  // ... so the variance needs a factorisation first
     std::vector<char> run_route;   // per pending timed run: 1 = PCG
-    double pcg_bytes = 0.0, pcg_part_bytes = 0.0, pcg_flops = 0.0;   // per iteration (workload)
+    std::vector<double> h_pmat, h_ppart;   // per PcgBlk: lower-triangle bytes (uint16) / partial-sum bytes per iteration
+    std::vector<char> h_pmiss;     // per PcgBlk: missing calls (fp64 Sigma, 4x the matrix bytes)
+    double pcg_cbytes = 0.0, pcg_pbytes = 0.0, pcg_fbytes = 0.0;   // the latest run (workload [19]-[21])
     PcgArgs pcg_args{};            // the arguments of the latest PCG run (continuation chunks)
     hipEvent_t pcg_ev_end = nullptr;   // its timing end event (re-recorded by a continuation)
 };
@@ -1375,10 +1377,11 @@ static int collect_timing(dbslmm_plan* p) {
         float t[kEvPerRun] = {0.f};
         for (int k = 1; k < kEvPerRun; ++k) HIP_TRY(ctx, hipEventElapsedTime(&t[k], e[0], e[k]));
         const float fend = std::max(t[8], t[11]), cstart = std::min(t[8], t[11]);
-        float span[DBSLMM_K_COUNT] = {t[1], t[2] - t[1], t[3] - t[2], t[5] - t[4], fend - t[6], t[7] - cstart, 0.f};
+        float span[DBSLMM_K_COUNT] = {t[1], t[2] - t[1], t[3] - t[2], t[5] - t[4], fend - t[6], t[7] - cstart, 0.f, 0.f};
         if (r < static_cast<int>(p->run_route.size()) && p->run_route[r]) {   // PCG: unpack, Gram, iterations
             for (int k = 2; k < DBSLMM_K_COUNT; ++k) span[k] = 0.f;
             span[DBSLMM_K_PCG] = t[7] - t[2];
+            span[DBSLMM_K_PCG_BLOCK] = t[4] - t[3];   // (inside the PCG span, on the second stream)
         }
         for (int k = 0; k < DBSLMM_K_COUNT; ++k) p->ms_acc[k] += span[k];
         // the lead group's Gram (9 -> 10) sits between the two unpack launches (0 -> 1)
@@ -2034,11 +2037,11 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     using namespace pcg;
     std::vector<PcgBlk> blk;
     std::vector<int32_t> flist;          // blocks solved whole by dbslmm_pcg_block
+    std::vector<double> mat, part;
     std::vector<int4> items;
     std::vector<int2> rows;
     int64_t vo = 0, po = 0, dof = 0;
     int32_t sco = 0;
-    double bytes = 0.0, pbytes = 0.0, flops = 0.0;
     const double esz = p->pcg_g16 ? 2.0 : 8.0;
     // tiles per product item: one (measured at config 4: 10.65 / 10.90 / 11.13 / 11.34 ms per step
     // at 1 / 2 / 4 / 8, and the N = 8 shards' product 114 -> ~45 us: many short items keep more
@@ -2066,10 +2069,12 @@ static int pcg_layout(dbslmm_plan* p, int n) {
             rows.push_back(int2{bi, I});
             for (int J0 = 0; J0 <= I; J0 += run) items.push_back(int4{bi, I, J0, std::min(I, J0 + run - 1)});
         }
-        bytes += 0.5 * m * (m + 1.0) * esz;
-        flops += 4.0 * nc * 0.5 * m * (m + 1.0);
-        // partials written and read once: a column slot per tile (I, J <= I), a row slot per run
-        pbytes += 2.0 * 8.0 * nc * kT * (0.5 * Tb * (Tb + 1.0) + Tb * 0.5 * (nrun + 1.0));
+        // per iteration: the lower triangle in its storage; partials written and read once (a column
+        // slot per tile (I, J <= I), a row slot per run; none for a block solved whole)
+        mat.push_back(0.5 * m * (m + 1.0) * esz);
+        double runs = 0.0;
+        for (int I = 0; I < Tb; ++I) runs += I / run + 1;
+        part.push_back(fused ? 0.0 : 2.0 * 8.0 * nc * kT * (0.5 * Tb * (Tb + 1.0) + runs));
     }
     // biggest blocks' items first (their tile rows are the longest runs of work); the items of the
     // blocks dbslmm_pcg_block solves last (they return at once unless the block has missing calls)
@@ -2086,9 +2091,8 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     p->n_pitem = static_cast<int32_t>(items.size());
     p->n_prow = static_cast<int32_t>(rows.size());
     p->pcg_vstride = vo;
-    p->pcg_bytes = bytes;
-    p->pcg_part_bytes = pbytes;
-    p->pcg_flops = flops;
+    p->h_pmat = mat;
+    p->h_ppart = part;
     HIP_TRY(ctx, dev_upload(&p->d_pblk, blk, ctx->stream));
     HIP_TRY(ctx, dev_upload(&p->d_pitem, items, ctx->stream));
     HIP_TRY(ctx, dev_upload(&p->d_prow, rows, ctx->stream));
@@ -2164,7 +2168,24 @@ static int pcg_finish(dbslmm_plan* p) {
                 std::vector<int32_t> fl(std::max(1, p->n_nonempty));
                 HIP_TRY(ctx, hipMemcpy(fl.data(), p->d_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
                 p->pcg_m_blocks = 0;
-                for (int b = 0; b < p->n_nonempty; ++b) p->pcg_m_blocks += fl[b] & 1;
+                p->h_pmiss.assign(p->n_pblk, 0);
+                for (int b = 0; b < p->n_nonempty; ++b) {
+                    p->pcg_m_blocks += fl[b] & 1;
+                    if (b < p->n_pblk) p->h_pmiss[b] = fl[b] & 1;
+                }
+            }
+            // bytes the run streamed: every block its own iteration count
+            p->pcg_cbytes = p->pcg_pbytes = p->pcg_fbytes = 0.0;
+            for (int b = 0; b < p->n_pblk && b < static_cast<int>(p->h_pmat.size()); ++b) {
+                const double it = p->h_pmon[1 + b];
+                const bool miss = !p->h_pmiss.empty() && p->h_pmiss[b];
+                const double mb = p->h_pmat[b] * (miss && p->pcg_g16 ? 4.0 : 1.0);
+                if (!p->h_pfused.empty() && p->h_pfused[b] && !miss) {
+                    p->pcg_fbytes += it * mb;
+                } else {
+                    p->pcg_cbytes += it * mb;
+                    p->pcg_pbytes += it * p->h_ppart[b];
+                }
             }
             break;
         }
@@ -2244,7 +2265,7 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
                            p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
                            p->d_mu, p->d_rsd, nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
     HIP_TRY(ctx, hipGetLastError());
-    if (ev) for (int k : {2, 3, 4, 5, 6, 8, 11}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
+    if (ev) for (int k : {2, 5, 6, 8, 11}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
     PcgArgs a{};
     a.blk = p->d_pblk;
     a.G16 = g16;
@@ -2294,6 +2315,7 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
     if (p->n_pflist > 0) {   // the small blocks' whole solves beside the chip-wide iterations
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], ctx->stream2));   // dbslmm_pcg_block's span: 3 -> 4
         int per_cu = 1;   // workgroups per CU: the chip-wide kernels of the big blocks keep the rest
         if (const char* e = std::getenv("DBSLMM_PCG_FUSED_WG")) per_cu = std::max(1, std::atoi(e));   // (A/B)
         const int grid = std::max(1, std::min(p->n_pflist, per_cu * ctx->n_cu));
@@ -2301,8 +2323,11 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
         hipLaunchKernelGGL(dbslmm_pcg_block, dim3(grid), dim3(pcg::kThreads), pcg::block_lds_bytes(), ctx->stream2, a,
                            p->d_pflist, p->n_pflist, p->d_pfnext, p->pcg_maxit);
         HIP_TRY(ctx, hipGetLastError());
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ctx->stream2));
         HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->stream2));
         p->pcg_join = true;
+    } else if (ev) {
+        for (int k : {3, 4}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
     }
     p->pcg_it = 0;
     p->pcg_pending = true;
@@ -2825,9 +2850,9 @@ int dbslmm_plan_workload(const dbslmm_plan* p, double* out) {
     for (int i = 0; i < DBSLMM_WORKLOAD_LEN; ++i) out[i] = p->wl[i];
     out[17] = p->pcg_ran ? 1.0 : 0.0;
     out[18] = p->pcg_ran ? p->pcg_iters_max : 0.0;
-    out[19] = p->pcg_ran ? p->pcg_bytes : 0.0;
-    out[20] = p->pcg_ran ? p->pcg_part_bytes : 0.0;
-    out[21] = p->pcg_ran ? p->pcg_flops : 0.0;
+    out[19] = p->pcg_ran ? p->pcg_cbytes : 0.0;
+    out[20] = p->pcg_ran ? p->pcg_pbytes : 0.0;
+    out[21] = p->pcg_ran ? p->pcg_fbytes : 0.0;
     if (p->cg_ran && p->d_cgit) {   // the passes each tiled block ran before it converged (run_multi is synchronous)
         std::vector<int32_t> it(std::max(1, p->n_nonempty));
         if (hipSetDevice(p->ctx->device) != hipSuccess ||

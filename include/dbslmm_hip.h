@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 13
+#define DBSLMM_ABI_VERSION 14
 
 enum {
     DBSLMM_OK = 0,
@@ -210,7 +210,9 @@ enum {
                                  tiled blocks on the base copy's factor (run_multi; 0 otherwise) */
     DBSLMM_K_PCG = 6,         /* dbslmm_pcg_*: the PCG route's iterations (init to final; 0 on the
                                  factorisation route) */
-    DBSLMM_K_COUNT = 7
+    DBSLMM_K_PCG_BLOCK = 7,   /* dbslmm_pcg_block: the small blocks solved whole (ABI 14; runs on a
+                                 second stream inside the K_PCG span) */
+    DBSLMM_K_COUNT = 8
 };
 
 int dbslmm_abi_version(void);
@@ -328,9 +330,10 @@ int dbslmm_plan_kernel_ms(dbslmm_plan* plan, double* ms_out /*[DBSLMM_K_COUNT]*/
  * iterations of the latest run_multi (0: none; with CG their cap), [15] its base copy (-1: none),
  * [16] factor bytes its h2f passes read (CG: each tiled block's own iteration count),
  * [17] 1 when the latest run took the PCG route, [18] its iterations (the slowest block),
- * [19] bytes one PCG iteration's product streams (the blocks' lower-triangle LD matrices in their
- * storage: uint16 integer Gram / fp64 Sigma), [20] its partial-sum bytes (written + read once),
- * [21] the product's fp64 flops per iteration (2 per stored element and copy, both directions). */
+ * [19] the lower-triangle LD matrix bytes the chip-wide PCG kernels streamed in that run (in their
+ * storage: uint16 integer Gram / fp64 Sigma; every block times its own iterations), [20] their
+ * partial-sum bytes (written + read once), [21] the same matrix bytes of the blocks
+ * dbslmm_pcg_block solved whole (ABI 14; before: per-iteration figures). */
 #define DBSLMM_WORKLOAD_LEN 22
 int dbslmm_plan_workload(const dbslmm_plan* plan, double* out /*[DBSLMM_WORKLOAD_LEN]*/);
 /* PCG iterations of each block in the latest run (ABI 13): iters[b] (num_block entries) = the
