@@ -738,8 +738,8 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
 // atomics), then w, the dots, the coefficients, the convergence test and the update exactly as
 // dbslmm_pcg_rows / dbslmm_pcg_update compute them -- with no partial slots, no per-iteration
 // launches and no hand-off between workgroups.  Thread t owns slots t + 256 q (q < kFPer): r, s
-// and w in registers, x and p of every copy in the block's global vectors (private to this
-// workgroup); U = rsd o u in LDS.  The chip-wide kernels skip these blocks (init marks them
+// and w in registers, U = rsd o u and x and p of every copy in LDS (x goes to the block's global
+// vectors at the end).  The chip-wide kernels skip these blocks (init marks them
 // done = 3); dbslmm_pcg_final writes their betas and status from x and cnv as for the others.
 // ------------------------------------------------------------------------------------------
 namespace pcg {
@@ -756,8 +756,12 @@ __device__ __forceinline__ void block_sum(double (&v)[N], double* red, int tid) 
 #pragma unroll
     for (int k = 0; k < N; ++k) v[k] = ((red[k] + red[N + k]) + red[2 * N + k]) + red[3 * N + k];
 }
-// LDS: y per wave, U, the block_sum scratch, the recurrence state and flags
-constexpr size_t block_lds_bytes() { return sizeof(double) * (5 * kFRows + 4 * (3 + kMaxNC) + 12 + 3 * kMaxNC + 4); }
+// LDS of n copies: y per wave, U, x and p of every copy, the block_sum scratch, the recurrence
+// state and flags (56 / 88 KB at 1 / 3 copies: one workgroup per CU, and at 3 copies still room
+// for a chip-wide product workgroup, 64 KB, beside it)
+constexpr size_t block_lds_bytes(int n) {
+    return sizeof(double) * ((5 + 2 * n) * kFRows + 4 * (3 + kMaxNC) + 12 + 3 * kMaxNC + 4);
+}
 }  // namespace pcg
 
 __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_t maxit) {
@@ -765,11 +769,14 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
     extern __shared__ double blds[];
     double* yw = blds;                       // [4][kFRows] per-wave product sums
     double* Ul = blds + 4 * kFRows;          // [kFRows] rsd o u
-    double* red = Ul + kFRows;               // block_sum scratch
+    const int n = a.ncopy;
+    double* Xl = Ul + kFRows;                // [copy][kFRows] x (to global at the end)
+    double* Pl = Xl + n * kFRows;            // [copy][kFRows] p
+    double* red = Pl + n * kFRows;           // block_sum scratch
     if (a.done[bi] != 3) return;             // (monomorphic, or missing calls: the chip-wide path)
     const PcgBlk B = a.blk[bi];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = a.ncopy, m = B.m, Tb = B.Tb;
+    const int m = B.m, Tb = B.Tb;
     const bool msh = B.mshift != 0;
     const double dc = col_shift(a, B, 0);    // the product column's shift (the seed's on a multi-shift block)
     // ---- state: x = p = 0, r = z, s = w = 0, U = rsd o r / diag
@@ -786,7 +793,8 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
             sg[0] += a.S[B.row0 + i] * u;
         }
         Ul[i] = u;                           // (zero past m)
-        for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;   // (x = p = 0: dbslmm_pcg_init)
+        for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;
+        for (int c = 0; c < n; ++c) Xl[c * kFRows + i] = Pl[c * kFRows + i] = 0.0;
     }
     block_sum(sg, red, tid);
     double sig = sg[0];
@@ -901,7 +909,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
                 d[1] += w * u;
                 d[2] += r[q] * r[q];
                 for (int c = 0; c < n; ++c) {
-                    const double xv = a.X[c * a.vstride + B.vo + i];
+                    const double xv = Xl[c * kFRows + i];
                     d[3 + c] += xv * xv;
                 }
             }
@@ -966,10 +974,10 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
             if (msh) {
                 for (int c = 0; c < n; ++c) {
                     if (flag[c]) continue;
-                    const int64_t o = c * a.vstride + B.vo + i;
-                    const double pv = __builtin_fma(st[12 + 3 * c + 1], a.P[o], st[12 + 3 * c + 2] * r[q]);
-                    a.P[o] = pv;
-                    a.X[o] = __builtin_fma(st[12 + 3 * c], pv, a.X[o]);
+                    const int o = c * kFRows + i;
+                    const double pv = __builtin_fma(st[12 + 3 * c + 1], Pl[o], st[12 + 3 * c + 2] * r[q]);
+                    Pl[o] = pv;
+                    Xl[o] = __builtin_fma(st[12 + 3 * c], pv, Xl[o]);
                 }
                 const double sn = __builtin_fma(be, sv[q], wv[q]);
                 rn = __builtin_fma(-al, sn, r[q]);
@@ -977,13 +985,12 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
                 r[q] = rn;
                 Ul[i] = rn * rsd_i;
             } else {
-                const int64_t o = B.vo + i;
                 const double dg = jdiag(a, B, i, dc);
                 const double u = r[q] / dg;
-                const double pv = __builtin_fma(be, a.P[o], u);
+                const double pv = __builtin_fma(be, Pl[i], u);
                 const double sn = __builtin_fma(be, sv[q], wv[q]);
-                a.P[o] = pv;
-                a.X[o] = __builtin_fma(al, pv, a.X[o]);
+                Pl[i] = pv;
+                Xl[i] = __builtin_fma(al, pv, Xl[i]);
                 rn = __builtin_fma(-al, sn, r[q]);
                 sv[q] = sn;
                 r[q] = rn;
@@ -993,6 +1000,13 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
         }
         block_sum(sg2, red, tid);
         sig = sg2[0];
+    }
+    // x to the block's global vectors (dbslmm_pcg_final reads it); each thread its own rows
+#pragma unroll
+    for (int q = 0; q < kFPer; ++q) {
+        const int i = tid + kThreads * q;
+        if (i < m)
+            for (int c = 0; c < n; ++c) a.X[c * a.vstride + B.vo + i] = Xl[c * kFRows + i];
     }
     if (tid == 0) a.itb[bi] = it + (it < maxit ? 1 : 0);
 }

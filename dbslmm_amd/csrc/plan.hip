@@ -750,6 +750,9 @@ int dbslmm_ctx_create(int device, dbslmm_ctx** out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gram::kLdsBytes) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_gram_huge),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, gram::kHLdsBytes) == hipSuccess &&
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_pcg_block),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(pcg::block_lds_bytes(pcg::kMaxNC))) == hipSuccess &&
             hipFuncSetAttribute(reinterpret_cast<const void*>(dbslmm_tchol_region),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 static_cast<int>(kRegionLds)) == hipSuccess &&
@@ -2252,19 +2255,27 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
     if (ev) for (int k : {1, 9, 10}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
     uint16_t* g16 = p->pcg_g16 ? p->d_G16 : nullptr;
     const double nrd = static_cast<double>(p->n_ref), padk = static_cast<double>(p->kpad - p->n_ref);
-    if (p->n_htiles > 0)
-        hipLaunchKernelGGL(dbslmm_gram_huge, dim3(p->n_htiles), dim3(512), gram::kHLdsBytes, s, p->d_G, p->kpad,
-                           p->d_htiles, p->n_htiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
-                           p->d_mu, p->d_rsd, nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
-    if (p->n_tiles > 0)
-        hipLaunchKernelGGL(dbslmm_gram_i8, dim3((p->n_tiles + 3) / 4), dim3(256), 0, s, p->d_G, p->kpad, p->d_tiles,
-                           p->n_tiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd,
-                           nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
-    if (p->n_btiles > 0)
-        hipLaunchKernelGGL(dbslmm_gram_big, dim3(p->n_btiles), dim3(256), gram::kLdsBytes, s, p->d_G, p->kpad,
-                           p->d_btiles, p->n_btiles, p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S,
-                           p->d_mu, p->d_rsd, nrd, padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
-    HIP_TRY(ctx, hipGetLastError());
+    // the Gram of tile lists (i8, big, huge) on stream st
+    auto gram = [&](hipStream_t st, const GramTile* ti, int32_t nt, const GramTile* tb, int32_t nb,
+                    const GramTile* th, int32_t nh) {
+        if (nh > 0)
+            hipLaunchKernelGGL(dbslmm_gram_huge, dim3(nh), dim3(512), gram::kHLdsBytes, st, p->d_G, p->kpad, th, nh,
+                               p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd, nrd,
+                               padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
+        if (nt > 0)
+            hipLaunchKernelGGL(dbslmm_gram_i8, dim3((nt + 3) / 4), dim3(256), 0, st, p->d_G, p->kpad, ti, nt, p->d_row0,
+                               p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd, nrd, padk, p->tau,
+                               p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
+        if (nb > 0)
+            hipLaunchKernelGGL(dbslmm_gram_big, dim3(nb), dim3(256), gram::kLdsBytes, st, p->d_G, p->kpad, tb, nb,
+                               p->d_row0, p->d_m, p->d_ld, p->d_matoff, p->d_flags, p->d_S, p->d_mu, p->d_rsd, nrd,
+                               padk, p->tau, p->d_M, 1, p->M_elems, INT32_MAX, -1, g16, p->d_off16, p->d_ld16);
+        return hipGetLastError();
+    };
+    // (Measured and dropped: the Gram of the blocks dbslmm_pcg_block solves on the second stream
+    // beside the chip-wide iterations -- its 256-tile workgroups hold 128 KiB of LDS, so the product
+    // items cannot run beside them: config 4 8.8 -> 9.6 ms.)
+    HIP_TRY(ctx, gram(s, p->d_tiles, p->n_tiles, p->d_btiles, p->n_btiles, p->d_htiles, p->n_htiles));
     if (ev) for (int k : {2, 5, 6, 8, 11}) HIP_TRY(ctx, hipEventRecord(ev[k], s));
     PcgArgs a{};
     a.blk = p->d_pblk;
@@ -2316,11 +2327,11 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
         HIP_TRY(ctx, hipEventRecord(ctx->fork, s));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], ctx->stream2));   // dbslmm_pcg_block's span: 3 -> 4
-        int per_cu = 1;   // workgroups per CU: the chip-wide kernels of the big blocks keep the rest
-        if (const char* e = std::getenv("DBSLMM_PCG_FUSED_WG")) per_cu = std::max(1, std::atoi(e));   // (A/B)
-        const int grid = std::max(1, std::min(p->n_pflist, per_cu * ctx->n_cu));
+        // one workgroup per CU (its LDS holds x and p: one fits): the chip-wide kernels of the
+        // other blocks keep the rest of every CU
+        const int grid = std::max(1, std::min(p->n_pflist, ctx->n_cu));
         HIP_TRY(ctx, hipMemsetAsync(p->d_pfnext, 0, 16, ctx->stream2));
-        hipLaunchKernelGGL(dbslmm_pcg_block, dim3(grid), dim3(pcg::kThreads), pcg::block_lds_bytes(), ctx->stream2, a,
+        hipLaunchKernelGGL(dbslmm_pcg_block, dim3(grid), dim3(pcg::kThreads), pcg::block_lds_bytes(n), ctx->stream2, a,
                            p->d_pflist, p->n_pflist, p->d_pfnext, p->pcg_maxit);
         HIP_TRY(ctx, hipGetLastError());
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], ctx->stream2));
