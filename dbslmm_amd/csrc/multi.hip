@@ -229,8 +229,8 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
 
 // ---------------------------------------------------------------- time model, PCG route
 // On the PCG route (pcg.hip) a device runs one sequence: unpack + Gram of its blocks, then two
-// concurrent paths -- dbslmm_pcg_block solving its small one-column blocks whole (cost per
-// quadrant and iteration) and the chip-wide iterations of the others (per tile and per tile row
+// concurrent paths -- dbslmm_pcg_block solving its blocks of <= 8 tile rows whole (cost per
+// quadrant, iteration and sequence) and the chip-wide iterations of the others (per tile and per tile row
 // and copy column, plus a floor per iteration: three dependent launches) -- then the result
 // download.  No block needs splitting: the largest (9.7k SNPs) is ~1 ms of work.  Rates fitted to
 // the round-6 one-GPU rehearsals of configs 3-5 at N = 1, 2, 4, 8 (45 devices:
@@ -282,8 +282,8 @@ static PcgCost pcg_block_cost(double m, double ml, double n_ref, int copies, int
               n_ref * m * (m + 1.0) / (m >= huge_min ? kPcgGramOpsHuge : kPcgGramOpsBig) * 1e3;
     const double Tb = std::ceil(m / 128.0), Q = std::ceil(m / 64.0);
     const int nc = (copies > 1 && ml > 0) ? copies : 1;   // multi-shift: one column without large SNPs
-    if (nc == 1 && Tb <= kPcgFusedTb) {
-        c.fused = iters * Q * (Q + 1.0) / 2.0 * kPcgFusedQuadNs * 1e-6;
+    if (Tb <= kPcgFusedTb) {   // one sequence per product column, each its own workgroup
+        c.fused = nc * iters * Q * (Q + 1.0) / 2.0 * kPcgFusedQuadNs * 1e-6;
     } else {
         c.chip = iters * (Tb * (Tb + 1.0) / 2.0 * (1.0 + 0.5 * (nc - 1)) * kPcgTileNs + Tb * nc * kPcgRowNs) * 1e-6;
         c.chip_iters = iters;

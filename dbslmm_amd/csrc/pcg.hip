@@ -76,8 +76,8 @@ struct PcgBlk {
                                     // columns past m stay zero: no masks in the product)
     int32_t nc;                     // product columns: 1 (multi-shift block) or the copies
     int32_t mshift;                 // 1: no large SNP and several copies -> one Krylov sequence
-    int32_t fused;                  // 1: one product column and <= kFTb tile rows -- on the uint16
-                                    // Gram the whole solve runs in dbslmm_pcg_block (done = 3)
+    int32_t fused;                  // 1: <= kFTb tile rows -- on the uint16 Gram the whole solve
+                                    // runs in dbslmm_pcg_block (done = 3), one entry per sequence
     int32_t pad_;
 };
 
@@ -729,9 +729,9 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
 }
 
 // ------------------------------------------------------------------------------------------
-// The small blocks' whole solve in one launch (round 6).  A block with one product column (a
-// multi-shift block, or a single copy) and at most kFTb tile rows on the uint16 Gram is solved by
-// ONE workgroup from the right-hand side to convergence (a persistent grid of one workgroup per CU
+// The small blocks' whole solve in one launch (round 6).  A block of at most kFTb tile rows on the
+// uint16 Gram is solved by ONE workgroup per Krylov sequence (a multi-shift block: one for every
+// copy; a block with large SNPs: one per copy) from the right-hand side to convergence (a persistent grid of one workgroup per CU
 // takes the blocks from a counter, so the chip-wide kernels keep half of every CU): per iteration the block's quadrants are
 // streamed once (the 8 x 8 lane sub-blocks and reduce-scatters of quad_mul16, next quadrant in
 // flight), each wave adding its row and column sums into its own LDS copy of y (fixed order, no
@@ -764,7 +764,10 @@ constexpr size_t block_lds_bytes(int n) {
 }
 }  // namespace pcg
 
-__device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_t maxit) {
+// One list entry: block bi, copy cc (-1: a multi-shift block, every copy in one sequence; else one
+// copy's own Jacobi-preconditioned sequence -- a block with large SNPs and several copies has one
+// entry per copy, each on its own workgroup).
+__device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc, int32_t maxit) {
     using namespace pcg;
     extern __shared__ double blds[];
     double* yw = blds;                       // [4][kFRows] per-wave product sums
@@ -777,8 +780,9 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
     const PcgBlk B = a.blk[bi];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m = B.m, Tb = B.Tb;
-    const bool msh = B.mshift != 0;
-    const double dc = col_shift(a, B, 0);    // the product column's shift (the seed's on a multi-shift block)
+    const bool msh = cc < 0;
+    const int nx = msh ? n : 1;              // copies of x this sequence yields
+    const double dc = msh ? col_shift(a, B, 0) : a.dshift[cc];   // the sequence's shift (the seed's: multi-shift)
     // ---- state: x = p = 0, r = z, s = w = 0, U = rsd o r / diag
     double r[kFPer], sv[kFPer], wv[kFPer], sg[1] = {0.0};
 #pragma unroll
@@ -794,7 +798,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
         }
         Ul[i] = u;                           // (zero past m)
         for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;
-        for (int c = 0; c < n; ++c) Xl[c * kFRows + i] = Pl[c * kFRows + i] = 0.0;
+        for (int c = 0; c < nx; ++c) Xl[c * kFRows + i] = Pl[c * kFRows + i] = 0.0;
     }
     block_sum(sg, red, tid);
     double sig = sg[0];
@@ -908,7 +912,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
                 d[0] += r[q] * u;
                 d[1] += w * u;
                 d[2] += r[q] * r[q];
-                for (int c = 0; c < n; ++c) {
+                for (int c = 0; c < nx; ++c) {
                     const double xv = Xl[c * kFRows + i];
                     d[3 + c] += xv * xv;
                 }
@@ -946,11 +950,11 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
                     running += flag[c] ? 0 : 1;
                 }
             } else {                          // one copy (n = 1), Jacobi-preconditioned
-                const double lam = B.ms == B.m ? a.dshift[0] + 1.0 - a.tau : 1.0 - a.tau;
+                const double lam = B.ms == B.m ? dc + 1.0 - a.tau : 1.0 - a.tau;
                 const double t = a.tol * lam;
                 if (rr == 0.0 || rr <= t * t * d[3]) {
                     flag[0] = 1;
-                    a.cnv[B.sco] = it + 1;
+                    a.cnv[B.sco + cc] = it + 1;
                 }
                 running = flag[0] ? 0 : 1;
             }
@@ -1006,16 +1010,16 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int32_
     for (int q = 0; q < kFPer; ++q) {
         const int i = tid + kThreads * q;
         if (i < m)
-            for (int c = 0; c < n; ++c) a.X[c * a.vstride + B.vo + i] = Xl[c * kFRows + i];
+            for (int c = 0; c < nx; ++c) a.X[(msh ? c : cc) * a.vstride + B.vo + i] = Xl[c * kFRows + i];
     }
-    if (tid == 0) a.itb[bi] = it + (it < maxit ? 1 : 0);
+    if (tid == 0) atomicMax(a.itb + bi, it + (it < maxit ? 1 : 0));   // (several copies: the slowest)
 }
 
 #ifndef PCG_BLOCK_WAVES
 #define PCG_BLOCK_WAVES 2   // waves per SIMD dbslmm_pcg_block is compiled for (3: 94 VGPRs spilled)
 #endif
 extern "C" __global__ __launch_bounds__(pcg::kThreads) __attribute__((amdgpu_waves_per_eu(PCG_BLOCK_WAVES, 8)))
-void dbslmm_pcg_block(PcgArgs a, const int32_t* __restrict__ list, int32_t n_list, int32_t* __restrict__ next,
+void dbslmm_pcg_block(PcgArgs a, const int2* __restrict__ list, int32_t n_list, int32_t* __restrict__ next,
                       int32_t maxit) {
     // blocks taken in list order (biggest first) by whichever workgroup is free: the next index from
     // one counter (zeroed before the launch); which workgroup solves a block never changes its result
@@ -1026,7 +1030,7 @@ void dbslmm_pcg_block(PcgArgs a, const int32_t* __restrict__ list, int32_t n_lis
         __syncthreads();
         const int e = e_s;
         if (e >= n_list) break;
-        pcg_block_solve(a, list[e], maxit);
+        pcg_block_solve(a, list[e].x, list[e].y, maxit);
     }
 }
 

@@ -277,12 +277,15 @@ struct dbslmm_plan {
     int4* d_pitem = nullptr;
     int2* d_prow = nullptr;
     int32_t n_pblk = 0, n_pitem = 0, n_prow = 0;
+    int32_t n_pitem_chip = 0, n_prow_chip = 0;   // ... of them, those of the chip-wide blocks (listed first)
+    bool pcg_trim = false;         // launch only those: no block dbslmm_pcg_block takes has missing calls
     int32_t pcg_run = pcg::kRunMax;  // tiles per product item (pcg_layout)
     bool pcg_fused = true;         // small one-column blocks solved whole by dbslmm_pcg_block
-    int32_t* d_pflist = nullptr;   // ... their PcgBlk indices (biggest first)
+    int2* d_pflist = nullptr;      // ... their (PcgBlk, copy) sequences (biggest first)
     int32_t* d_pfnext = nullptr;   // ... the next list index to take (16 B, zeroed per run)
     int32_t n_pflist = 0;
     std::vector<char> h_pfused;    // per PcgBlk: 1 = in that list
+    std::vector<int32_t> h_pnseq;  // ... its sequences there (1, or the copies with large SNPs)
     bool pcg_join = false;         // the main stream still has to wait for dbslmm_pcg_block
     double *d_pvec = nullptr, *d_ppart = nullptr, *d_pdot = nullptr, *d_pqs = nullptr;
     int32_t *d_pcnv = nullptr, *d_pitb = nullptr, *d_pdone = nullptr, *d_pact = nullptr;
@@ -2037,9 +2040,10 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     for (void* q : old)
         if (q) (void)hipFree(q);
     p->d_pflist = nullptr;               // (uploaded below only when some block is solved whole)
+    p->pcg_trim = false;                 // (until a run of this layout has read the flags)
     using namespace pcg;
     std::vector<PcgBlk> blk;
-    std::vector<int32_t> flist;          // blocks solved whole by dbslmm_pcg_block
+    std::vector<int2> flist;             // (block, copy) sequences solved whole by dbslmm_pcg_block
     std::vector<double> mat, part;
     std::vector<int4> items;
     std::vector<int2> rows;
@@ -2058,10 +2062,14 @@ static int pcg_layout(dbslmm_plan* p, int n) {
         // (multi-shift CG, one product column); with large SNPs each copy iterates on its own
         const bool msh = n > 1 && p->h_ms[b] == m;
         const int32_t nc = msh ? 1 : n;
-        const bool fused = p->pcg_fused && nc == 1 && Tb <= kFTb && !p->h_off16.empty();
+        const bool fused = p->pcg_fused && Tb <= kFTb && !p->h_off16.empty();
         PcgBlk k{b, p->h_row0[b], m, p->h_ms[b], p->h_ld[b], Tb, Tb + nrun, sco, p->h_matoff[b], vo, po, dof,
                  p->h_off16.empty() ? 0 : p->h_off16[b], nc, msh ? 1 : 0, fused ? 1 : 0, 0};
-        if (fused) flist.push_back(static_cast<int32_t>(blk.size()));
+        if (fused) {   // one entry per Krylov sequence: copy -1 = every copy (multi-shift, or one copy)
+            const int32_t bi = static_cast<int32_t>(blk.size());
+            if (nc == 1) flist.push_back(int2{bi, msh ? -1 : 0});
+            else for (int c = 0; c < nc; ++c) flist.push_back(int2{bi, c});
+        }
         const int bi = static_cast<int>(blk.size());
         blk.push_back(k);
         vo += static_cast<int64_t>(Tb) * kT;
@@ -2084,9 +2092,19 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     std::stable_sort(items.begin(), items.end(), [&](const int4& x, const int4& y) {
         return blk[x.x].fused != blk[y.x].fused ? blk[x.x].fused < blk[y.x].fused : blk[x.x].Tb > blk[y.x].Tb;
     });
-    std::stable_sort(flist.begin(), flist.end(), [&](int32_t x, int32_t y) { return blk[x].Tb > blk[y].Tb; });
+    std::stable_sort(flist.begin(), flist.end(), [&](const int2& x, const int2& y) { return blk[x.x].Tb > blk[y.x].Tb; });
+    // tile rows of those blocks last too: once no such block turns out to have missing calls, the
+    // chip-wide launches stop short of them (pcg_iters)
+    std::stable_sort(rows.begin(), rows.end(), [&](const int2& x, const int2& y) { return blk[x.x].fused < blk[y.x].fused; });
+    p->n_prow_chip = p->n_pitem_chip = 0;
+    for (const int2& r : rows) p->n_prow_chip += blk[r.x].fused ? 0 : 1;
+    for (const int4& e : items) p->n_pitem_chip += blk[e.x].fused ? 0 : 1;
     p->h_pfused.assign(blk.size(), 0);
-    for (int32_t f : flist) p->h_pfused[f] = 1;
+    p->h_pnseq.assign(blk.size(), 0);
+    for (const int2& f : flist) {
+        p->h_pfused[f.x] = 1;
+        p->h_pnseq[f.x] += 1;
+    }
     p->n_pflist = static_cast<int32_t>(flist.size());
     if (!flist.empty()) HIP_TRY(ctx, dev_upload(&p->d_pflist, flist, ctx->stream));
     if (!flist.empty() && !p->d_pfnext) HIP_TRY(ctx, hipMalloc(&p->d_pfnext, 16));
@@ -2129,15 +2147,17 @@ static int pcg_iters(dbslmm_plan* p, int K) {
     dbslmm_ctx* ctx = p->ctx;
     hipStream_t s = ctx->stream;
     for (int k = 0; k < K; ++k) {
-        const dim3 g((p->n_pitem + pcg::kWaves - 1) / pcg::kWaves);
+        const int32_t ni = p->pcg_trim ? p->n_pitem_chip : p->n_pitem, nr = p->pcg_trim ? p->n_prow_chip : p->n_prow;
+        if (ni == 0 && nr == 0) continue;
+        const dim3 g((std::max(1, ni) + pcg::kWaves - 1) / pcg::kWaves);
         if (p->pcg_g16)
             hipLaunchKernelGGL(dbslmm_pcg_symv16, g, dim3(pcg::kThreads), pcg::lds_bytes(p->pcg_n), s, p->pcg_args,
-                               p->d_pitem, p->n_pitem);
+                               p->d_pitem, ni);
         if (!p->pcg_g16 || p->pcg_m_blocks != 0)   // (-1: not known yet)
             hipLaunchKernelGGL(dbslmm_pcg_symv64, g, dim3(pcg::kThreads), pcg::lds_bytes(p->pcg_n), s, p->pcg_args,
-                               p->d_pitem, p->n_pitem);
-        hipLaunchKernelGGL(dbslmm_pcg_rows, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
-        hipLaunchKernelGGL(dbslmm_pcg_update, dim3(p->n_prow), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
+                               p->d_pitem, ni);
+        hipLaunchKernelGGL(dbslmm_pcg_rows, dim3(std::max(1, nr)), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
+        hipLaunchKernelGGL(dbslmm_pcg_update, dim3(std::max(1, nr)), dim3(pcg::kThreads), 0, s, p->pcg_args, p->d_prow);
     }
     HIP_TRY(ctx, hipGetLastError());
     p->pcg_it += K;
@@ -2177,6 +2197,9 @@ static int pcg_finish(dbslmm_plan* p) {
                     if (b < p->n_pblk) p->h_pmiss[b] = fl[b] & 1;
                 }
             }
+            p->pcg_trim = true;   // (the fused flags are those of the current layout)
+            for (int b = 0; b < p->n_pblk && b < static_cast<int>(p->h_pfused.size()); ++b)
+                if (p->h_pfused[b] && p->h_pmiss[b]) p->pcg_trim = false;
             // bytes the run streamed: every block its own iteration count
             p->pcg_cbytes = p->pcg_pbytes = p->pcg_fbytes = 0.0;
             for (int b = 0; b < p->n_pblk && b < static_cast<int>(p->h_pmat.size()); ++b) {
@@ -2184,7 +2207,7 @@ static int pcg_finish(dbslmm_plan* p) {
                 const bool miss = !p->h_pmiss.empty() && p->h_pmiss[b];
                 const double mb = p->h_pmat[b] * (miss && p->pcg_g16 ? 4.0 : 1.0);
                 if (!p->h_pfused.empty() && p->h_pfused[b] && !miss) {
-                    p->pcg_fbytes += it * mb;
+                    p->pcg_fbytes += it * mb * p->h_pnseq[b];
                 } else {
                     p->pcg_cbytes += it * mb;
                     p->pcg_pbytes += it * p->h_ppart[b];

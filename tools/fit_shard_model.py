@@ -33,13 +33,13 @@ def features(m, ml, n_ref, K, it):
     hm = 384 if kp >= 4096 else 768
     Tb = np.ceil(m / 128)
     nc = np.where((K > 1) & (ml > 0), K, 1)
-    fused = (nc == 1) & (Tb <= FTB)
+    fused = Tb <= FTB
     Q = np.ceil(m / 64)
     ops = n_ref * m * (m + 1.0)
     return dict(
         unpack=float((m * (math.ceil(n_ref / 4) + kp / 4)).sum()),
         gram_huge=float(ops[m >= hm].sum()), gram_big=float(ops[m < hm].sum()), kp=kp,
-        fq=float((it * Q * (Q + 1) / 2)[fused].sum()),
+        fq=float((nc * it * Q * (Q + 1) / 2)[fused].sum()),
         ct=float((it * Tb * (Tb + 1) / 2 * (1 + 0.5 * (nc - 1)))[~fused].sum()),
         cr=float((it * Tb * nc)[~fused].sum()),
         citmax=float(it[~fused].max()) if (~fused).any() else 0.0,
