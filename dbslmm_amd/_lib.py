@@ -24,7 +24,7 @@ EXPORTS = (
     "dbslmm_plan_block_iters",
 )
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 K_UNPACK, K_GRAM, K_CHOL_LARGE, K_CHOL_SMALL, K_CHOL_TILED, K_TRSV, K_PCG, K_PCG_BLOCK = 0, 1, 2, 3, 4, 5, 6, 7
 KERNEL_NAMES = ("dbslmm_unpack_stats", "dbslmm_gram", "dbslmm_chol_large", "dbslmm_chol_small",
                 "dbslmm_tchol", "dbslmm_trsv", "dbslmm_pcg", "dbslmm_pcg_block")
@@ -42,6 +42,7 @@ class Options(C.Structure):
         ("debug_stop", C.c_int32), ("sub_split", C.c_int32), ("sub_grid_lead", C.c_int32),
         ("sub_grid_rest", C.c_int32), ("shard_copies", C.c_int32), ("h2f_iter", C.c_int32),
         ("solver", C.c_int32), ("pcg_tol", C.c_double), ("pcg_maxit", C.c_int32),
+        ("pcg_whole", C.c_int32),
     ]
 
 

@@ -312,12 +312,14 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     const int64_t ld16 = static_cast<int64_t>(B.Tb) * kT;
     const int rg = lane >> 3, cg = lane & 7;
     auto vj_of = [&](int J) -> double* { return J == I ? vI : vJb + ((J - J0) & 1) * nc * kVS; };
-    auto load = [&](int J, int q, pcg_u4 (&raw)[8]) {
+    auto load = [&](int J, int q, pcg_u4 (&raw)[8]) {   // (sub-blocks wholly above the diagonal or past m: zeros)
         if constexpr (U16) {
-            const int i0 = I * kT + 64 * (q >> 1), j0 = J * kT + 64 * (q & 1);
-            const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(i0 + 8 * rg) * ld16 + j0 + 8 * cg;
+            const int i0 = I * kT + 64 * (q >> 1) + 8 * rg, j0 = J * kT + 64 * (q & 1) + 8 * cg;
+            const bool skip = j0 >= B.m || (J == I && (q == 0 || q == 3) && cg > rg);
+            const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(i0) * ld16 + j0;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) raw[r] = *reinterpret_cast<const pcg_u4*>(q16 + r * ld16);
+            for (int r = 0; r < 8; ++r)
+                raw[r] = (skip || i0 + r >= B.m) ? pcg_u4{0u, 0u, 0u, 0u} : *reinterpret_cast<const pcg_u4*>(q16 + r * ld16);
         }
     };
     auto mult = [&](int J, int q, const pcg_u4 (&raw)[8]) {
@@ -742,6 +744,9 @@ extern "C" __global__ __launch_bounds__(pcg::kThreads) void dbslmm_pcg_update(Pc
 // vectors at the end).  The chip-wide kernels skip these blocks (init marks them
 // done = 3); dbslmm_pcg_final writes their betas and status from x and cnv as for the others.
 // ------------------------------------------------------------------------------------------
+#ifndef PCG_BLOCK_DEPTH
+#define PCG_BLOCK_DEPTH 3   // quadrant buffers per wave in dbslmm_pcg_block (2: one in flight)
+#endif
 namespace pcg {
 // sum of v over the workgroup, every thread gets the total (fixed order: lanes, then waves 0..3)
 template <int N>
@@ -813,12 +818,15 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
         while ((qi + 1) * (qi + 2) / 2 <= t) ++qi;
         qj = t - qi * (qi + 1) / 2;
     };
-    auto load = [&](int t, pcg_u4 (&raw)[8]) {
+    auto load = [&](int t, pcg_u4 (&raw)[8]) {   // (sub-blocks wholly above the diagonal or past m: zeros, not read)
         int qi, qj;
         quad_of(t, qi, qj);
-        const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(64 * qi + 8 * rg) * ld16 + 64 * qj + 8 * cg;
+        const int r0 = 64 * qi + 8 * rg, c0 = 64 * qj + 8 * cg;
+        const bool skip = c0 >= m || (qi == qj && cg > rg);
+        const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(r0) * ld16 + c0;
 #pragma unroll
-        for (int rr = 0; rr < 8; ++rr) raw[rr] = *reinterpret_cast<const pcg_u4*>(q16 + rr * ld16);
+        for (int rr = 0; rr < 8; ++rr)
+            raw[rr] = (skip || r0 + rr >= m) ? pcg_u4{0u, 0u, 0u, 0u} : *reinterpret_cast<const pcg_u4*>(q16 + rr * ld16);
     };
     auto mult = [&](int t, const pcg_u4 (&raw)[8]) {
         int qi, qj;
@@ -874,6 +882,26 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
         // ---- product y = G U (U in LDS since the last update)
         __syncthreads();
         {
+#if PCG_BLOCK_DEPTH == 3
+            // two quadrants in flight while one is multiplied (three register buffers, rotated)
+            pcg_u4 ra[8], rb[8], rc[8];
+            int t = wave;
+            if (t < nq) load(t, ra);
+            if (t + 4 < nq) load(t + 4, rb);
+            while (t < nq) {
+                if (t + 8 < nq) load(t + 8, rc);
+                mult(t, ra);
+                t += 4;
+                if (t >= nq) break;
+                if (t + 8 < nq) load(t + 8, ra);
+                mult(t, rb);
+                t += 4;
+                if (t >= nq) break;
+                if (t + 8 < nq) load(t + 8, rb);
+                mult(t, rc);
+                t += 4;
+            }
+#else
             pcg_u4 ra[8], rb[8];
             int t = wave;
             if (t < nq) load(t, ra);
@@ -888,6 +916,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
                 mult(t, rb);
                 t = tn2;
             }
+#endif
         }
         __syncthreads();
         // ---- w = M u, dots r.u, w.u, r.r and x.x per copy (dbslmm_pcg_rows)
@@ -1015,10 +1044,14 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
     if (tid == 0) atomicMax(a.itb + bi, it + (it < maxit ? 1 : 0));   // (several copies: the slowest)
 }
 
-#ifndef PCG_BLOCK_WAVES
-#define PCG_BLOCK_WAVES 2   // waves per SIMD dbslmm_pcg_block is compiled for (3: 94 VGPRs spilled)
+extern "C" __global__ __launch_bounds__(pcg::kThreads)
+#if PCG_BLOCK_DEPTH == 3
+// one wave per SIMD (its LDS allows one workgroup per CU); at most 312 VGPRs, so a chip-wide
+// product wave (192) still fits beside it on every SIMD
+__attribute__((amdgpu_waves_per_eu(1, 8), amdgpu_num_vgpr(312)))
+#else
+__attribute__((amdgpu_waves_per_eu(2, 8)))
 #endif
-extern "C" __global__ __launch_bounds__(pcg::kThreads) __attribute__((amdgpu_waves_per_eu(PCG_BLOCK_WAVES, 8)))
 void dbslmm_pcg_block(PcgArgs a, const int2* __restrict__ list, int32_t n_list, int32_t* __restrict__ next,
                       int32_t maxit) {
     // blocks taken in list order (biggest first) by whichever workgroup is free: the next index from

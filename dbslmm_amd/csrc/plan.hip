@@ -448,6 +448,18 @@ static hipError_t upload_staged(void* dst, const void* src, size_t n, hipStream_
 // buffers): the caller's pages of the file are never faulted in, so neither the copy nor the
 // process's exit pays for hundreds of thousands of page-table entries.
 static hipError_t upload_staged_fd(void* dst, int fd, size_t n, hipStream_t st) {
+    if (n <= (size_t(32) << 20)) {   // small images (the reference's example: 72 KB): one read and one
+                                     // pageable copy -- pinning the staging buffers would cost ~20 ms
+        std::vector<char> h(n);
+        size_t got = 0;
+        while (got < n) {
+            const ssize_t r = pread(fd, h.data() + got, n - got, static_cast<off_t>(got));
+            if (r <= 0) return hipErrorInvalidValue;
+            got += static_cast<size_t>(r);
+        }
+        const hipError_t e = hipMemcpyAsync(dst, h.data(), n, hipMemcpyHostToDevice, st);
+        return e != hipSuccess ? e : hipStreamSynchronize(st);
+    }
     return upload_pipelined(dst, n, st, [fd](char* d, size_t off, size_t len) {
         size_t got = 0;
         while (got < len) {
@@ -936,7 +948,7 @@ int dbslmm_plan_create(dbslmm_ctx* ctx, const dbslmm_problem* pr, dbslmm_plan** 
                    op.shard_copies <= 64 && op.h2f_iter >= 0 && op.h2f_iter <= 2 && op.solver >= 0 &&
                    op.solver <= 2 && op.pcg_tol >= 0.0 && op.pcg_maxit >= 0, "bad dbslmm_options");
     p->solver = op.solver;
-    if (const char* e = std::getenv("DBSLMM_PCG_FUSED")) p->pcg_fused = std::atoi(e) != 0;   // (A/B)
+    p->pcg_fused = op.pcg_whole >= 0;
     if (op.pcg_tol > 0.0) p->pcg_tol = std::max(1e-15, op.pcg_tol);
     if (op.pcg_maxit > 0) p->pcg_maxit = op.pcg_maxit;
     p->pcg_g16 = 4 * static_cast<int64_t>(pr->n_ref) <= 65535;
@@ -2054,7 +2066,6 @@ static int pcg_layout(dbslmm_plan* p, int n) {
     // at 1 / 2 / 4 / 8, and the N = 8 shards' product 114 -> ~45 us: many short items keep more
     // row segments in flight than a few long ones)
     int run = 1;
-    if (const char* e = std::getenv("DBSLMM_PCG_RUN")) run = std::clamp(std::atoi(e), 1, static_cast<int>(kRunMax));   // (A/B)
     p->pcg_run = run;
     for (int b = 0; b < p->n_nonempty; ++b) {
         const int32_t m = p->h_m[b], Tb = (m + kT - 1) / kT, nrun = (Tb + run - 1) / run;
@@ -2352,6 +2363,7 @@ static int run_pcg(dbslmm_plan* p, const double* sigmas, int n) {
         if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], ctx->stream2));   // dbslmm_pcg_block's span: 3 -> 4
         // one workgroup per CU (its LDS holds x and p: one fits): the chip-wide kernels of the
         // other blocks keep the rest of every CU
+        // (two per CU at one copy, where their LDS fits: configs 3 / 5 6.02 -> 6.27 / 2.35 -> 2.51 ms)
         const int grid = std::max(1, std::min(p->n_pflist, ctx->n_cu));
         HIP_TRY(ctx, hipMemsetAsync(p->d_pfnext, 0, 16, ctx->stream2));
         hipLaunchKernelGGL(dbslmm_pcg_block, dim3(grid), dim3(pcg::kThreads), pcg::block_lds_bytes(n), ctx->stream2, a,

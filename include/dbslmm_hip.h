@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSLMM_ABI_VERSION 14
+#define DBSLMM_ABI_VERSION 15
 
 enum {
     DBSLMM_OK = 0,
@@ -138,6 +138,10 @@ typedef struct dbslmm_plan dbslmm_plan;
  *                above its bound there is reported DBSLMM_BLOCK_NOT_CONVERGED with its iterate.
  *                Also lowers the cap of the factorisation route's h2f CG (h2f_iter 2) below its
  *                default, the Chebyshev count.
+ * pcg_whole      PCG (ABI 15): blocks of at most 8 tile rows (1024 SNPs) on the uint16 Gram are
+ *                solved whole by one workgroup per Krylov sequence (dbslmm_pcg_block) beside the
+ *                chip-wide iterations of the others; 0 = default (on), -1 = off (every block on
+ *                the chip-wide kernels: A/B and parity tests).  Results agree within pcg_tol.
  */
 typedef struct dbslmm_options {
     int32_t tiled_min;
@@ -158,6 +162,7 @@ typedef struct dbslmm_options {
     int32_t solver;
     double pcg_tol;
     int32_t pcg_maxit;
+    int32_t pcg_whole;
 } dbslmm_options;
 
 /* One LD-block problem set, the arguments of DBSLMMFIT::est in flat form.

@@ -183,9 +183,9 @@ def test_large_panel_fp64_sigma_path():
 
 
 @pytest.mark.parametrize("factors", [(1.0,), (0.8, 1.0, 1.2)])
-def test_whole_block_kernel_matches_chip_path(monkeypatch, factors):
+def test_whole_block_kernel_matches_chip_path(factors):
     """dbslmm_pcg_block (blocks of one product column and <= 8 tile rows solved whole by one
-    workgroup) against the chip-wide kernels on the same plan inputs (DBSLMM_PCG_FUSED=0): every
+    workgroup) against the chip-wide kernels on the same plan inputs (pcg_whole = -1): every
     copy within the stopping bound of each other and 1e-10 of the oracle; statuses and the
     monomorphic block as there; repeated runs bit-identical."""
     prob = _problem(seed=11, n_ref=512, sizes=[60, 200, 700, 1100, 130], mono_block=4, miss_rate=0.0)
@@ -195,8 +195,9 @@ def test_whole_block_kernel_matches_chip_path(monkeypatch, factors):
     fz2, _ = _run(prob, sig)
     for x, y in zip(fz, fz2):
         assert all(np.array_equal(u, v, equal_nan=True) for u, v in zip(x, y))
-    monkeypatch.setenv("DBSLMM_PCG_FUSED", "0")
+    prob.opts["pcg_whole"] = -1
     ch, wlc = _run(prob, sig)
+    prob.opts.pop("pcg_whole")
     assert wl["pcg_route"] == 1 and wlc["pcg_route"] == 1
     for c in range(len(sig)):
         np.testing.assert_array_equal(fz[c][2], ch[c][2])
