@@ -229,24 +229,26 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
 
 // ---------------------------------------------------------------- time model, PCG route
 // On the PCG route (pcg.hip) a device runs one sequence: unpack + Gram of its blocks, then two
-// concurrent paths -- dbslmm_pcg_block solving its blocks of <= 8 tile rows whole (cost per
-// quadrant, iteration and sequence) and the chip-wide iterations of the others (per tile and per tile row
-// and copy column, plus a floor per iteration: three dependent launches) -- then the result
-// download.  No block needs splitting: the largest (9.7k SNPs) is ~1 ms of work.  Rates fitted to
-// the round-6 one-GPU rehearsals of configs 3-5 at N = 1, 2, 4, 8 (45 devices:
-// two rehearsals on two boxes, tools/fit_shard_model.py; config 4 devices within 14 % (mean 5 %),
-// config 5 18 % (5 %), config 3 20 % (12 %) -- the rehearsals themselves differ by up to 12 % box to
-// box), iteration counts a priori (pcg_iters_model), DESIGN.md section 6.
-constexpr double kPcgUnpackMs0 = 0.0172, kPcgUnpackBps = 4.70e12;     // dwordx4 unpack
-constexpr double kPcgGramMs0 = 0.0753;                               // Gram launches
-constexpr double kPcgGramOpsHuge = 3.10e15, kPcgGramOpsBig = 1.50e15;   // 256- / 128-tile kernels
-constexpr double kPcgFusedQuadNs = 2.39;     // dbslmm_pcg_block: per 64 x 64 quadrant and iteration
-constexpr double kPcgTileNs = 5.76;          // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
-constexpr double kPcgRowNs = 43.6;           // rows + update: per tile row, copy column and iteration
-constexpr double kPcgIterFloorUs = 32.9;     // per chip-wide iteration (launch chain)
-constexpr double kPcgShare = 0.69;           // both paths at once: 0.66 of their summed times
-constexpr double kPcgRunMs = 0.127;          // per run: memsets, init, final, read-back, host
-constexpr double kPcgDownloadMsPerM = 0.809; // per million (SNP, copy) results downloaded + scattered
+// concurrent paths -- dbslmm_pcg_block solving its blocks of <= 8 tile rows whole (one workgroup per
+// Krylov sequence: its time is the larger of the chip's throughput over all of them, the longest
+// sequence on one CU, and the sequences packed onto the CUs) and the chip-wide iterations of the
+// others (per tile and per tile row and copy column, plus a floor per iteration: three dependent
+// launches) -- then the result download.  No block needs splitting: the largest (9.7k SNPs) is
+// ~1 ms of work.  Rates fitted to the round-6 one-GPU rehearsals of configs 3-5 at N = 1, 2, 4, 8
+// (tools/fit_shard_model2.py, the model's own structure; 45 devices), iteration counts a priori
+// (pcg_iters_model), DESIGN.md section 6.
+constexpr double kPcgUnpackMs0 = 0.0155, kPcgUnpackBps = 4.755e12;    // dwordx4 unpack
+constexpr double kPcgGramMs0 = 0.0756;                               // Gram launches
+constexpr double kPcgGramOpsHuge = 3.160e15, kPcgGramOpsBig = 1.529e15;   // 256- / 128-tile kernels
+constexpr double kPcgFusedQuadNs = 1.745;    // dbslmm_pcg_block, chip throughput: per 64 x 64 quadrant and iteration
+constexpr double kPcgSeqQuadUs = 0.2982;     // ... one sequence on its CU: per quadrant and iteration
+constexpr double kPcgCUs = 256.0;            // (the sequences packed onto the CUs)
+constexpr double kPcgTileNs = 12.28;         // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
+constexpr double kPcgRowNs = 1.0;            // rows + update: per tile row, copy column and iteration
+constexpr double kPcgIterFloorUs = 22.85;    // per chip-wide iteration (launch chain)
+constexpr double kPcgShare = 0.706;          // both paths at once: this share of their summed times
+constexpr double kPcgRunMs = 0.0679;         // per run: memsets, init, final, read-back, host
+constexpr double kPcgDownloadMsPerM = 0.912; // per million (SNP, copy) results downloaded + scattered
 constexpr int kPcgFusedTb = 8;               // pcg::kFTb
 
 // a priori iterations of a block at relative tolerance tol: CG's bound at kappa = 1 + 10 /
@@ -260,18 +262,20 @@ static int pcg_iters_model(double dmin, double tau, double tol, bool large) {
 
 // a device's PCG-route work, accumulated block by block
 struct PcgDev {
-    double front = 0.0, fused = 0.0, chip = 0.0, results = 0.0;
+    double front = 0.0, fq = 0.0, seq_max = 0.0, chip = 0.0, results = 0.0;   // fq: quadrant-iterations
     int chip_iters = 0;
     double time() const {
         if (front == 0.0 && results == 0.0) return 0.0;
+        const double fused = std::max({fq * kPcgFusedQuadNs * 1e-6, seq_max * kPcgSeqQuadUs * 1e-3,
+                                       fq * kPcgSeqQuadUs * 1e-3 / kPcgCUs});
         const double p = std::max({chip, fused, kPcgShare * (chip + fused)}) + chip_iters * kPcgIterFloorUs * 1e-3;
         return kPcgUnpackMs0 + kPcgGramMs0 + front + p + kPcgRunMs + kPcgDownloadMsPerM * results * 1e-6;
     }
 };
 struct PcgCost {
-    double front = 0.0, fused = 0.0, chip = 0.0, results = 0.0;
+    double front = 0.0, fq = 0.0, seq = 0.0, chip = 0.0, results = 0.0;   // seq: one sequence's quadrant-iterations
     int chip_iters = 0;
-    double ms() const { return front + fused + chip; }   // (the ordering key)
+    double ms() const { return front + fq * kPcgFusedQuadNs * 1e-6 + chip; }   // (the ordering key)
 };
 static PcgCost pcg_block_cost(double m, double ml, double n_ref, int copies, int iters) {
     PcgCost c;
@@ -283,7 +287,8 @@ static PcgCost pcg_block_cost(double m, double ml, double n_ref, int copies, int
     const double Tb = std::ceil(m / 128.0), Q = std::ceil(m / 64.0);
     const int nc = (copies > 1 && ml > 0) ? copies : 1;   // multi-shift: one column without large SNPs
     if (Tb <= kPcgFusedTb) {   // one sequence per product column, each its own workgroup
-        c.fused = nc * iters * Q * (Q + 1.0) / 2.0 * kPcgFusedQuadNs * 1e-6;
+        c.seq = iters * Q * (Q + 1.0) / 2.0;
+        c.fq = nc * c.seq;
     } else {
         c.chip = iters * (Tb * (Tb + 1.0) / 2.0 * (1.0 + 0.5 * (nc - 1)) * kPcgTileNs + Tb * nc * kPcgRowNs) * 1e-6;
         c.chip_iters = iters;
@@ -308,7 +313,8 @@ static void plan_units_pcg(int32_t nb, const int32_t* m, const int32_t* ml, int3
     std::vector<PcgDev> dev(G);
     auto with = [&](PcgDev d, const PcgCost& c) {
         d.front += c.front;
-        d.fused += c.fused;
+        d.fq += c.fq;
+        d.seq_max = std::max(d.seq_max, c.seq);
         d.chip += c.chip;
         d.results += c.results;
         d.chip_iters = std::max(d.chip_iters, c.chip_iters);

@@ -193,6 +193,20 @@ __device__ __forceinline__ double cvt_hi(uint32_t w) {
 
 typedef uint32_t pcg_u4 __attribute__((ext_vector_type(4)));
 
+// A range-checked buffer descriptor over `bytes` of the integer Gram from `base` (wave-uniform: its
+// inputs go through readfirstlane, as 32-bit unsigned halves -- readfirstlane returns int, and a
+// low half >= 2^31 widened as int would set the high word).  A load at an offset >= bytes returns
+// zeros and touches no memory.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t g16_rsrc(const uint16_t* base, uint32_t bytes) {
+    const uint64_t gb = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(gb & 0xffffffffu)));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(gb >> 32)));
+    const int nb = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo),
+                                             static_cast<short>(0), nb, 0x00020000);
+}
+constexpr uint32_t kG16Oob = 0x80000000u;   // (an offset beyond any descriptor's range)
+
 // One 64 x 64 quadrant of a tile: lane (rg = lane >> 3, cg = lane & 7) holds rows 8 rg .. + 7,
 // columns 8 cg .. + 7 as 8 x 8 uint16 (raw: four dwords per row; on a diagonal quadrant the row
 // sums take j <= i, the column sums j < i).  Per copy k: row sums (G v_J) reduce-scatter over cg
@@ -312,14 +326,21 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     const int64_t ld16 = static_cast<int64_t>(B.Tb) * kT;
     const int rg = lane >> 3, cg = lane & 7;
     auto vj_of = [&](int J) -> double* { return J == I ? vI : vJb + ((J - J0) & 1) * nc * kVS; };
-    auto load = [&](int J, int q, pcg_u4 (&raw)[8]) {   // (sub-blocks wholly above the diagonal or past m: zeros)
+    // tile row I of the Gram through a range-checked buffer descriptor (wave-uniform: one item per
+    // wave): sub-block rows wholly above the diagonal or past m, and the quadrant after the item's
+    // last (none), read beyond the range -- zeros, no memory access -- so every load() issues its 8
+    // loads unconditionally and the wait before a quadrant's product counts only its own loads
+    const __amdgpu_buffer_rsrc_t g16 =
+        g16_rsrc(a.G16 + B.off16 + static_cast<int64_t>(I) * kT * ld16, U16 ? static_cast<uint32_t>(kT * ld16 * 2) : 0u);
+    auto load = [&](int J, int q, pcg_u4 (&raw)[8], bool none) {
         if constexpr (U16) {
-            const int i0 = I * kT + 64 * (q >> 1) + 8 * rg, j0 = J * kT + 64 * (q & 1) + 8 * cg;
-            const bool skip = j0 >= B.m || (J == I && (q == 0 || q == 3) && cg > rg);
-            const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(i0) * ld16 + j0;
+            const int i0 = 64 * (q >> 1) + 8 * rg, j0 = J * kT + 64 * (q & 1) + 8 * cg;   // (i0 within the tile row)
+            const bool skip = none || j0 >= B.m || (J == I && (q == 0 || q == 3) && cg > rg);
+            const uint32_t o = static_cast<uint32_t>((static_cast<int64_t>(i0) * ld16 + j0) * 2);
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-                raw[r] = (skip || i0 + r >= B.m) ? pcg_u4{0u, 0u, 0u, 0u} : *reinterpret_cast<const pcg_u4*>(q16 + r * ld16);
+                raw[r] = __builtin_amdgcn_raw_buffer_load_b128(
+                    g16, (skip || I * kT + i0 + r >= B.m) ? kG16Oob : o + static_cast<uint32_t>(r * ld16 * 2), 0, 0);
         }
     };
     auto mult = [&](int J, int q, const pcg_u4 (&raw)[8]) {
@@ -346,7 +367,7 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     };
     pcg_u4 ra[8], rb[8];
     int J = J0, q = 0;                       // quadrant 0 of a tile of the run is always active
-    load(J, q, ra);
+    load(J, q, ra, false);
     stage_v(a, B, I, nc, lane, vI);
     if (J != I) stage_v(a, B, J, nc, lane, vj_of(J));
     for (int t = 0; t < 2 * nc; ++t) rsum[t * 64 + lane] = csum[t * 64 + lane] = 0.0;
@@ -357,10 +378,8 @@ __device__ void symv_item(const PcgArgs& a, int4 item, int lane, double* vI, dou
     auto step = [&](pcg_u4 (&cur)[8], pcg_u4 (&nxt)[8]) -> bool {
         int Jn = J, qn = q;
         const bool more = next_quad(B, I, J1, Jn, qn);
-        if (more) {
-            load(Jn, qn, nxt);
-            if (Jn != J && Jn != I) stage_v(a, B, Jn, nc, lane, vj_of(Jn));
-        }
+        load(more ? Jn : J, more ? qn : q, nxt, !more);        // (issued either way: counted waits)
+        if (more && Jn != J && Jn != I) stage_v(a, B, Jn, nc, lane, vj_of(Jn));
         mult(J, q, cur);
         if (!more || Jn != J) flush(J);
         wave_fence();                        // the next column vector is in LDS before its use
@@ -789,17 +808,20 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
     const int nx = msh ? n : 1;              // copies of x this sequence yields
     const double dc = msh ? col_shift(a, B, 0) : a.dshift[cc];   // the sequence's shift (the seed's: multi-shift)
     // ---- state: x = p = 0, r = z, s = w = 0, U = rsd o r / diag
-    double r[kFPer], sv[kFPer], wv[kFPer], sg[1] = {0.0};
+    // (S and rsd of the thread's slots in registers: no global reads inside the iterations)
+    double r[kFPer], sv[kFPer], wv[kFPer], Sr[kFPer], Rr[kFPer], sg[1] = {0.0};
 #pragma unroll
     for (int q = 0; q < kFPer; ++q) {
         const int i = tid + kThreads * q;
         const bool in = i < m;
         r[q] = in ? a.z[B.row0 + i] : 0.0;
+        Sr[q] = in ? a.S[B.row0 + i] : 0.0;
+        Rr[q] = in ? a.rsd[B.row0 + i] : 0.0;
         sv[q] = wv[q] = 0.0;
         double u = 0.0;
         if (in) {
-            u = (r[q] / jdiag(a, B, i, dc)) * a.rsd[B.row0 + i];
-            sg[0] += a.S[B.row0 + i] * u;
+            u = (r[q] / jdiag(a, B, i, dc)) * Rr[q];
+            sg[0] += Sr[q] * u;
         }
         Ul[i] = u;                           // (zero past m)
         for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;
@@ -818,15 +840,22 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
         while ((qi + 1) * (qi + 2) / 2 <= t) ++qi;
         qj = t - qi * (qi + 1) / 2;
     };
-    auto load = [&](int t, pcg_u4 (&raw)[8]) {   // (sub-blocks wholly above the diagonal or past m: zeros, not read)
+    // The block's Gram through a range-checked buffer descriptor: a sub-block row wholly above the
+    // diagonal or past m, and every quadrant past the last (t >= nq), reads at an offset beyond the
+    // range -- zeros with no memory access -- so each load() issues exactly 8 loads unconditionally
+    // and the waits before mult() count only the quadrant they need (with the loads under branches
+    // the compiler waited for all of them, vmcnt(0): one quadrant in flight, 16.5 GB/s per CU).
+    const __amdgpu_buffer_rsrc_t g16 = g16_rsrc(a.G16 + B.off16, static_cast<uint32_t>(ld16 * ld16 * 2));
+    auto load = [&](int t, pcg_u4 (&raw)[8]) {
         int qi, qj;
         quad_of(t, qi, qj);
         const int r0 = 64 * qi + 8 * rg, c0 = 64 * qj + 8 * cg;
-        const bool skip = c0 >= m || (qi == qj && cg > rg);
-        const uint16_t* q16 = a.G16 + B.off16 + static_cast<int64_t>(r0) * ld16 + c0;
+        const bool skip = t >= nq || c0 >= m || (qi == qj && cg > rg);
+        const uint32_t o = static_cast<uint32_t>((r0 * static_cast<int>(ld16) + c0) * 2);
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr)
-            raw[rr] = (skip || r0 + rr >= m) ? pcg_u4{0u, 0u, 0u, 0u} : *reinterpret_cast<const pcg_u4*>(q16 + rr * ld16);
+            raw[rr] = __builtin_amdgcn_raw_buffer_load_b128(
+                g16, (skip || r0 + rr >= m) ? kG16Oob : o + static_cast<uint32_t>(rr * ld16 * 2), 0, 0);
     };
     auto mult = [&](int t, const pcg_u4 (&raw)[8]) {
         int qi, qj;
@@ -884,37 +913,36 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
         {
 #if PCG_BLOCK_DEPTH == 3
             // two quadrants in flight while one is multiplied (three register buffers, rotated)
+            // (loads past the last quadrant are out of range: issued, no memory access)
             pcg_u4 ra[8], rb[8], rc[8];
             int t = wave;
-            if (t < nq) load(t, ra);
-            if (t + 4 < nq) load(t + 4, rb);
+            load(t, ra);
+            load(t + 4, rb);
             while (t < nq) {
-                if (t + 8 < nq) load(t + 8, rc);
+                load(t + 8, rc);
                 mult(t, ra);
                 t += 4;
                 if (t >= nq) break;
-                if (t + 8 < nq) load(t + 8, ra);
+                load(t + 8, ra);
                 mult(t, rb);
                 t += 4;
                 if (t >= nq) break;
-                if (t + 8 < nq) load(t + 8, rb);
+                load(t + 8, rb);
                 mult(t, rc);
                 t += 4;
             }
 #else
             pcg_u4 ra[8], rb[8];
             int t = wave;
-            if (t < nq) load(t, ra);
+            load(t, ra);
             while (t < nq) {
-                const int tn = t + 4;
-                if (tn < nq) load(tn, rb);
+                load(t + 4, rb);
                 mult(t, ra);
-                t = tn;
+                t += 4;
                 if (t >= nq) break;
-                const int tn2 = t + 4;
-                if (tn2 < nq) load(tn2, ra);
+                load(t + 4, ra);
                 mult(t, rb);
-                t = tn2;
+                t += 4;
             }
 #endif
         }
@@ -933,7 +961,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
                 for (int w = 0; w < 4; ++w) yw[w * kFRows + i] = 0.0;
             }
             if (i < m) {
-                const double Si = a.S[B.row0 + i], ri = a.rsd[B.row0 + i];
+                const double Si = Sr[q], ri = Rr[q];
                 const double u = r[q] / jdiag(a, B, i, dc);
                 const double sh = i < B.ms ? dc : 0.0;
                 const double w = a.tau * a.rn * ri * __builtin_fma(-Si, sig * a.rn, y) + (1.0 - a.tau + sh) * u;
@@ -1002,7 +1030,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
         for (int q = 0; q < kFPer; ++q) {
             const int i = tid + kThreads * q;
             if (i >= m) continue;
-            const double rsd_i = a.rsd[B.row0 + i];
+            const double rsd_i = Rr[q];
             double rn;
             if (msh) {
                 for (int c = 0; c < n; ++c) {
@@ -1029,7 +1057,7 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
                 r[q] = rn;
                 Ul[i] = (rn / dg) * rsd_i;
             }
-            sg2[0] += a.S[B.row0 + i] * Ul[i];
+            sg2[0] += Sr[q] * Ul[i];
         }
         block_sum(sg2, red, tid);
         sig = sg2[0];

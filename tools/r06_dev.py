@@ -39,7 +39,7 @@ def main(out, cfg=4, ns=(1, 2, 4, 8), only=None):
                 plan.run_multi(sig, out=o)
             plan.enable_timing(True)
             batches = []
-            for _ in range(3):                    # the median of three batches of five solves
+            for _ in range(7):                    # the median of seven batches of five solves (host noise)
                 t0 = time.perf_counter()
                 for _ in range(5):
                     plan.run_multi(sig, out=o)
