@@ -122,30 +122,82 @@ __device__ __forceinline__ void wave_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Reduce-scatter of v[0..8) over the 8 lanes that differ in lane bits (x2, x1, x0): the lane
+// v from lane ^ X.  X = 1, 2, 4, 8 stay inside a 16-lane row and move through DPP (VALU, no LDS
+// round trip): xor 1 / 2 as quad permutations, xor 4 as the half-row mirror (lane i <- 7 - i of
+// its eight) then the quad reversal, xor 8 as the row rotation by 8; wider ones go through
+// ds_bpermute (__shfl_xor).
+template <int Ctrl>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b & 0xffffffffu), Ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), Ctrl, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+}
+// xor 16 / 32 through gfx950's row swaps: v_permlane16_swap / v_permlane32_swap of a value with
+// itself leave, in a lane of an odd 16-lane row (upper 32-lane half), its partner's value in the
+// first result and in an even row (lower half) in the second (tools/micro/probe_permlane.hip)
+template <int X>
+__device__ __forceinline__ uint32_t swap_xor(uint32_t x, bool up) {
+    if constexpr (X == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return up ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return up ? r[0] : r[1];
+    }
+}
+template <int X>
+__device__ __forceinline__ double lane_xor(double v) {
+#ifndef PCG_NO_DPP
+    if constexpr (X == 1) return dpp_mov<0xB1>(v);                   // quad_perm [1, 0, 3, 2]
+    else if constexpr (X == 2) return dpp_mov<0x4E>(v);              // quad_perm [2, 3, 0, 1]
+    else if constexpr (X == 4) return dpp_mov<0x1B>(dpp_mov<0x141>(v));   // row_half_mirror, quad_perm [3, 2, 1, 0]
+    else if constexpr (X == 8) return dpp_mov<0x128>(v);             // row_ror:8
+#ifndef PCG_NO_PERMLANE
+    else if constexpr (X == 16 || X == 32) {
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        const bool up = (__lane_id() & X) != 0;
+        const uint32_t lo = swap_xor<X>(static_cast<uint32_t>(b & 0xffffffffu), up);
+        const uint32_t hi = swap_xor<X>(static_cast<uint32_t>(b >> 32), up);
+        return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+    }
+#endif
+    else
+#endif
+        return __shfl_xor(v, X);
+}
+
+// Reduce-scatter of v[0..8) over the 8 lanes that differ in lane bits (X2, X1, X0): the lane
 // whose bits read s = 4 b2 + 2 b1 + b0 returns the sum of v[s] over those lanes (fixed order).
-__device__ __forceinline__ double rscatter8(const double (&v)[8], int lane, int x2, int x1, int x0) {
-    const bool h2 = (lane & x2) != 0, h1 = (lane & x1) != 0, h0 = (lane & x0) != 0;
+template <int X2, int X1, int X0>
+__device__ __forceinline__ double rscatter8(const double (&v)[8], int lane) {
+    const bool h2 = (lane & X2) != 0, h1 = (lane & X1) != 0, h0 = (lane & X0) != 0;
     double u[4], w[2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const double send = h2 ? v[q] : v[q + 4], keep = h2 ? v[q + 4] : v[q];
-        u[q] = keep + __shfl_xor(send, x2);
+        u[q] = keep + lane_xor<X2>(send);
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const double send = h1 ? u[q] : u[q + 2], keep = h1 ? u[q + 2] : u[q];
-        w[q] = keep + __shfl_xor(send, x1);
+        w[q] = keep + lane_xor<X1>(send);
     }
     const double send = h0 ? w[0] : w[1], keep = h0 ? w[1] : w[0];
-    return keep + __shfl_xor(send, x0);
+    return keep + lane_xor<X0>(send);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+__device__ __forceinline__ double wave_sum(double v) {   // (fixed order: xor 32, 16, .., 1)
+    v += lane_xor<32>(v);
+    v += lane_xor<16>(v);
+    v += lane_xor<8>(v);
+    v += lane_xor<4>(v);
+    v += lane_xor<2>(v);
+    v += lane_xor<1>(v);
     return v;
 }
+
+
 
 // sum of p[s * st] over s in [s0, s1) in order, eight loads in flight (a serial chain of dependent
 // loads over a 76-slot tile row cost ~100 us per launch)
@@ -246,8 +298,8 @@ __device__ __forceinline__ void quad_mul16(const pcg_u4 (&raw)[8], bool diagq, i
                     cacc[c] = __builtin_fma(dd < 0 ? g : 0.0, vi[r], cacc[c]);
                 }
         }
-        rsum[k * 64 + lane] += rscatter8(racc, lane, 4, 2, 1);
-        csum[k * 64 + lane] += rscatter8(cacc, lane, 32, 16, 8);
+        rsum[k * 64 + lane] += rscatter8<4, 2, 1>(racc, lane);
+        csum[k * 64 + lane] += rscatter8<32, 16, 8>(cacc, lane);
     }
 }
 
@@ -279,8 +331,8 @@ __device__ __forceinline__ void quad_mul64(const double* __restrict__ base, int6
                     if (q == r) racc[q] = __builtin_fma(gr, vj[c], racc[q]);
                 cacc[c] = __builtin_fma(gc, vi[r], cacc[c]);
             }
-        rsum[k * 64 + lane] += rscatter8(racc, lane, 4, 2, 1);
-        csum[k * 64 + lane] += rscatter8(cacc, lane, 32, 16, 8);
+        rsum[k * 64 + lane] += rscatter8<4, 2, 1>(racc, lane);
+        csum[k * 64 + lane] += rscatter8<32, 16, 8>(cacc, lane);
     }
 }
 
@@ -892,9 +944,9 @@ __device__ __forceinline__ void pcg_block_solve(const PcgArgs& a, int bi, int cc
         }
         double* y = yw + wave * kFRows;
         const int ri = 64 * qi + 8 * rg + cg, ci = 64 * qj + 8 * cg + rg;
-        y[ri] += rscatter8(racc, lane, 4, 2, 1);
+        y[ri] += rscatter8<4, 2, 1>(racc, lane);
         wave_fence();                          // (a diagonal quadrant: the row sums land first)
-        y[ci] += rscatter8(cacc, lane, 32, 16, 8);
+        y[ci] += rscatter8<32, 16, 8>(cacc, lane);
     };
     // recurrence state: thread 0 keeps it in LDS (kept out of the registers of the product loop)
     double* st = red + 4 * (3 + kMaxNC);     // [0] gamma_prev, [1] alpha_prev, [2] alpha, [3] beta,
