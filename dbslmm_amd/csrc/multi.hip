@@ -237,18 +237,18 @@ static void plan_units(int32_t nb, const int32_t* m, int32_t n_ref, int32_t G, i
 // ~1 ms of work.  Rates fitted to the round-6 one-GPU rehearsals of configs 3-5 at N = 1, 2, 4, 8
 // (tools/fit_shard_model2.py, the model's own structure; 45 devices), iteration counts a priori
 // (pcg_iters_model), DESIGN.md section 6.
-constexpr double kPcgUnpackMs0 = 0.0155, kPcgUnpackBps = 4.755e12;    // dwordx4 unpack
-constexpr double kPcgGramMs0 = 0.0756;                               // Gram launches
-constexpr double kPcgGramOpsHuge = 3.160e15, kPcgGramOpsBig = 1.529e15;   // 256- / 128-tile kernels
-constexpr double kPcgFusedQuadNs = 1.745;    // dbslmm_pcg_block, chip throughput: per 64 x 64 quadrant and iteration
-constexpr double kPcgSeqQuadUs = 0.2982;     // ... one sequence on its CU: per quadrant and iteration
+constexpr double kPcgUnpackMs0 = 0.0102, kPcgUnpackBps = 4.581e12;    // dwordx4 unpack
+constexpr double kPcgGramMs0 = 0.0840;                               // Gram launches
+constexpr double kPcgGramOpsHuge = 3.379e15, kPcgGramOpsBig = 1.508e15;   // 256- / 128-tile kernels
+constexpr double kPcgFusedQuadNs = 1.502;    // dbslmm_pcg_block, chip throughput: per 64 x 64 quadrant and iteration
+constexpr double kPcgSeqQuadUs = 0.2594;     // ... one sequence on its CU: per quadrant and iteration
 constexpr double kPcgCUs = 256.0;            // (the sequences packed onto the CUs)
-constexpr double kPcgTileNs = 12.28;         // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
-constexpr double kPcgRowNs = 1.0;            // rows + update: per tile row, copy column and iteration
-constexpr double kPcgIterFloorUs = 22.85;    // per chip-wide iteration (launch chain)
-constexpr double kPcgShare = 0.706;          // both paths at once: this share of their summed times
-constexpr double kPcgRunMs = 0.0679;         // per run: memsets, init, final, read-back, host
-constexpr double kPcgDownloadMsPerM = 0.912; // per million (SNP, copy) results downloaded + scattered
+constexpr double kPcgTileNs = 12.35;         // chip-wide product: per 128 x 128 tile and iteration (+50 % per extra column)
+constexpr double kPcgRowNs = 1.21;            // rows + update: per tile row, copy column and iteration
+constexpr double kPcgIterFloorUs = 20.37;    // per chip-wide iteration (launch chain)
+constexpr double kPcgShare = 0.741;          // both paths at once: this share of their summed times
+constexpr double kPcgRunMs = 0.0692;         // per run: memsets, init, final, read-back, host
+constexpr double kPcgDownloadMsPerM = 0.753; // per million (SNP, copy) results downloaded + scattered
 constexpr int kPcgFusedTb = 8;               // pcg::kFTb
 
 // a priori iterations of a block at relative tolerance tol: CG's bound at kappa = 1 + 10 /
