@@ -7,9 +7,10 @@ coalesced streaming read (MI355X_MICROARCH.md, HBM section): the read side is do
 Also records launches per kernel and, for the composite phases the bench times as one slot --
 the tiled Cholesky (dbslmm_tchol_* launches plus the persistent backward substitution
 dbslmm_trsv_bwd<1>) and the h2f substitutions (dbslmm_trsv_fwd/bwd<2>) -- the summed
-HBM bytes per run (= per bench step; runs = launches of dbslmm_gram_i8, one per run -- the unpack
-is two launches per run with a lead group) under
-"dbslmm_tchol" and "dbslmm_trsv" (key "hbm_bytes_per_step").
+HBM bytes per run (= per bench step; runs = launches of dbslmm_pcg_init on the PCG route, else of
+dbslmm_gram_i8, one per run -- the unpack is two launches per run with a lead group) under
+"dbslmm_tchol" and "dbslmm_trsv", and likewise the Gram launches under "dbslmm_gram" and the
+chip-wide PCG launches under "dbslmm_pcg" (key "hbm_bytes_per_step").
 """
 import collections
 import csv
@@ -34,8 +35,9 @@ def main(src, dst, bench_args=""):
                      f"`python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline {bench_args}`".rstrip(),
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
            "kernels": {}}
-    runs = f.get("dbslmm_gram_i8", (0, 0))[1]
-    seq = trsv = 0.0
+    # runs: one dbslmm_pcg_init per run on the PCG route, else one dbslmm_gram_i8
+    runs = f.get("dbslmm_pcg_init", (0, 0))[1] or f.get("dbslmm_gram_i8", (0, 0))[1]
+    seq = trsv = gram = pcg = 0.0
     for k in sorted(set(f) | set(w)):
         name = k[5:] if k.startswith("void ") else k
         if not name.startswith("dbslmm_"):
@@ -46,12 +48,22 @@ def main(src, dst, bench_args=""):
             seq += (2 * fk + wk) * 1024.0 * n
         elif name.startswith("dbslmm_trsv_"):
             trsv += (2 * fk + wk) * 1024.0 * n
+        if name.startswith("dbslmm_gram_"):
+            gram += (2 * fk + wk) * 1024.0 * n
+        elif name.startswith("dbslmm_pcg_") and name != "dbslmm_pcg_block":
+            pcg += (2 * fk + wk) * 1024.0 * n
     if runs and seq:
         out["kernels"]["dbslmm_tchol"] = dict(hbm_bytes_per_step=seq / runs, runs=runs,
                                               note="dbslmm_tchol_* + persistent backward, per run")
     if runs and trsv:
         out["kernels"]["dbslmm_trsv"] = dict(hbm_bytes_per_step=trsv / runs, runs=runs,
                                              note="h2f substitutions (CG by default), per run")
+    if runs and gram:
+        out["kernels"]["dbslmm_gram"] = dict(hbm_bytes_per_step=gram / runs, runs=runs,
+                                             note="dbslmm_gram_huge / _big / _i8 launches, per run")
+    if runs and pcg:
+        out["kernels"]["dbslmm_pcg"] = dict(hbm_bytes_per_step=pcg / runs, runs=runs,
+                                            note="chip-wide PCG launches (init, symv, rows, update, final), per run")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
