@@ -210,3 +210,28 @@ def test_whole_block_kernel_matches_chip_path(factors):
     a = _cat(fz[-1])
     ok = np.isfinite(ref) & np.isfinite(a)
     assert normwise(a[ok], ref[ok]) < 1e-10
+
+
+def test_block_sizes_at_the_quadrant_and_whole_block_edges():
+    """Block sizes at the edges the product loads mask (range-checked buffer loads: rows and columns
+    past m, the quadrant after a wave's last) and at the whole-block limit (1024 SNPs = 8 tile rows
+    solved whole; 1025 on the chip-wide path): 1, 63 / 64 / 65 and 1023 / 1024 / 1025 SNPs, large
+    SNPs in every other block, n_ref % 4 = 1, three h2f copies -- every copy within 1e-10 of the
+    oracle's direct solve, and the whole-block kernel within 1e-11 of the chip-wide path."""
+    prob = _problem(seed=23, n_ref=509, sizes=[1, 63, 64, 65, 1023, 1024, 1025, 130], miss_rate=0.0)
+    prob.sigma_s = 0.5 / 1e6
+    factors = (0.8, 1.0, 1.2)
+    sig = [prob.sigma_s * f for f in factors]
+    fz, wl = _run(prob, sig)
+    assert wl["pcg_route"] == 1
+    prob.opts["pcg_whole"] = -1
+    ch, _ = _run(prob, sig)
+    prob.opts.pop("pcg_whole")
+    base = prob.sigma_s
+    for c, s in enumerate(sig):
+        assert np.all(fz[c][2] == 0) and np.all(ch[c][2] == 0)
+        assert normwise(_cat(fz[c]), _cat(ch[c])) < 1e-11, c
+        prob.sigma_s = s
+        ref, _ = _oracle(prob)
+        assert normwise(_cat(fz[c]), ref) < 1e-10, (c, normwise(_cat(fz[c]), ref))
+    prob.sigma_s = base
