@@ -377,10 +377,11 @@ def big_block_check(prob, res, sigmas):
 
 def predict_leg(args, full, sigmas, m_b, ctx):
     """One-GPU rehearsal of the N-GPU strong-scaling step: for each N the
-    library's shard plan (dbslmm_shard_plan) splits the problem into N devices' units; each
-    device's units plan (dbslmm_plan_create_units, exactly what rank d of `torch.distributed.run
-    --nproc-per-node N bench.py` runs) is timed ALONE on this GPU -- 2 warm-up + `k` timed solves,
-    synchronous like the timed step -- and the predicted step is the slowest device (plus the
+    library's shard plan (dbslmm_shard_plan_problem) splits the problem into N devices' units;
+    each device's units plan (dbslmm_plan_create_units, exactly what rank d of
+    `torch.distributed.run --nproc-per-node N bench.py` runs) is timed ALONE on this GPU -- 2
+    warm-up, then the median of five batches of `k` synchronous solves, like the timed step --
+    and the predicted step is the slowest device (plus the
     time model's own prediction beside it).  The RCCL gather of <= 3 x 8 MB over xGMI is not
     included (~0.1 ms)."""
     import numpy as np
@@ -399,18 +400,21 @@ def predict_leg(args, full, sigmas, m_b, ctx):
             o = (np.zeros((K, full.n_s)), np.zeros((K, full.n_l)), np.zeros((K, full.num_block), dtype=np.int32))
             for _ in range(2):
                 plan.run_multi(sig, out=o)
-            t0 = time.perf_counter()
-            for _ in range(k):
-                plan.run_multi(sig, out=o)
-            per.append((time.perf_counter() - t0) / k * 1e3)
+            batches = []
+            for _ in range(5):          # the median of five batches of k (host noise: tools/r06_dev.py)
+                t0 = time.perf_counter()
+                for _ in range(k):
+                    plan.run_multi(sig, out=o)
+                batches.append((time.perf_counter() - t0) / k * 1e3)
+            per.append(float(np.median(batches)))
             plan.close()
         step = max(per)
         out[str(N)] = dict(step_ms=step, value=float(m_b.sum()) / (step * 1e-3), per_device_ms=per,
                            model_ms=model.tolist(),
                            split_blocks=[dict(block=int(b), snps=int(m_b[b]), devices=ud[b].tolist()) for b in split])
     return dict(results=out, unit="SNPs/s", note=(
-        "one-GPU rehearsal: each device's units plan of the N-device shard plan timed alone (2 warm-up + "
-        f"{k} synchronous solves); predicted N-GPU step = the slowest device; value = the problem's SNPs / "
+        "one-GPU rehearsal: each device's units plan of the N-device shard plan timed alone (2 warm-up, "
+        f"the median of 5 batches of {k} synchronous solves); predicted N-GPU step = the slowest device; value = the problem's SNPs / "
         "that step.  Excludes the per-step RCCL gather of the betas to rank 0."))
 
 
